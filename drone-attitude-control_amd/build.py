@@ -1,0 +1,48 @@
+"""Build the in-tree HIP library `lib/libnmpc_hip.so` for gfx950 (MI355X).
+
+Explicit hipcc (no JIT cache, no torch extension): the .so lives in the source tree so it
+travels to the GPU box with the repository snapshot.
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib", "libnmpc_hip.so")
+SOURCES = ["nmpc_ipm.hip", "nmpc_plant.hip", "nmpc_closed_loop.hip", "nmpc_api.cpp"]
+HEADERS = ["nmpc_internal.h", os.path.join("..", "..", "include", "nmpc.h")]
+ARCH = os.environ.get("NMPC_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value",
+         f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
+
+
+def sources():
+    return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def up_to_date():
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    deps = sources() + [os.path.join(CSRC, h) for h in HEADERS] + [__file__]
+    return all(os.path.getmtime(d) <= t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=True):
+    if not force and up_to_date():
+        return LIB
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = ["hipcc", *FLAGS, *sources(), "-o", tmp]
+    if verbose:
+        print("[nmpc build]", " ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print(LIB)

@@ -1,0 +1,885 @@
+// nmpc_api.cpp — C-ABI of the batched NMPC engine (declared in include/nmpc.h).
+//
+// Host side of the drop-in boundary: owns the device buffers of one batched solver handle,
+// turns an acados-style OCP description (AcadosOcp: model / cost / constraints /
+// solver_options, force_model/ocp.py:21-96) into the stage-wise QP data the kernels consume,
+// and stages set/get traffic like acados's ocp_nlp_cost_model_set / ocp_nlp_out_get.
+//
+// "Sensitivity functions": the reference lets CasADi generate the integrator and its
+// forward sensitivities for an affine model (force_model/dynamics.py:32-47 with IRK,
+// jerk_model/dynamics.py:35-52 with ERK-1). For an affine ODE held over one step those
+// sensitivities are constant, so they are computed here once, natively, from the Butcher
+// tableau of the requested integrator (Gauss-Legendre collocation or explicit RK).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nmpc.h"
+#include "nmpc_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+constexpr double kInf = 1e30;
+
+bool has_bound(double b) { return std::fabs(b) < 1e20; }
+
+// ---------------------------------------------------------------- small dense linear algebra
+// solve M X = R in place (M n x n, R n x m), partial pivoting; returns false if singular
+bool gauss_solve(std::vector<double> &M, std::vector<double> &R, int n, int m)
+{
+    for (int col = 0; col < n; col++) {
+        int piv = col;
+        for (int r = col + 1; r < n; r++)
+            if (std::fabs(M[r * n + col]) > std::fabs(M[piv * n + col])) piv = r;
+        if (std::fabs(M[piv * n + col]) < 1e-300) return false;
+        if (piv != col) {
+            for (int j = 0; j < n; j++) std::swap(M[col * n + j], M[piv * n + j]);
+            for (int j = 0; j < m; j++) std::swap(R[col * m + j], R[piv * m + j]);
+        }
+        for (int r = 0; r < n; r++) {
+            if (r == col) continue;
+            const double f = M[r * n + col] / M[col * n + col];
+            if (f == 0.0) continue;
+            for (int j = col; j < n; j++) M[r * n + j] -= f * M[col * n + j];
+            for (int j = 0; j < m; j++) R[r * m + j] -= f * R[col * m + j];
+        }
+    }
+    for (int r = 0; r < n; r++)
+        for (int j = 0; j < m; j++) R[r * m + j] /= M[r * n + r];
+    return true;
+}
+
+// Butcher tableau of the acados integrators used by the reference
+bool butcher(int type, int s, std::vector<double> &a, std::vector<double> &b, std::vector<double> &c)
+{
+    a.assign(s * s, 0.0);
+    b.assign(s, 0.0);
+    c.assign(s, 0.0);
+    if (type == NMPC_ERK) {
+        if (s == 1) {
+            b[0] = 1.0;
+        } else if (s == 2) {  // explicit midpoint
+            a[1 * 2 + 0] = 0.5;
+            c[1] = 0.5;
+            b[1] = 1.0;
+        } else if (s == 4) {  // classic RK4
+            a[1 * 4 + 0] = 0.5;
+            a[2 * 4 + 1] = 0.5;
+            a[3 * 4 + 2] = 1.0;
+            c[1] = c[2] = 0.5;
+            c[3] = 1.0;
+            b[0] = b[3] = 1.0 / 6.0;
+            b[1] = b[2] = 1.0 / 3.0;
+        } else {
+            return false;
+        }
+        return true;
+    }
+    if (type != NMPC_IRK || s < 1 || s > 9) return false;
+    // Gauss-Legendre nodes: roots of P_s(2c-1), Newton on the Legendre recurrence
+    for (int i = 0; i < s; i++) {
+        double x = std::cos(M_PI * (i + 0.75) / (s + 0.5));
+        for (int itn = 0; itn < 100; itn++) {
+            double p0 = 1.0, p1 = x;
+            for (int n = 2; n <= s; n++) {
+                const double p2 = ((2.0 * n - 1.0) * x * p1 - (n - 1.0) * p0) / n;
+                p0 = p1;
+                p1 = p2;
+            }
+            const double pl = s == 1 ? x : p1;
+            const double p_prev = s == 1 ? 1.0 : p0;
+            const double dp = s * (x * pl - p_prev) / (x * x - 1.0);
+            const double dx = pl / dp;
+            x -= dx;
+            if (std::fabs(dx) < 1e-16) break;
+        }
+        c[i] = 0.5 * (1.0 - x);
+    }
+    std::sort(c.begin(), c.end());
+    // collocation conditions: sum_j a_ij c_j^(q-1) = c_i^q / q, sum_j b_j c_j^(q-1) = 1/q
+    std::vector<double> V(s * s), R(s * (s + 1));
+    for (int q = 0; q < s; q++)
+        for (int j = 0; j < s; j++) V[q * s + j] = std::pow(c[j], q);
+    for (int q = 0; q < s; q++) {
+        for (int i = 0; i < s; i++) R[q * (s + 1) + i] = std::pow(c[i], q + 1) / (q + 1);
+        R[q * (s + 1) + s] = 1.0 / (q + 1);
+    }
+    if (!gauss_solve(V, R, s, s + 1)) return false;
+    for (int j = 0; j < s; j++) {
+        for (int i = 0; i < s; i++) a[i * s + j] = R[j * (s + 1) + i];
+        b[j] = R[j * (s + 1) + s];
+    }
+    return true;
+}
+
+// exact discrete map of x' = Ac x + Bc u + cc under one step of the RK scheme, composed
+// over num_steps sub-steps of h/num_steps (forward sensitivities of the integrator)
+bool discretize(int nx, int nu, const double *Ac, const double *Bc, const double *cc, int type, int stages,
+                int steps, double h, std::vector<double> &A, std::vector<double> &B, std::vector<double> &c)
+{
+    std::vector<double> a, bw, cn;
+    if (!butcher(type, stages, a, bw, cn) || steps < 1) return false;
+    const double hs = h / steps;
+    const int s = stages, n = s * nx, m = nx + nu + 1;
+    std::vector<double> M(n * n, 0.0), Rh(n * m, 0.0);
+    for (int i = 0; i < s; i++)
+        for (int r = 0; r < nx; r++) {
+            for (int j = 0; j < s; j++)
+                for (int q = 0; q < nx; q++) M[(i * nx + r) * n + j * nx + q] = -hs * a[i * s + j] * Ac[r * nx + q];
+            M[(i * nx + r) * n + i * nx + r] += 1.0;
+            for (int q = 0; q < nx; q++) Rh[(i * nx + r) * m + q] = Ac[r * nx + q];
+            for (int q = 0; q < nu; q++) Rh[(i * nx + r) * m + nx + q] = Bc[r * nu + q];
+            Rh[(i * nx + r) * m + nx + nu] = cc[r];
+        }
+    if (!gauss_solve(M, Rh, n, m)) return false;
+    // one-step map T = [Phi Gam gam]
+    std::vector<double> T(nx * m, 0.0);
+    for (int r = 0; r < nx; r++) {
+        T[r * m + r] = 1.0;
+        for (int i = 0; i < s; i++)
+            for (int q = 0; q < m; q++) T[r * m + q] += hs * bw[i] * Rh[(i * nx + r) * m + q];
+    }
+    // compose: X_{j+1} = Phi X_j + [0 Gam gam]
+    std::vector<double> Acur(nx * nx), Bcur(nx * nu), ccur(nx);
+    for (int r = 0; r < nx; r++) {
+        for (int q = 0; q < nx; q++) Acur[r * nx + q] = T[r * m + q];
+        for (int q = 0; q < nu; q++) Bcur[r * nu + q] = T[r * m + nx + q];
+        ccur[r] = T[r * m + nx + nu];
+    }
+    for (int st = 1; st < steps; st++) {
+        std::vector<double> An(nx * nx, 0.0), Bn(nx * nu, 0.0), cn2(nx, 0.0);
+        for (int r = 0; r < nx; r++) {
+            for (int q = 0; q < nx; q++)
+                for (int l = 0; l < nx; l++) An[r * nx + q] += T[r * m + l] * Acur[l * nx + q];
+            for (int q = 0; q < nu; q++) {
+                double v = T[r * m + nx + q];
+                for (int l = 0; l < nx; l++) v += T[r * m + l] * Bcur[l * nu + q];
+                Bn[r * nu + q] = v;
+            }
+            double v = T[r * m + nx + nu];
+            for (int l = 0; l < nx; l++) v += T[r * m + l] * ccur[l];
+            cn2[r] = v;
+        }
+        Acur.swap(An);
+        Bcur.swap(Bn);
+        ccur.swap(cn2);
+    }
+    A = Acur;
+    B = Bcur;
+    c = ccur;
+    return true;
+}
+
+hipError_t upload_any(void *dst, const double *src, size_t n, bool f64, hipStream_t s, std::vector<float> &tmp)
+{
+    if (f64) return hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, s);
+    tmp.resize(n);
+    for (size_t i = 0; i < n; i++) tmp[i] = (float)src[i];
+    return hipMemcpyAsync(dst, tmp.data(), n * sizeof(float), hipMemcpyHostToDevice, s);
+}
+
+}  // namespace
+
+struct nmpc_solver {
+    std::string name, err;
+    int device = 0, precision = NMPC_FP64, batch = 0;
+    int nx = 0, nu = 0, N = 0, ny = 0, ny_e = 0;
+    int kidx = -1, ipw = 1, lds = 0, yref_is_z = 0;
+    int max_iter = 50;
+    double tol_comp = 0, tol_res = 0, mu0 = 0, inv_m = 1, ts = 0, scale_e = 1;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.f;
+    // host model (double)
+    std::vector<double> A, B, c, W, Vx, Vu, W_e, Vx_e;
+    std::vector<double> H, G, He, Ge, lbnd, ubnd;
+    // host staging
+    std::vector<double> h_x0, h_lbx0, h_ubx0, h_yref, h_x, h_u;
+    std::vector<int32_t> h_status, h_iters;
+    bool x0_dirty = true, yref_dirty = true, out_valid = false;
+    // device
+    void *d_model = nullptr, *d_x0 = nullptr, *d_yref = nullptr, *d_x = nullptr, *d_u = nullptr;
+    void *d_scratch = nullptr;
+    int *d_status = nullptr, *d_iters = nullptr;
+    size_t off_AB = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
+    std::vector<float> tmp_x0f, tmp_yf;
+    double cost_s = 1.0;  // stage cost factor (time step or 1)
+
+    size_t ystride() const { return (size_t)N * ny + ny_e; }
+    size_t esz() const { return precision == NMPC_FP64 ? sizeof(double) : sizeof(float); }
+    int fail(int code, const std::string &msg)
+    {
+        err = msg;
+        g_err = msg;
+        return code;
+    }
+};
+
+namespace {
+
+int hip_fail(nmpc_solver *h, hipError_t e, const char *what)
+{
+    return h->fail(NMPC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void free_all(nmpc_solver *h)
+{
+    hipSetDevice(h->device);
+    for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
+                    (void *)h->d_iters})
+        if (p) hipFree(p);
+    if (h->ev0) hipEventDestroy(h->ev0);
+    if (h->ev1) hipEventDestroy(h->ev1);
+    if (h->own_stream) hipStreamDestroy(h->own_stream);
+}
+
+template <typename T>
+int launch(nmpc_solver *h)
+{
+    nmpc::IpmParams<T> p;
+    p.B = h->batch;
+    p.N = h->N;
+    p.ny = h->ny;
+    p.ny_e = h->ny_e;
+    p.yref_is_z = h->yref_is_z;
+    p.max_iter = h->max_iter;
+    p.tol_comp = (T)h->tol_comp;
+    p.tol_res = (T)h->tol_res;
+    p.mu0 = (T)h->mu0;
+    p.inv_m = (T)h->inv_m;
+    const char *m = (const char *)h->d_model;
+    p.AB = (const T *)(m + h->off_AB);
+    p.c = (const T *)(m + h->off_c);
+    p.H = (const T *)(m + h->off_H);
+    p.He = (const T *)(m + h->off_He);
+    p.G = (const T *)(m + h->off_G);
+    p.Ge = (const T *)(m + h->off_Ge);
+    p.lbnd = (const T *)(m + h->off_lb);
+    p.ubnd = (const T *)(m + h->off_ub);
+    p.x0 = (const T *)h->d_x0;
+    p.yref = (const T *)h->d_yref;
+    p.xout = (T *)h->d_x;
+    p.uout = (T *)h->d_u;
+    p.status = h->d_status;
+    p.iters = h->d_iters;
+    p.scratch = (T *)h->d_scratch;
+    hipEventRecord(h->ev0, h->stream);
+    hipError_t e = nmpc::ipm_launch<T>(h->kidx, p, h->stream);
+    hipEventRecord(h->ev1, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "ipm kernel launch");
+    return 0;
+}
+
+int field_is(const char *f, const char *name) { return f && std::strcmp(f, name) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int nmpc_abi_version(void) { return NMPC_ABI_VERSION; }
+
+int nmpc_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *nmpc_last_error_global(void) { return g_err.c_str(); }
+
+const char *nmpc_last_error(const nmpc_solver *h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nmpc_solver **out)
+{
+    if (!out) return (g_err = "nmpc_create: out is NULL", NMPC_EINVAL);
+    *out = nullptr;
+    if (!d || d->abi_version != NMPC_ABI_VERSION) {
+        g_err = "nmpc_create: missing descriptor or ABI version mismatch";
+        return NMPC_EINVAL;
+    }
+    if (d->nx < 1 || d->nu < 1 || d->N < 1 || d->ny < 1 || d->ny_e < 0 || batch < 1) {
+        g_err = "nmpc_create: invalid dimensions";
+        return NMPC_EINVAL;
+    }
+    if (precision != NMPC_FP64 && precision != NMPC_FP32) {
+        g_err = "nmpc_create: precision must be NMPC_FP64 or NMPC_FP32";
+        return NMPC_EINVAL;
+    }
+    if (!d->A || !d->B || !d->c || !d->W || !d->Vx || !d->Vu || (d->ny_e > 0 && (!d->W_e || !d->Vx_e))) {
+        g_err = "nmpc_create: dynamics / cost matrices missing";
+        return NMPC_EINVAL;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+        g_err = "nmpc_create: no HIP device available (the engine has no CPU fallback)";
+        return NMPC_EDEVICE;
+    }
+    if (device < 0 || device >= ndev) {
+        g_err = "nmpc_create: device index out of range";
+        return NMPC_EINVAL;
+    }
+    nmpc_solver *h = new nmpc_solver();
+    h->name = d->name ? d->name : "nmpc";
+    h->device = device;
+    h->precision = precision;
+    h->batch = batch;
+    h->nx = d->nx;
+    h->nu = d->nu;
+    h->N = d->N;
+    h->ny = d->ny;
+    h->ny_e = d->ny_e;
+    const int nx = d->nx, nu = d->nu, nz = nx + nu, N = d->N, ny = d->ny, ny_e = d->ny_e;
+
+    int ipw_req = 0;
+    if (const char *e = std::getenv("NMPC_IPW")) ipw_req = std::atoi(e);
+    h->kidx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, -1, &h->ipw, &h->lds)
+                                     : nmpc::ipm_find<float>(nx, nu, -1, &h->ipw, &h->lds);
+    if (h->kidx < 0) {
+        std::string msg = "nmpc_create: no compiled kernel for nx=" + std::to_string(nx) + " nu=" + std::to_string(nu);
+        delete h;
+        g_err = msg;
+        return NMPC_EUNSUPPORTED;
+    }
+    // packing heuristic: keep >= 2 wavefronts per SIMD (1024 SIMDs on MI355X) if possible
+    if (ipw_req <= 0) {
+        int cand[4] = {8, 4, 2, 1}, chosen = -1;
+        for (int ipw : cand) {
+            int ip, ld;
+            const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw, &ip, &ld)
+                                                   : nmpc::ipm_find<float>(nx, nu, ipw, &ip, &ld);
+            if (idx < 0) continue;
+            if (chosen < 0) chosen = ipw;  // widest compiled
+            if ((batch + ipw - 1) / ipw >= 2048) {
+                chosen = ipw;
+                break;
+            }
+            chosen = ipw;  // keep narrowing toward 1 while waves are scarce
+        }
+        ipw_req = chosen;
+    }
+    {
+        const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw_req, &h->ipw, &h->lds)
+                                               : nmpc::ipm_find<float>(nx, nu, ipw_req, &h->ipw, &h->lds);
+        if (idx >= 0) h->kidx = idx;
+    }
+
+    // ---- dynamics
+    if (d->dyn_type == NMPC_DYN_DISCRETE_AFFINE) {
+        h->A.assign(d->A, d->A + nx * nx);
+        h->B.assign(d->B, d->B + nx * nu);
+        h->c.assign(d->c, d->c + nx);
+    } else if (d->dyn_type == NMPC_DYN_CONTINUOUS_AFFINE) {
+        if (!(d->tf > 0.0)) {
+            delete h;
+            g_err = "nmpc_create: tf must be > 0 for continuous dynamics";
+            return NMPC_EINVAL;
+        }
+        const int stages = d->num_stages > 0 ? d->num_stages : (d->integrator_type == NMPC_IRK ? 4 : 4);
+        const int steps = d->num_steps > 0 ? d->num_steps : 1;
+        if (!discretize(nx, nu, d->A, d->B, d->c, d->integrator_type, stages, steps, d->tf / N, h->A, h->B, h->c)) {
+            delete h;
+            g_err = "nmpc_create: unsupported integrator (IRK: 1..9 stages, ERK: 1, 2 or 4 stages)";
+            return NMPC_EUNSUPPORTED;
+        }
+    } else {
+        delete h;
+        g_err = "nmpc_create: unknown dyn_type";
+        return NMPC_EINVAL;
+    }
+    h->ts = d->tf > 0.0 ? d->tf / N : 1.0;
+    // ---- LINEAR_LS cost -> stage QP data
+    const double s = (d->cost_scaling == NMPC_COST_SCALING_TIME_STEPS) ? h->ts : 1.0;
+    h->cost_s = s;
+    h->W.assign(d->W, d->W + ny * ny);
+    h->Vx.assign(d->Vx, d->Vx + ny * nx);
+    h->Vu.assign(d->Vu, d->Vu + ny * nu);
+    if (ny_e > 0) {
+        h->W_e.assign(d->W_e, d->W_e + ny_e * ny_e);
+        h->Vx_e.assign(d->Vx_e, d->Vx_e + ny_e * nx);
+    }
+    std::vector<double> V(ny * nz);
+    for (int r = 0; r < ny; r++) {
+        for (int q = 0; q < nx; q++) V[r * nz + q] = d->Vx[r * nx + q];
+        for (int q = 0; q < nu; q++) V[r * nz + nx + q] = d->Vu[r * nu + q];
+    }
+    h->H.assign(nz * nz, 0.0);
+    h->G.assign(nz * ny, 0.0);
+    for (int i = 0; i < nz; i++)
+        for (int j = 0; j < ny; j++) {
+            double wv = 0.0;
+            for (int r = 0; r < ny; r++) wv += V[r * nz + i] * d->W[r * ny + j];
+            h->G[i * ny + j] = -s * wv;
+        }
+    for (int i = 0; i < nz; i++)
+        for (int j = 0; j < nz; j++) {
+            double acc = 0.0;
+            for (int r = 0; r < ny; r++) acc += -h->G[i * ny + r] * V[r * nz + j];
+            h->H[i * nz + j] = acc;
+        }
+    h->He.assign(nx * nx, 0.0);
+    h->Ge.assign(nx * std::max(ny_e, 1), 0.0);
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < ny_e; j++) {
+            double wv = 0.0;
+            for (int r = 0; r < ny_e; r++) wv += d->Vx_e[r * nx + i] * d->W_e[r * ny_e + j];
+            h->Ge[i * ny_e + j] = -h->scale_e * wv;
+        }
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < nx; j++) {
+            double acc = 0.0;
+            for (int r = 0; r < ny_e; r++) acc += -h->Ge[i * ny_e + r] * d->Vx_e[r * nx + j];
+            h->He[i * nx + j] = acc;
+        }
+    bool sel = (ny == nz) && (ny_e == nx);
+    for (int r = 0; sel && r < ny; r++)
+        for (int q = 0; sel && q < nz; q++)
+            if (V[r * nz + q] != (r == q ? 1.0 : 0.0)) sel = false;
+    for (int r = 0; sel && r < ny_e; r++)
+        for (int q = 0; sel && q < nx; q++)
+            if (d->Vx_e[r * nx + q] != (r == q ? 1.0 : 0.0)) sel = false;
+    h->yref_is_z = sel ? 1 : 0;
+    // ---- bounds [3][nz]
+    h->lbnd.assign(3 * nz, -kInf);
+    h->ubnd.assign(3 * nz, kInf);
+    int nlb_u = 0, nub_u = 0, nlb_x = 0, nub_x = 0, nlb_e = 0, nub_e = 0;
+    for (int j = 0; j < d->nbu; j++) {
+        const int i = d->idxbu[j];
+        if (i < 0 || i >= nu) {
+            delete h;
+            g_err = "nmpc_create: idxbu out of range";
+            return NMPC_EINVAL;
+        }
+        for (int t = 0; t < 2; t++) {
+            h->lbnd[t * nz + nx + i] = d->lbu[j];
+            h->ubnd[t * nz + nx + i] = d->ubu[j];
+        }
+        nlb_u += has_bound(d->lbu[j]);
+        nub_u += has_bound(d->ubu[j]);
+    }
+    for (int j = 0; j < d->nbx; j++) {
+        const int i = d->idxbx[j];
+        if (i < 0 || i >= nx) {
+            delete h;
+            g_err = "nmpc_create: idxbx out of range";
+            return NMPC_EINVAL;
+        }
+        h->lbnd[1 * nz + i] = d->lbx[j];
+        h->ubnd[1 * nz + i] = d->ubx[j];
+        nlb_x += has_bound(d->lbx[j]);
+        nub_x += has_bound(d->ubx[j]);
+    }
+    for (int j = 0; j < d->nbx_e; j++) {
+        const int i = d->idxbx_e[j];
+        if (i < 0 || i >= nx) {
+            delete h;
+            g_err = "nmpc_create: idxbx_e out of range";
+            return NMPC_EINVAL;
+        }
+        h->lbnd[2 * nz + i] = d->lbx_e[j];
+        h->ubnd[2 * nz + i] = d->ubx_e[j];
+        nlb_e += has_bound(d->lbx_e[j]);
+        nub_e += has_bound(d->ubx_e[j]);
+    }
+    const long m = (long)N * (nlb_u + nub_u) + (long)(N - 1) * (nlb_x + nub_x) + (nlb_e + nub_e);
+    h->inv_m = 1.0 / (double)std::max(1L, m);
+    // ---- options
+    const bool f64 = precision == NMPC_FP64;
+    h->max_iter = d->qp_solver_iter_max > 0 ? d->qp_solver_iter_max : 50;
+    h->tol_comp = d->qp_solver_tol_comp > 0 ? d->qp_solver_tol_comp : (f64 ? 1e-15 : 1e-7);
+    h->tol_res = d->qp_solver_tol_res > 0 ? d->qp_solver_tol_res : (f64 ? 1e-12 : 1e-5);
+    h->mu0 = d->qp_solver_mu0 > 0 ? d->qp_solver_mu0 : 1e-2;
+    // ---- host staging
+    h->h_x0.assign((size_t)batch * nx, 0.0);
+    if (d->x0)
+        for (int b = 0; b < batch; b++) std::memcpy(&h->h_x0[(size_t)b * nx], d->x0, nx * sizeof(double));
+    h->h_lbx0 = h->h_x0;
+    h->h_ubx0 = h->h_x0;
+    h->h_yref.assign((size_t)batch * h->ystride(), 0.0);
+    if (d->yref || d->yref_e)
+        for (int b = 0; b < batch; b++) {
+            for (int k = 0; k < N && d->yref; k++)
+                std::memcpy(&h->h_yref[b * h->ystride() + (size_t)k * ny], d->yref, ny * sizeof(double));
+            if (d->yref_e && ny_e > 0)
+                std::memcpy(&h->h_yref[b * h->ystride() + (size_t)N * ny], d->yref_e, ny_e * sizeof(double));
+        }
+    h->h_x.assign((size_t)batch * (N + 1) * nx, 0.0);
+    h->h_u.assign((size_t)batch * N * nu, 0.0);
+    h->h_status.assign(batch, 0);
+    h->h_iters.assign(batch, 0);
+
+    // ---- device
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) {
+        int r = hip_fail(h, e, "hipSetDevice");
+        delete h;
+        return r;
+    }
+    if ((e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking)) != hipSuccess) {
+        int r = hip_fail(h, e, "hipStreamCreate");
+        delete h;
+        return r;
+    }
+    h->stream = h->own_stream;
+    hipEventCreate(&h->ev0);
+    hipEventCreate(&h->ev1);
+    const size_t es = h->esz();
+    size_t off = 0;
+    auto carve = [&](size_t n) {
+        size_t o = off;
+        off += ((n * es + 255) / 256) * 256;
+        return o;
+    };
+    h->off_AB = carve((size_t)nx * nz);
+    h->off_c = carve(nx);
+    h->off_H = carve((size_t)nz * nz);
+    h->off_He = carve((size_t)nx * nx);
+    h->off_G = carve((size_t)nz * ny);
+    h->off_Ge = carve((size_t)nx * std::max(ny_e, 1));
+    h->off_lb = carve(3 * nz);
+    h->off_ub = carve(3 * nz);
+    const size_t model_bytes = off;
+    const size_t ngroups = (size_t)(batch + h->ipw - 1) / h->ipw;
+    const size_t scratch_bytes = ngroups * h->ipw * nmpc::scratch_elems_per_instance(N, nx, nu) * es;
+    bool ok = hipMalloc(&h->d_model, model_bytes) == hipSuccess &&
+              hipMalloc(&h->d_x0, (size_t)batch * nx * es) == hipSuccess &&
+              hipMalloc(&h->d_yref, (size_t)batch * h->ystride() * es) == hipSuccess &&
+              hipMalloc(&h->d_x, (size_t)batch * (N + 1) * nx * es) == hipSuccess &&
+              hipMalloc(&h->d_u, (size_t)batch * N * nu * es) == hipSuccess &&
+              hipMalloc((void **)&h->d_status, (size_t)batch * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_iters, (size_t)batch * sizeof(int)) == hipSuccess &&
+              hipMalloc(&h->d_scratch, scratch_bytes) == hipSuccess;
+    if (!ok) {
+        h->fail(NMPC_ENOMEM, "nmpc_create: device allocation failed");
+        free_all(h);
+        delete h;
+        return NMPC_ENOMEM;
+    }
+    // model upload
+    std::vector<double> AB((size_t)nx * nz);
+    for (int r = 0; r < nx; r++) {
+        for (int q = 0; q < nx; q++) AB[r * nz + q] = h->A[r * nx + q];
+        for (int q = 0; q < nu; q++) AB[r * nz + nx + q] = h->B[r * nu + q];
+    }
+    char *dm = (char *)h->d_model;
+    auto put = [&](size_t o, const std::vector<double> &v) {
+        if (f64) {
+            hipMemcpy(dm + o, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice);
+        } else {
+            std::vector<float> t(v.begin(), v.end());
+            hipMemcpy(dm + o, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice);
+        }
+    };
+    put(h->off_AB, AB);
+    put(h->off_c, h->c);
+    put(h->off_H, h->H);
+    put(h->off_He, h->He);
+    put(h->off_G, h->G);
+    put(h->off_Ge, h->Ge);
+    put(h->off_lb, h->lbnd);
+    put(h->off_ub, h->ubnd);
+    if ((e = hipDeviceSynchronize()) != hipSuccess) {
+        int r = hip_fail(h, e, "model upload");
+        free_all(h);
+        delete h;
+        return r;
+    }
+    *out = h;
+    return 0;
+}
+
+void nmpc_destroy(nmpc_solver *h)
+{
+    if (!h) return;
+    free_all(h);
+    delete h;
+}
+
+int nmpc_set_stream(nmpc_solver *h, void *s)
+{
+    if (!h) return NMPC_EINVAL;
+    h->stream = s ? (hipStream_t)s : h->own_stream;
+    return 0;
+}
+
+void *nmpc_get_stream(nmpc_solver *h) { return h ? (void *)h->stream : nullptr; }
+
+int nmpc_get_model(const nmpc_solver *h, double *A, double *B, double *c)
+{
+    if (!h) return NMPC_EINVAL;
+    if (A) std::memcpy(A, h->A.data(), h->A.size() * sizeof(double));
+    if (B) std::memcpy(B, h->B.data(), h->B.size() * sizeof(double));
+    if (c) std::memcpy(c, h->c.data(), h->c.size() * sizeof(double));
+    return 0;
+}
+
+int nmpc_set(nmpc_solver *h, int inst, int stage, const char *field, const double *v, int n)
+{
+    if (!h || !field || !v) return NMPC_EINVAL;
+    if (inst < -1 || inst >= h->batch) return h->fail(NMPC_EINVAL, "nmpc_set: instance out of range");
+    const int b0 = inst < 0 ? 0 : inst, b1 = inst < 0 ? h->batch : inst + 1;
+    if (field_is(field, "yref")) {
+        if (stage < 0 || stage > h->N) return h->fail(NMPC_EINVAL, "nmpc_set: stage out of range");
+        const int want = stage < h->N ? h->ny : h->ny_e;
+        if (n != want)
+            return h->fail(NMPC_EINVAL, "nmpc_set: yref at stage " + std::to_string(stage) + " needs " +
+                                            std::to_string(want) + " values, got " + std::to_string(n));
+        for (int b = b0; b < b1; b++)
+            std::memcpy(&h->h_yref[b * h->ystride() + (size_t)stage * h->ny], v, n * sizeof(double));
+        h->yref_dirty = true;
+        return 0;
+    }
+    if (field_is(field, "lbx") || field_is(field, "ubx") || field_is(field, "x0")) {
+        if (!field_is(field, "x0") && stage != 0)
+            return h->fail(NMPC_EUNSUPPORTED,
+                           "nmpc_set: state bounds can only be set at stage 0 (x0 pinning); stage " +
+                               std::to_string(stage) + " bounds are part of the model");
+        if (n != h->nx) return h->fail(NMPC_EINVAL, "nmpc_set: lbx/ubx/x0 need nx values");
+        for (int b = b0; b < b1; b++) {
+            if (!field_is(field, "ubx")) std::memcpy(&h->h_lbx0[(size_t)b * h->nx], v, n * sizeof(double));
+            if (!field_is(field, "lbx")) std::memcpy(&h->h_ubx0[(size_t)b * h->nx], v, n * sizeof(double));
+        }
+        h->x0_dirty = true;
+        return 0;
+    }
+    return h->fail(NMPC_EINVAL, std::string("nmpc_set: unknown field '") + field + "'");
+}
+
+int nmpc_get(nmpc_solver *h, int inst, int stage, const char *field, double *out, int n)
+{
+    if (!h || !field || !out) return NMPC_EINVAL;
+    if (inst < 0 || inst >= h->batch) return h->fail(NMPC_EINVAL, "nmpc_get: instance out of range");
+    if (!h->out_valid) return h->fail(NMPC_ESTATE, "nmpc_get: no solution available (call nmpc_solve first)");
+    if (field_is(field, "x")) {
+        if (stage < 0 || stage > h->N || n != h->nx) return h->fail(NMPC_EINVAL, "nmpc_get: bad stage/size for x");
+        std::memcpy(out, &h->h_x[((size_t)inst * (h->N + 1) + stage) * h->nx], n * sizeof(double));
+        return 0;
+    }
+    if (field_is(field, "u")) {
+        if (stage < 0 || stage >= h->N || n != h->nu) return h->fail(NMPC_EINVAL, "nmpc_get: bad stage/size for u");
+        std::memcpy(out, &h->h_u[((size_t)inst * h->N + stage) * h->nu], n * sizeof(double));
+        return 0;
+    }
+    return h->fail(NMPC_EINVAL, std::string("nmpc_get: unknown field '") + field + "'");
+}
+
+int nmpc_set_batch(nmpc_solver *h, const char *field, const double *v, size_t count)
+{
+    if (!h || !field || !v) return NMPC_EINVAL;
+    if (field_is(field, "x0")) {
+        if (count != h->h_x0.size()) return h->fail(NMPC_EINVAL, "nmpc_set_batch: x0 needs batch*nx values");
+        std::memcpy(h->h_lbx0.data(), v, count * sizeof(double));
+        std::memcpy(h->h_ubx0.data(), v, count * sizeof(double));
+        h->x0_dirty = true;
+        return 0;
+    }
+    if (field_is(field, "yref")) {
+        if (count != h->h_yref.size())
+            return h->fail(NMPC_EINVAL, "nmpc_set_batch: yref needs batch*(N*ny+ny_e) values");
+        std::memcpy(h->h_yref.data(), v, count * sizeof(double));
+        h->yref_dirty = true;
+        return 0;
+    }
+    return h->fail(NMPC_EINVAL, std::string("nmpc_set_batch: unknown field '") + field + "'");
+}
+
+int nmpc_get_batch(nmpc_solver *h, const char *field, double *out, size_t count)
+{
+    if (!h || !field || !out) return NMPC_EINVAL;
+    if (!h->out_valid) return h->fail(NMPC_ESTATE, "nmpc_get_batch: no solution available");
+    const std::vector<double> *src = field_is(field, "x") ? &h->h_x : field_is(field, "u") ? &h->h_u : nullptr;
+    if (!src) return h->fail(NMPC_EINVAL, std::string("nmpc_get_batch: unknown field '") + field + "'");
+    if (count != src->size()) return h->fail(NMPC_EINVAL, "nmpc_get_batch: size mismatch");
+    std::memcpy(out, src->data(), count * sizeof(double));
+    return 0;
+}
+
+int nmpc_get_batch_int(nmpc_solver *h, const char *field, int32_t *out, size_t count)
+{
+    if (!h || !field || !out) return NMPC_EINVAL;
+    if (!h->out_valid) return h->fail(NMPC_ESTATE, "nmpc_get_batch_int: no solution available");
+    const std::vector<int32_t> *src =
+        field_is(field, "status") ? &h->h_status : field_is(field, "qp_iter") ? &h->h_iters : nullptr;
+    if (!src) return h->fail(NMPC_EINVAL, std::string("nmpc_get_batch_int: unknown field '") + field + "'");
+    if (count != src->size()) return h->fail(NMPC_EINVAL, "nmpc_get_batch_int: size mismatch");
+    std::memcpy(out, src->data(), count * sizeof(int32_t));
+    return 0;
+}
+
+int nmpc_device_ptr(nmpc_solver *h, const char *field, void **out)
+{
+    if (!h || !field || !out) return NMPC_EINVAL;
+    if (field_is(field, "x0")) *out = h->d_x0;
+    else if (field_is(field, "yref")) *out = h->d_yref;
+    else if (field_is(field, "x")) *out = h->d_x;
+    else if (field_is(field, "u")) *out = h->d_u;
+    else if (field_is(field, "status")) *out = h->d_status;
+    else if (field_is(field, "qp_iter")) *out = h->d_iters;
+    else return h->fail(NMPC_EINVAL, std::string("nmpc_device_ptr: unknown field '") + field + "'");
+    return 0;
+}
+
+int nmpc_solve_async(nmpc_solver *h)
+{
+    if (!h) return NMPC_EINVAL;
+    hipSetDevice(h->device);
+    h->out_valid = false;
+    return h->precision == NMPC_FP64 ? launch<double>(h) : launch<float>(h);
+}
+
+int nmpc_synchronize(nmpc_solver *h)
+{
+    if (!h) return NMPC_EINVAL;
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize");
+    hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1);
+    return 0;
+}
+
+int nmpc_solve(nmpc_solver *h)
+{
+    if (!h) return NMPC_EINVAL;
+    hipSetDevice(h->device);
+    hipError_t e;
+    if (h->x0_dirty) {
+        for (size_t i = 0; i < h->h_lbx0.size(); i++)
+            if (h->h_lbx0[i] != h->h_ubx0[i])
+                return h->fail(NMPC_EUNSUPPORTED,
+                               "nmpc_solve: stage-0 lbx != ubx for instance " + std::to_string(i / h->nx) +
+                                   " (the engine pins x0 = lbx = ubx, as the reference does)");
+        h->h_x0 = h->h_lbx0;
+        e = upload_any(h->d_x0, h->h_x0.data(), h->h_x0.size(), h->precision == NMPC_FP64, h->stream, h->tmp_x0f);
+        if (e != hipSuccess) return hip_fail(h, e, "upload x0");
+        h->x0_dirty = false;
+    }
+    if (h->yref_dirty) {
+        e = upload_any(h->d_yref, h->h_yref.data(), h->h_yref.size(), h->precision == NMPC_FP64, h->stream,
+                       h->tmp_yf);
+        if (e != hipSuccess) return hip_fail(h, e, "upload yref");
+        h->yref_dirty = false;
+    }
+    int r = h->precision == NMPC_FP64 ? launch<double>(h) : launch<float>(h);
+    if (r < 0) return r;
+    const size_t nxo = h->h_x.size(), nuo = h->h_u.size();
+    if (h->precision == NMPC_FP64) {
+        hipMemcpyAsync(h->h_x.data(), h->d_x, nxo * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+        hipMemcpyAsync(h->h_u.data(), h->d_u, nuo * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+    }
+    std::vector<float> fx, fu;
+    if (h->precision == NMPC_FP32) {
+        fx.resize(nxo);
+        fu.resize(nuo);
+        hipMemcpyAsync(fx.data(), h->d_x, nxo * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+        hipMemcpyAsync(fu.data(), h->d_u, nuo * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+    }
+    hipMemcpyAsync(h->h_status.data(), h->d_status, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    hipMemcpyAsync(h->h_iters.data(), h->d_iters, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "solve");
+    if (h->precision == NMPC_FP32) {
+        for (size_t i = 0; i < nxo; i++) h->h_x[i] = fx[i];
+        for (size_t i = 0; i < nuo; i++) h->h_u[i] = fu[i];
+    }
+    hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1);
+    h->out_valid = true;
+    int st = 0;
+    for (int b = 0; b < h->batch; b++) st = std::max(st, (int)h->h_status[b]);
+    return st;
+}
+
+int nmpc_get_cost(nmpc_solver *h, int inst, double *cost)
+{
+    if (!h || !cost) return NMPC_EINVAL;
+    if (inst < 0 || inst >= h->batch) return h->fail(NMPC_EINVAL, "nmpc_get_cost: instance out of range");
+    if (!h->out_valid) return h->fail(NMPC_ESTATE, "nmpc_get_cost: no solution available");
+    const int nx = h->nx, nu = h->nu, N = h->N, ny = h->ny, ny_e = h->ny_e;
+    const double sc = h->cost_s;
+    const double *X = &h->h_x[(size_t)inst * (N + 1) * nx];
+    const double *U = &h->h_u[(size_t)inst * N * nu];
+    const double *Y = &h->h_yref[(size_t)inst * h->ystride()];
+    double total = 0.0;
+    std::vector<double> r(std::max(ny, ny_e));
+    for (int k = 0; k < N; k++) {
+        for (int i = 0; i < ny; i++) {
+            double y = -Y[(size_t)k * ny + i];
+            for (int q = 0; q < nx; q++) y += h->Vx[i * nx + q] * X[k * nx + q];
+            for (int q = 0; q < nu; q++) y += h->Vu[i * nu + q] * U[k * nu + q];
+            r[i] = y;
+        }
+        double acc = 0.0;
+        for (int i = 0; i < ny; i++)
+            for (int j = 0; j < ny; j++) acc += r[i] * h->W[i * ny + j] * r[j];
+        total += 0.5 * sc * acc;
+    }
+    if (ny_e > 0) {
+        for (int i = 0; i < ny_e; i++) {
+            double y = -Y[(size_t)N * ny + i];
+            for (int q = 0; q < nx; q++) y += h->Vx_e[i * nx + q] * X[N * nx + q];
+            r[i] = y;
+        }
+        double acc = 0.0;
+        for (int i = 0; i < ny_e; i++)
+            for (int j = 0; j < ny_e; j++) acc += r[i] * h->W_e[i * ny_e + j] * r[j];
+        total += 0.5 * acc;
+    }
+    *cost = total;
+    return 0;
+}
+
+int nmpc_get_stats(nmpc_solver *h, double *st, int n)
+{
+    if (!h || !st || n < 1) return NMPC_EINVAL;
+    double mx = 0, mean = 0, nf = 0;
+    for (int b = 0; b < h->batch; b++) {
+        mx = std::max(mx, (double)h->h_iters[b]);
+        mean += h->h_iters[b];
+        nf += h->h_status[b] != 0;
+    }
+    const double v[5] = {mx, mean / h->batch, nf, (double)h->last_ms, 1.0};
+    for (int i = 0; i < n && i < 5; i++) st[i] = v[i];
+    return 0;
+}
+
+int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
+{
+    if (!h || !out) return NMPC_EINVAL;
+    const int v[4] = {h->ipw, (h->batch + h->ipw - 1) / h->ipw, 64, h->lds};
+    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
+    return 0;
+}
+
+int nmpc_sim_plant(int device, int batch, int num_stages, double T, double mass, double g, const double *x_in,
+                   const double *u, double *x_out)
+{
+    if (batch < 1 || !x_in || !u || !x_out || (num_stages != 1 && num_stages != 4)) {
+        g_err = "nmpc_sim_plant: invalid arguments (num_stages must be 1 or 4)";
+        return NMPC_EINVAL;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        g_err = "nmpc_sim_plant: no HIP device";
+        return NMPC_EDEVICE;
+    }
+    double *d = nullptr;
+    if (hipMalloc(&d, sizeof(double) * (size_t)batch * 10) != hipSuccess) {
+        g_err = "nmpc_sim_plant: allocation failed";
+        return NMPC_ENOMEM;
+    }
+    hipMemcpy(d, x_in, sizeof(double) * batch * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d + batch * 4, u, sizeof(double) * batch * 2, hipMemcpyHostToDevice);
+    hipError_t e = nmpc::plant_step_launch(batch, num_stages, T, mass, g, d, d + batch * 4, d + batch * 6, 0);
+    if (e == hipSuccess) e = hipMemcpy(x_out, d + batch * 6, sizeof(double) * batch * 4, hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) {
+        g_err = std::string("nmpc_sim_plant: ") + hipGetErrorString(e);
+        return NMPC_EDEVICE;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,49 @@
+// nmpc_internal.h — device-side parameter blocks shared by the HIP kernels and the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace nmpc {
+
+// Kernel parameters of the batched IPM solve (nmpc_ipm.hip). All pointers are device
+// pointers. Model data (AB..ubnd) is shared by every instance of a handle.
+template <typename T>
+struct IpmParams {
+    int B;          // instances
+    int N;          // horizon
+    int ny, ny_e;   // LINEAR_LS residual sizes
+    int yref_is_z;  // y = [x; u] (selection Vx, Vu): use yref as the initial guess
+    int max_iter;
+    T tol_comp, tol_res, mu0, inv_m;
+    const T *AB;    // [nx][nx+nu]   discrete [A B], row-major
+    const T *c;     // [nx]
+    const T *H;     // [nz][nz]      stage Hessian (cost-scaled), z = [x; u]
+    const T *He;    // [nx][nx]
+    const T *G;     // [nz][ny]      stage gradient map: g_k = G yref_k
+    const T *Ge;    // [nx][ny_e]
+    const T *lbnd;  // [3][nz]       bounds: stage 0 (x entries absent), 1..N-1, N
+    const T *ubnd;  // [3][nz]
+    const T *x0;    // [B][nx]
+    const T *yref;  // [B][N*ny + ny_e]
+    T *xout;        // [B][N+1][nx]
+    T *uout;        // [B][N][nu]
+    int *status;    // [B]
+    int *iters;     // [B]
+    T *scratch;     // [ceil(B/IPW)*IPW][scratch_elems_per_instance]
+};
+
+size_t scratch_elems_per_instance(int N, int nx, int nu);
+
+// returns an index into the kernel table (or -1), the chosen instances-per-wave and the
+// static LDS bytes per workgroup. ipw_req <= 0 picks the widest packing compiled.
+template <typename T>
+int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out);
+template <typename T>
+hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s);
+
+// plant simulator (nmpc_plant.hip)
+hipError_t plant_step_launch(int batch, int num_stages, double T, double mass, double g,
+                             const double *x_in, const double *u, double *x_out, hipStream_t s);
+
+}  // namespace nmpc

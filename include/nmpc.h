@@ -1,0 +1,192 @@
+/*
+ * nmpc.h — C-ABI of the MI355X batched NMPC solve engine (libnmpc_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path. In the reference every closed-loop step
+ * goes Python -> acados_template (ctypes) -> the generated `libacados_ocp_solver_<model>.so`:
+ *
+ *   reference call site                                   replaced by
+ *   ---------------------------------------------------   -----------------------------------
+ *   AcadosOcpSolver(ocp, json_file=...)                    nmpc_create()
+ *     force_model/ocp.py:95-96, jerk_model/ocp.py:94-95     (JSON render + CasADi codegen +
+ *     [ext: <name>_acados_create / ocp_nlp_* setup]          make + dlopen -> one C call)
+ *   ocp_solver.set(k, 'yref', v)                           nmpc_set(h, inst, k, "yref", v, n)
+ *     force_model/ocp.py:120-122, jerk_model/ocp.py:121-123
+ *     [ext: ocp_nlp_cost_model_set(..., "yref")]
+ *   ocp_solver.set(0, 'lbx'/'ubx', x0_bar)                 nmpc_set(h, inst, 0, "lbx"/"ubx", ...)
+ *     force_model/controller.py:30-31, jerk_model/controller.py:31-32
+ *     [ext: ocp_nlp_constraints_model_set(..., "lbx")]
+ *   status = ocp_solver.solve()                            nmpc_solve(h)
+ *     force_model/controller.py:32, jerk_model/controller.py:33
+ *     [ext: <name>_acados_solve]
+ *   ocp_solver.get(k, 'u' / 'x')                           nmpc_get(h, inst, k, "u"/"x", out, n)
+ *     force_model/controller.py:37,39, jerk_model/controller.py:38-39
+ *     [ext: ocp_nlp_out_get(..., "u")]
+ *   ocp_solver.get_cost(), print_statistics()              nmpc_get_cost(), nmpc_get_stats()
+ *     force_model/ocp.py:164, force_model/controller.py:34
+ *   AcadosSimSolver.set/solve/get (plant step)             nmpc_sim_step()
+ *     force_model/ocp.py:108-112, jerk_model/ocp.py:110-113
+ *
+ * Every handle carries a batch dimension: `instance` selects one of `batch` independent
+ * OCPs (instance = -1 in nmpc_set broadcasts to all). Batched host/device entry points
+ * (nmpc_set_batch / nmpc_get_batch / nmpc_device_ptr) serve the batched drivers.
+ *
+ * Conventions: the engine owns its device buffers, the caller owns host buffers (copied in
+ * and out). Return codes: >= 0 are acados solver status codes (src/Readme.md:14-20:
+ * 0 success, 1 failure, 2 max iterations, 3 min step, 4 QP solver failed); < 0 are API
+ * errors (NMPC_E*), with a message from nmpc_last_error(). One handle per host thread;
+ * every handle runs on its own HIP stream unless nmpc_set_stream() supplies one.
+ * All matrices are row-major doubles. A bound with |value| >= 1e20 means "no bound"
+ * (acados ACADOS_INFTY convention).
+ */
+#ifndef NMPC_H
+#define NMPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMPC_ABI_VERSION 1
+
+/* solver status codes (acados, src/Readme.md:14-20) */
+#define NMPC_SUCCESS 0
+#define NMPC_FAILURE 1
+#define NMPC_MAXITER 2
+#define NMPC_MINSTEP 3
+#define NMPC_QP_FAILURE 4
+
+/* API error codes */
+#define NMPC_EINVAL -1
+#define NMPC_EDEVICE -2
+#define NMPC_ENOMEM -3
+#define NMPC_EUNSUPPORTED -4
+#define NMPC_ESTATE -5
+
+/* precision */
+#define NMPC_FP64 0
+#define NMPC_FP32 1
+
+/* dynamics description */
+#define NMPC_DYN_CONTINUOUS_AFFINE 0 /* x' = A x + B u + c, integrated by `integrator` */
+#define NMPC_DYN_DISCRETE_AFFINE 1   /* x+ = A x + B u + c */
+
+/* integrator_type (acados solver_options.integrator_type) */
+#define NMPC_IRK 0 /* Gauss-Legendre collocation, num_stages (acados default 4) */
+#define NMPC_ERK 1 /* explicit Runge-Kutta: 1 = Euler, 2 = midpoint, 4 = classic RK4 */
+
+/* cost_scaling */
+#define NMPC_COST_SCALING_TIME_STEPS 0 /* stage cost x time step, terminal x 1 (acados) */
+#define NMPC_COST_SCALING_NONE 1
+
+typedef struct nmpc_ocp_desc {
+    int abi_version; /* = NMPC_ABI_VERSION */
+    const char *name;
+    /* dims (AcadosOcp.dims) */
+    int nx, nu, N, ny, ny_e;
+    /* dynamics (AcadosModel f_expl_expr of an affine model; replaces the CasADi-generated
+     * integrator sensitivities of force_model/dynamics.py:32-47, jerk_model/dynamics.py:35-52) */
+    int dyn_type;
+    const double *A; /* nx*nx */
+    const double *B; /* nx*nu */
+    const double *c; /* nx */
+    int integrator_type, num_stages, num_steps;
+    double tf; /* horizon length; time step = tf / N (ocp.py:92-93) */
+    /* LINEAR_LS cost (force_model/ocp.py:28-58) */
+    const double *W, *Vx, *Vu; /* ny*ny, ny*nx, ny*nu */
+    const double *W_e, *Vx_e;  /* ny_e*ny_e, ny_e*nx */
+    const double *yref, *yref_e; /* initial cost.yref (ny) / cost.yref_e (ny_e); may be NULL */
+    int cost_scaling;
+    /* box constraints BGH (force_model/ocp.py:62-78); x at stage 0 is pinned by lbx=ubx */
+    int nbu;
+    const int *idxbu;
+    const double *lbu, *ubu;
+    int nbx;
+    const int *idxbx;
+    const double *lbx, *ubx; /* stages 1..N-1 */
+    int nbx_e;
+    const int *idxbx_e;
+    const double *lbx_e, *ubx_e;
+    const double *x0; /* constraints.x0 initial value (nx); may be NULL */
+    /* QP / IPM options (solver_options.qp_solver_*) */
+    int qp_solver_iter_max;    /* <= 0: 50 */
+    double qp_solver_tol_comp; /* <= 0: 1e-15 (fp64) / 1e-7 (fp32) */
+    double qp_solver_tol_res;  /* <= 0: 1e-12 (fp64) / 1e-6 (fp32) */
+    double qp_solver_mu0;      /* <= 0: 1e-2 */
+} nmpc_ocp_desc;
+
+typedef struct nmpc_solver nmpc_solver;
+
+/* library / device */
+int nmpc_abi_version(void);
+int nmpc_device_count(void);
+const char *nmpc_last_error_global(void);
+
+/* lifecycle */
+int nmpc_create(const nmpc_ocp_desc *desc, int batch, int device, int precision, nmpc_solver **out);
+void nmpc_destroy(nmpc_solver *h);
+const char *nmpc_last_error(const nmpc_solver *h);
+int nmpc_set_stream(nmpc_solver *h, void *hip_stream); /* NULL: back to the handle's own stream */
+void *nmpc_get_stream(nmpc_solver *h);
+
+/* discrete model actually used on the device (after integration): A (nx*nx), B (nx*nu), c (nx) */
+int nmpc_get_model(const nmpc_solver *h, double *A, double *B, double *c);
+
+/* per-instance field access (AcadosOcpSolver.set/get). Fields:
+ *   set: "yref" (stage 0..N-1: ny values, stage N: ny_e), "lbx"/"ubx" (stage 0 only: nx,
+ *        must end up equal = x0_bar), "x0" (stage ignored: nx, sets lbx=ubx)
+ *   get: "x" (stage 0..N: nx), "u" (stage 0..N-1: nu)
+ * instance = -1 in nmpc_set applies the value to every instance. */
+int nmpc_set(nmpc_solver *h, int instance, int stage, const char *field, const double *value, int n);
+int nmpc_get(nmpc_solver *h, int instance, int stage, const char *field, double *out, int n);
+
+/* batched host access. Fields and layouts (row-major, instance-major):
+ *   "x0"   batch*nx                 (set)
+ *   "yref" batch*(N*ny + ny_e)      (set; stage-stacked horizon window)
+ *   "x"    batch*(N+1)*nx           (get)
+ *   "u"    batch*N*nu               (get)
+ *   "status", "qp_iter"  batch int32 (get; use nmpc_get_batch_int)
+ * `count` = number of doubles supplied / requested, checked against the layout. */
+int nmpc_set_batch(nmpc_solver *h, const char *field, const double *values, size_t count);
+int nmpc_get_batch(nmpc_solver *h, const char *field, double *out, size_t count);
+int nmpc_get_batch_int(nmpc_solver *h, const char *field, int32_t *out, size_t count);
+
+/* device-resident access for batched drivers: the engine's own device buffer for a field
+ * ("x0", "yref", "x", "u", "status", "qp_iter"), element type double (NMPC_FP64) or float
+ * (NMPC_FP32) / int32. Writing "x0"/"yref" there before nmpc_solve_async() skips the copy. */
+int nmpc_device_ptr(nmpc_solver *h, const char *field, void **out);
+
+/* solve all instances. nmpc_solve: upload host-staged inputs, launch, wait, download; returns
+ * the max status over instances (0 when every instance succeeded) or < 0 on API error.
+ * nmpc_solve_async: launch on the handle's stream using the device buffers as they are;
+ * returns immediately (no host staging). */
+int nmpc_solve(nmpc_solver *h);
+int nmpc_solve_async(nmpc_solver *h);
+int nmpc_synchronize(nmpc_solver *h);
+
+/* cost of the current solution of one instance (AcadosOcpSolver.get_cost, acados
+ * LINEAR_LS semantics: sum_k s_k 1/2|y_k - yref_k|^2_W + 1/2|y_N - yref_N|^2_We) */
+int nmpc_get_cost(nmpc_solver *h, int instance, double *cost);
+
+/* statistics of the last solve: stats[0] = max qp_iter, stats[1] = mean qp_iter,
+ * stats[2] = number of instances with status != 0, stats[3] = device time of the last
+ * solve in ms (HIP events), stats[4] = sqp_iter (always 1: one QP solves an LQ-OCP) */
+int nmpc_get_stats(nmpc_solver *h, double *stats, int n);
+
+/* kernel geometry chosen for this handle: out[0] = instances per wavefront,
+ * out[1] = workgroups per launch, out[2] = threads per workgroup, out[3] = LDS bytes/WG */
+int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n);
+
+/* plant simulator (AcadosSimSolver for src/plant.py:27-43): one step of the nonlinear 2-D
+ * Crazyflie plant x=[px,pz,vx,vz], u=[theta, F_d] on the device for `batch` states.
+ *   method NMPC_ERK, num_stages 4 over T (force_model/ocp.py:98-104), or
+ *   method NMPC_ERK, num_stages 1 over T (jerk_model/ocp.py:97-104).
+ * x_in/x_out: batch*4, u: batch*2 (host pointers). mass, g: plant constants. */
+int nmpc_sim_plant(int device, int batch, int num_stages, double T, double mass, double g,
+                   const double *x_in, const double *u, double *x_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NMPC_H */

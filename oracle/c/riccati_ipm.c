@@ -1,0 +1,451 @@
+/*
+ * riccati_ipm.c — plain-C fp64 reference of the batched NMPC step solve.
+ * TEST INFRASTRUCTURE ONLY (see oracle/__init__.py): used by tests/ as a second,
+ * stage-wise implementation next to the dense numpy oracle, and by bench.py's
+ * cpu_baseline leg ("port": OpenMP over instances on the host cores).
+ *
+ * What it restates: one `AcadosOcpSolver.solve()` per instance
+ * (src/force_model/controller.py:30-32, src/jerk_model/controller.py:31-33) for the
+ * reference's LTI / LINEAR_LS / box-constrained OCPs (force_model/ocp.py:21-96,
+ * jerk_model/ocp.py:20-95): SQP-GN == one QP, solved by a Mehrotra predictor-corrector
+ * interior-point method whose Newton systems are solved by a backward Riccati recursion
+ * over the N stages — the algorithm class of HPIPM's OCP-QP IPM [ext; HPIPM is not in
+ * the tree]. It is the same algorithm, step for step, as the HIP kernel
+ * (drone-attitude-control_amd/csrc/nmpc_kernels.hip), so its mean iteration count is
+ * the n_ipm used for the roofline's algorithmic flop count.
+ *
+ * Problem per instance (stage k = 0..N, z_k = [x_k; u_k], z_N = x_N, x_0 = x0 pinned):
+ *   min  sum_k 1/2 z_k' H z_k + (G yref_k)' z_k  +  1/2 x_N' He x_N + (Ge yref_N)' x_N
+ *   s.t. x_{k+1} = A x_k + B u_k + c,   lb_k <= z_k <= ub_k  (|bound| >= 1e20: absent)
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NZMAX 32
+#define INFB 1e20
+
+typedef struct {
+    int nx, nu, N, ny, ny_e;
+    const double *A, *B, *c;    /* row-major nx*nx, nx*nu, nx */
+    const double *H, *G;        /* nz*nz, nz*ny (stage cost, already scaled) */
+    const double *He, *Ge;      /* nx*nx, nx*ny_e */
+    const double *lb0, *ub0;    /* nz (x part ignored) */
+    const double *lb, *ub;      /* nz, stages 1..N-1 */
+    const double *lbe, *ube;    /* nx, stage N */
+    double tol_comp, tol_res, mu0;
+    int max_iter;
+} ocp_ref_desc;
+
+static int has(double b) { return fabs(b) < INFB; }
+
+/* per-instance workspace sizes */
+typedef struct {
+    double *z, *ll, *lu, *dza, *dz, *gc, *gf, *gh, *re, *Pr, *Luu, *Lxu, *lu_vec;
+} ws_t;
+
+static void interior(double *v, double l, double u)
+{
+    if (has(l) && has(u)) {
+        double d = 0.01 * (u - l);
+        if (*v < l + d) *v = l + d;
+        if (*v > u - d) *v = u - d;
+    } else if (has(l)) {
+        double d = 0.01 * (fabs(l) > 1.0 ? fabs(l) : 1.0);
+        if (*v < l + d) *v = l + d;
+    } else if (has(u)) {
+        double d = 0.01 * (fabs(u) > 1.0 ? fabs(u) : 1.0);
+        if (*v > u - d) *v = u - d;
+    }
+}
+
+/* bound accessors: stage k, component i */
+static double LBk(const ocp_ref_desc *d, int k, int i)
+{
+    if (k == d->N) return d->lbe[i];
+    if (k == 0) return i < d->nx ? -1e30 : d->lb0[i];
+    return d->lb[i];
+}
+static double UBk(const ocp_ref_desc *d, int k, int i)
+{
+    if (k == d->N) return d->ube[i];
+    if (k == 0) return i < d->nx ? 1e30 : d->ub0[i];
+    return d->ub[i];
+}
+
+static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref,
+                     double *xo, double *uo, int *iters_out, ws_t *w)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ny = d->ny;
+    const double *A = d->A, *B = d->B, *c = d->c;
+    double P[NZMAX * NZMAX], M[NZMAX * NZMAX], F[NZMAX * NZMAX], p[NZMAX], v[NZMAX], h[NZMAX];
+    int k, i, j, l, it, status = 2, m = 0;
+
+    /* stage widths: stage k<N has nz comps, stage N has nx */
+#define Z(k, i) w->z[(k) * nz + (i)]
+#define LL(k, i) w->ll[(k) * nz + (i)]
+#define LU(k, i) w->lu[(k) * nz + (i)]
+    /* constant gradient part g_k = G yref_k */
+    for (k = 0; k <= N; k++) {
+        int n = k < N ? nz : nx;
+        const double *Gm = k < N ? d->G : d->Ge;
+        int nyk = k < N ? ny : d->ny_e;
+        const double *y = yref + (size_t)k * ny;
+        for (i = 0; i < n; i++) {
+            double s = 0.0;
+            for (j = 0; j < nyk; j++) s += Gm[i * nyk + j] * y[j];
+            w->gc[k * nz + i] = s;
+        }
+    }
+    /* initial point: reference projected strictly inside the boxes, x0 pinned */
+    for (k = 0; k <= N; k++) {
+        int n = k < N ? nz : nx;
+        const double *y = yref + (size_t)k * ny;
+        for (i = 0; i < n; i++) {
+            double val = y[i];   /* LINEAR_LS with Vx=[I;0], Vu=[0;I] layout: y = [x;u] */
+            if (k < N ? (i < ny) : (i < d->ny_e)) val = y[i]; else val = 0.0;
+            interior(&val, LBk(d, k, i), UBk(d, k, i));
+            Z(k, i) = val;
+        }
+        for (i = n; i < nz; i++) Z(k, i) = 0.0;
+    }
+    for (i = 0; i < nx; i++) Z(0, i) = x0[i];
+    for (k = 0; k <= N; k++) {
+        int n = k < N ? nz : nx;
+        for (i = 0; i < nz; i++) { LL(k, i) = 0.0; LU(k, i) = 0.0; }
+        for (i = 0; i < n; i++) {
+            if (k == 0 && i < nx) continue;
+            double lbv = LBk(d, k, i), ubv = UBk(d, k, i);
+            if (has(lbv)) { LL(k, i) = d->mu0 / (Z(k, i) - lbv); m++; }
+            if (has(ubv)) { LU(k, i) = d->mu0 / (ubv - Z(k, i)); m++; }
+        }
+    }
+    /* gradient of the objective at z */
+#define GRADF(k, out) do { \
+        int n_ = (k) < N ? nz : nx; const double *Hm_ = (k) < N ? d->H : d->He; \
+        for (int a_ = 0; a_ < n_; a_++) { double s_ = w->gc[(k) * nz + a_]; \
+            for (int b_ = 0; b_ < n_; b_++) s_ += Hm_[a_ * n_ + b_] * Z(k, b_); (out)[a_] = s_; } \
+    } while (0)
+    /* initial residual scale r0 = max(|r_d|, |r_e|) with pi = 0 */
+    double r0 = 0.0;
+    for (k = 0; k <= N; k++) {
+        double g[NZMAX];
+        int n = k < N ? nz : nx;
+        GRADF(k, g);
+        for (i = (k == 0 ? nx : 0); i < n; i++) {
+            double r = fabs(g[i] - LL(k, i) + LU(k, i));
+            if (r > r0) r0 = r;
+        }
+    }
+    for (k = 0; k < N; k++)
+        for (i = 0; i < nx; i++) {
+            double s = c[i] - Z(k + 1, i);
+            for (j = 0; j < nx; j++) s += A[i * nx + j] * Z(k, j);
+            for (j = 0; j < nu; j++) s += B[i * nu + j] * Z(k, nx + j);
+            if (fabs(s) > r0) r0 = fabs(s);
+        }
+    double theta = 1.0;
+    if (m == 0) m = 1;
+
+    for (it = 0; it < d->max_iter; it++) {
+        /* complementarity measure */
+        double mu = 0.0;
+        for (k = 0; k <= N; k++) {
+            int n = k < N ? nz : nx;
+            for (i = 0; i < n; i++) {
+                if (LL(k, i) > 0.0) mu += LL(k, i) * (Z(k, i) - LBk(d, k, i));
+                if (LU(k, i) > 0.0) mu += LU(k, i) * (UBk(d, k, i) - Z(k, i));
+            }
+        }
+        mu /= m;
+        if (!isfinite(mu) || !isfinite(theta)) { status = 4; break; }
+        if (mu <= d->tol_comp && theta * r0 <= d->tol_res) { status = 0; break; }
+
+        /* objective gradient gf, dynamics residual re */
+        for (k = 0; k <= N; k++) GRADF(k, &w->gf[k * nz]);
+        for (k = 0; k < N; k++)
+            for (i = 0; i < nx; i++) {
+                double s = c[i] - Z(k + 1, i);
+                for (j = 0; j < nx; j++) s += A[i * nx + j] * Z(k, j);
+                for (j = 0; j < nu; j++) s += B[i * nu + j] * Z(k, nx + j);
+                w->re[k * nx + i] = s;
+            }
+        /* ---- backward factorisation (+ predictor vector) ---- */
+        for (i = 0; i < nx; i++) {
+            for (j = 0; j < nx; j++) P[i * nx + j] = d->He[i * nx + j];
+            double lbv = LBk(d, N, i), ubv = UBk(d, N, i);
+            if (LL(N, i) > 0.0) P[i * nx + i] += LL(N, i) / (Z(N, i) - lbv);
+            if (LU(N, i) > 0.0) P[i * nx + i] += LU(N, i) / (ubv - Z(N, i));
+            p[i] = w->gf[N * nz + i];
+        }
+        for (k = N - 1; k >= 0; k--) {
+            double *Pr = &w->Pr[k * nx], *Luu = &w->Luu[k * nu * nu], *Lxu = &w->Lxu[k * nx * nu];
+            double *luv = &w->lu_vec[k * nu];
+            for (i = 0; i < nx; i++) {
+                double s = 0.0;
+                for (j = 0; j < nx; j++) s += P[i * nx + j] * w->re[k * nx + j];
+                Pr[i] = s;
+                v[i] = s + p[i];
+            }
+            /* M = P [A B]  (nx x nz) */
+            for (i = 0; i < nx; i++)
+                for (j = 0; j < nz; j++) {
+                    double s = 0.0;
+                    for (l = 0; l < nx; l++)
+                        s += P[i * nx + l] * (j < nx ? A[l * nx + j] : B[l * nu + (j - nx)]);
+                    M[i * nz + j] = s;
+                }
+            /* F = [A B]' M + H + Sigma ; h = [A B]' v + gf */
+            for (i = 0; i < nz; i++) {
+                for (j = 0; j < nz; j++) {
+                    double s = d->H[i * nz + j];
+                    for (l = 0; l < nx; l++)
+                        s += (i < nx ? A[l * nx + i] : B[l * nu + (i - nx)]) * M[l * nz + j];
+                    F[i * nz + j] = s;
+                }
+                double s = w->gf[k * nz + i];
+                for (l = 0; l < nx; l++) s += (i < nx ? A[l * nx + i] : B[l * nu + (i - nx)]) * v[l];
+                h[i] = s;
+                if (k == 0 && i < nx) continue;
+                if (LL(k, i) > 0.0) F[i * nz + i] += LL(k, i) / (Z(k, i) - LBk(d, k, i));
+                if (LU(k, i) > 0.0) F[i * nz + i] += LU(k, i) / (UBk(d, k, i) - Z(k, i));
+            }
+            /* Luu = chol(F_uu) (row-major lower) */
+            for (i = 0; i < nu; i++)
+                for (j = 0; j <= i; j++) {
+                    double s = F[(nx + i) * nz + nx + j];
+                    for (l = 0; l < j; l++) s -= Luu[i * nu + l] * Luu[j * nu + l];
+                    if (i == j) {
+                        if (!(s > 0.0)) { status = 4; goto done; }
+                        Luu[i * nu + i] = sqrt(s);
+                    } else {
+                        Luu[i * nu + j] = s / Luu[j * nu + j];
+                    }
+                }
+            /* Lxu = F_xu Luu^-T  (row i: forward substitution) */
+            for (i = 0; i < nx; i++)
+                for (j = 0; j < nu; j++) {
+                    double s = F[i * nz + nx + j];
+                    for (l = 0; l < j; l++) s -= Lxu[i * nu + l] * Luu[j * nu + l];
+                    Lxu[i * nu + j] = s / Luu[j * nu + j];
+                }
+            /* l_u = Luu^-1 h_u */
+            for (j = 0; j < nu; j++) {
+                double s = h[nx + j];
+                for (l = 0; l < j; l++) s -= Luu[j * nu + l] * luv[l];
+                luv[j] = s / Luu[j * nu + j];
+            }
+            if (k > 0) {
+                for (i = 0; i < nx; i++) {
+                    for (j = 0; j < nx; j++) {
+                        double s = F[i * nz + j];
+                        for (l = 0; l < nu; l++) s -= Lxu[i * nu + l] * Lxu[j * nu + l];
+                        P[i * nx + j] = s;
+                    }
+                    double s = h[i];
+                    for (l = 0; l < nu; l++) s -= Lxu[i * nu + l] * luv[l];
+                    p[i] = s;
+                }
+            }
+        }
+        /* ---- forward substitution: direction into out[] ---- */
+#define FORWARD(out) do { \
+        double dx_[NZMAX]; for (i = 0; i < nx; i++) dx_[i] = 0.0; \
+        for (k = 0; k < N; k++) { \
+            const double *Luu_ = &w->Luu[k * nu * nu], *Lxu_ = &w->Lxu[k * nx * nu], *lu_ = &w->lu_vec[k * nu]; \
+            double t_[NZMAX]; \
+            for (j = 0; j < nu; j++) { double s_ = lu_[j]; \
+                for (i = 0; i < nx; i++) s_ += Lxu_[i * nu + j] * dx_[i]; t_[j] = s_; } \
+            for (j = nu - 1; j >= 0; j--) { double s_ = t_[j]; \
+                for (l = j + 1; l < nu; l++) s_ -= Luu_[l * nu + j] * t_[l]; t_[j] = s_ / Luu_[j * nu + j]; } \
+            for (i = 0; i < nx; i++) (out)[k * nz + i] = dx_[i]; \
+            for (j = 0; j < nu; j++) (out)[k * nz + nx + j] = -t_[j]; \
+            for (i = 0; i < nx; i++) { double s_ = w->re[k * nx + i]; \
+                for (j = 0; j < nx; j++) s_ += A[i * nx + j] * dx_[j]; \
+                for (j = 0; j < nu; j++) s_ += B[i * nu + j] * (out)[k * nz + nx + j]; \
+                t_[nu + i] = s_; } \
+            for (i = 0; i < nx; i++) dx_[i] = t_[nu + i]; \
+        } \
+        for (i = 0; i < nx; i++) (out)[N * nz + i] = dx_[i]; \
+    } while (0)
+        FORWARD(w->dza);
+
+        /* affine step length and mu_aff */
+        double a_aff = 1.0;
+        for (k = 0; k <= N; k++) {
+            int n = k < N ? nz : nx;
+            for (i = (k == 0 ? nx : 0); i < n; i++) {
+                double dz = w->dza[k * nz + i];
+                if (LL(k, i) > 0.0) {
+                    double t = Z(k, i) - LBk(d, k, i), dl = -LL(k, i) * (1.0 + dz / t);
+                    if (dz < 0.0 && -t / dz < a_aff) a_aff = -t / dz;
+                    if (dl < 0.0 && -LL(k, i) / dl < a_aff) a_aff = -LL(k, i) / dl;
+                }
+                if (LU(k, i) > 0.0) {
+                    double t = UBk(d, k, i) - Z(k, i), dl = -LU(k, i) * (1.0 - dz / t);
+                    if (dz > 0.0 && t / dz < a_aff) a_aff = t / dz;
+                    if (dl < 0.0 && -LU(k, i) / dl < a_aff) a_aff = -LU(k, i) / dl;
+                }
+            }
+        }
+        double mu_aff = 0.0;
+        for (k = 0; k <= N; k++) {
+            int n = k < N ? nz : nx;
+            for (i = (k == 0 ? nx : 0); i < n; i++) {
+                double dz = w->dza[k * nz + i];
+                if (LL(k, i) > 0.0) {
+                    double t = Z(k, i) - LBk(d, k, i), dl = -LL(k, i) * (1.0 + dz / t);
+                    mu_aff += (t + a_aff * dz) * (LL(k, i) + a_aff * dl);
+                }
+                if (LU(k, i) > 0.0) {
+                    double t = UBk(d, k, i) - Z(k, i), dl = -LU(k, i) * (1.0 - dz / t);
+                    mu_aff += (t - a_aff * dz) * (LU(k, i) + a_aff * dl);
+                }
+            }
+        }
+        mu_aff /= m;
+        double sg = mu_aff / mu;
+        double smu = sg * sg * sg * mu;
+        /* corrector gradient gh */
+        for (k = 0; k <= N; k++) {
+            int n = k < N ? nz : nx;
+            for (i = 0; i < n; i++) {
+                double g = w->gf[k * nz + i], dz = w->dza[k * nz + i];
+                if (!(k == 0 && i < nx)) {
+                    if (LL(k, i) > 0.0) {
+                        double t = Z(k, i) - LBk(d, k, i), dl = -LL(k, i) * (1.0 + dz / t);
+                        g += (dl * dz - smu) / t;
+                    }
+                    if (LU(k, i) > 0.0) {
+                        double t = UBk(d, k, i) - Z(k, i), dl = -LU(k, i) * (1.0 - dz / t);
+                        g += (dl * dz + smu) / t;
+                    }
+                }
+                w->gh[k * nz + i] = g;
+            }
+        }
+        /* backward vector pass with gh */
+        for (i = 0; i < nx; i++) p[i] = w->gh[N * nz + i];
+        for (k = N - 1; k >= 0; k--) {
+            const double *Pr = &w->Pr[k * nx], *Luu = &w->Luu[k * nu * nu], *Lxu = &w->Lxu[k * nx * nu];
+            double *luv = &w->lu_vec[k * nu];
+            for (i = 0; i < nx; i++) v[i] = Pr[i] + p[i];
+            for (i = 0; i < nz; i++) {
+                double s = w->gh[k * nz + i];
+                for (l = 0; l < nx; l++) s += (i < nx ? A[l * nx + i] : B[l * nu + (i - nx)]) * v[l];
+                h[i] = s;
+            }
+            for (j = 0; j < nu; j++) {
+                double s = h[nx + j];
+                for (l = 0; l < j; l++) s -= Luu[j * nu + l] * luv[l];
+                luv[j] = s / Luu[j * nu + j];
+            }
+            if (k > 0)
+                for (i = 0; i < nx; i++) {
+                    double s = h[i];
+                    for (l = 0; l < nu; l++) s -= Lxu[i * nu + l] * luv[l];
+                    p[i] = s;
+                }
+        }
+        FORWARD(w->dz);
+        /* dual directions and step length */
+        double alpha = 1.0;
+        for (k = 0; k <= N; k++) {
+            int n = k < N ? nz : nx;
+            for (i = (k == 0 ? nx : 0); i < n; i++) {
+                double dz = w->dz[k * nz + i], dza = w->dza[k * nz + i];
+                if (LL(k, i) > 0.0) {
+                    double t = Z(k, i) - LBk(d, k, i), dla = -LL(k, i) * (1.0 + dza / t);
+                    double dl = (smu - LL(k, i) * t - dla * dza - LL(k, i) * dz) / t;
+                    if (dz < 0.0 && -t / dz < alpha) alpha = -t / dz;
+                    if (dl < 0.0 && -LL(k, i) / dl < alpha) alpha = -LL(k, i) / dl;
+                }
+                if (LU(k, i) > 0.0) {
+                    double t = UBk(d, k, i) - Z(k, i), dla = -LU(k, i) * (1.0 - dza / t);
+                    double dl = (smu - LU(k, i) * t + dla * dza + LU(k, i) * dz) / t;
+                    if (dz > 0.0 && t / dz < alpha) alpha = t / dz;
+                    if (dl < 0.0 && -LU(k, i) / dl < alpha) alpha = -LU(k, i) / dl;
+                }
+            }
+        }
+        alpha *= 0.995;
+        if (alpha > 1.0) alpha = 1.0;
+        for (k = 0; k <= N; k++) {
+            int n = k < N ? nz : nx;
+            for (i = (k == 0 ? nx : 0); i < n; i++) {
+                double dz = w->dz[k * nz + i], dza = w->dza[k * nz + i];
+                if (LL(k, i) > 0.0) {
+                    double t = Z(k, i) - LBk(d, k, i), dla = -LL(k, i) * (1.0 + dza / t);
+                    LL(k, i) += alpha * (smu - LL(k, i) * t - dla * dza - LL(k, i) * dz) / t;
+                }
+                if (LU(k, i) > 0.0) {
+                    double t = UBk(d, k, i) - Z(k, i), dla = -LU(k, i) * (1.0 - dza / t);
+                    LU(k, i) += alpha * (smu - LU(k, i) * t + dla * dza + LU(k, i) * dz) / t;
+                }
+                Z(k, i) += alpha * dz;
+            }
+        }
+        theta *= (1.0 - alpha);
+    }
+done:
+    for (k = 0; k <= N; k++)
+        for (i = 0; i < nx; i++) xo[k * nx + i] = Z(k, i);
+    for (k = 0; k < N; k++)
+        for (j = 0; j < nu; j++) uo[k * nu + j] = Z(k, nx + j);
+    *iters_out = it;
+    return status;
+#undef Z
+#undef LL
+#undef LU
+#undef GRADF
+#undef FORWARD
+}
+
+/* Solve `batch` independent instances. x0: batch*nx; yref: batch*(N*ny + ny_e);
+ * xout: batch*(N+1)*nx; uout: batch*N*nu. nthreads <= 0: OpenMP default.
+ * Returns the number of instances with status != 0. */
+int riccati_ipm_solve_batch(const ocp_ref_desc *d, int batch, const double *x0, const double *yref,
+                            double *xout, double *uout, int *status, int *iters, int nthreads)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu;
+    if (nx + nu > NZMAX || nx < 1 || nu < 1 || N < 1 || d->ny != nz || d->ny_e != nx) return -1;
+    const size_t ystride = (size_t)N * d->ny + d->ny_e;
+    int nfail = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_num_procs();
+#else
+    nthreads = 1;
+#endif
+#pragma omp parallel num_threads(nthreads) reduction(+ : nfail)
+    {
+        size_t S = (size_t)(N + 1) * nz;
+        double *buf = (double *)malloc(sizeof(double) * (8 * S + (size_t)N * (2 * nx + nu * nu + nx * nu + nu)));
+        ws_t w;
+        w.z = buf; w.ll = w.z + S; w.lu = w.ll + S; w.dza = w.lu + S; w.dz = w.dza + S;
+        w.gc = w.dz + S; w.gf = w.gc + S; w.gh = w.gf + S;
+        w.re = w.gh + S; w.Pr = w.re + (size_t)N * nx; w.Luu = w.Pr + (size_t)N * nx;
+        w.Lxu = w.Luu + (size_t)N * nu * nu; w.lu_vec = w.Lxu + (size_t)N * nx * nu;
+#pragma omp for schedule(dynamic, 16)
+        for (int b = 0; b < batch; b++) {
+            int st = solve_one(d, x0 + (size_t)b * nx, yref + (size_t)b * ystride,
+                               xout + (size_t)b * (N + 1) * nx, uout + (size_t)b * N * nu,
+                               &iters[b], &w);
+            status[b] = st;
+            if (st != 0) nfail++;
+        }
+        free(buf);
+    }
+    return nfail;
+}
+
+int riccati_ipm_max_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_num_procs();
+#else
+    return 1;
+#endif
+}

@@ -1,0 +1,108 @@
+"""Generate QP / closed-loop golden vectors from the CPU oracle (oracle/).
+
+    python tests/golden/make_qp_golden.py
+
+Inputs are seeded synthetic instances built on the reference's own circle table
+(tests/golden/circle_ref.npz, generated from generate_trajectory.py by make_golden.py) and
+the seed-42 noise stream (main.py:44). Expected outputs are the oracle's KKT-certified
+exact QP solutions (oracle/qp.py) and its closed-loop restatement (oracle/closed_loop.py).
+These fixtures pin the HIP engine to the oracle; the oracle itself is pinned to the
+reference through the fixtures of make_golden.py (acados is absent: QP parity vs acados
+is unpinned).
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import closed_loop as CL  # noqa: E402
+from oracle import models, qp  # noqa: E402
+
+CASES = [("force", 20), ("force", 30), ("jerk", 40), ("jerk", 30), ("quad13", 20)]
+PER_CASE = 48
+
+
+def reference_table(name, N):
+    refs = np.load(os.path.join(HERE, "circle_ref.npz"))
+    base = refs[f"nh{N}_nx6"] if f"nh{N}_nx6" in refs else None
+    if name == "force":
+        return base[:, :4], base[:, 4:6]
+    if name == "jerk":
+        return base[:, :6], base[:, 6:]
+    r = models.quad13_reference(500, N)
+    return r[:, :13], r[:, 13:]
+
+
+def perturbed_x0(name, xr, t, rng):
+    x0 = xr[t].copy()
+    x0[:2] += rng.normal(0, 0.05, 2)
+    if name == "force":
+        x0[2:4] += rng.normal(0, 0.1, 2)
+        x0[2:4] = np.clip(x0[2:4], -0.95, 0.95)
+    elif name == "jerk":
+        x0[2:4] += rng.normal(0, 0.1, 2)
+        x0[2:4] = np.clip(x0[2:4], -0.95, 0.95)
+        x0[4:6] += rng.normal(0, 0.3, 2)
+    else:
+        x0[2] += rng.normal(0, 0.1)
+        x0[3:6] += rng.normal(0, 0.1, 3)
+        x0[3:6] = np.clip(x0[3:6], -0.9, 0.9)
+        x0[7:10] += rng.normal(0, 0.02, 3)
+        x0[10:13] += rng.normal(0, 0.2, 3)
+    x0[:2] = np.clip(x0[:2], -1.15, 1.15)
+    return x0
+
+
+def main():
+    out = {}
+    rng = np.random.default_rng(20251121)
+    for name, N in CASES:
+        spec = models.MODELS[name](N)
+        xr, ur = reference_table(name, N)
+        X0, Y, XS, US, COST = [], [], [], [], []
+        while len(X0) < PER_CASE:
+            t = int(rng.integers(0, 500))
+            x0 = perturbed_x0(name, xr, t, rng)
+            yref, yref_e = qp.yref_window(xr, ur, t, N)
+            sol = qp.solve_ocp(spec, x0, yref, yref_e)
+            if not sol["certified"]:
+                continue
+            X0.append(x0)
+            Y.append(np.concatenate([yref.ravel(), yref_e]))
+            XS.append(sol["X"])
+            US.append(sol["U"])
+            COST.append(sol["cost"])
+        key = f"{name}_N{N}"
+        out[key + "_x0"] = np.array(X0)
+        out[key + "_yref"] = np.array(Y)
+        out[key + "_X"] = np.array(XS)
+        out[key + "_U"] = np.array(US)
+        out[key + "_cost"] = np.array(COST)
+        print(key, "done")
+    np.savez_compressed(os.path.join(HERE, "qp_cases.npz"), **out)
+
+    # closed loops of main.py (seed 42 noise stream, x0 = [1, 0, 0, 0.62]), first 60 steps
+    noise = np.load(os.path.join(HERE, "noise_seed42.npy"))
+    cl = {}
+    for N in (20, 30):
+        refs = np.load(os.path.join(HERE, "circle_ref.npz"))
+        ref = refs[f"nh{N}_nx6"]
+        x0 = np.array([1.0, 0, 0, 0.62])
+        ns = CL.NoiseStream(noise)
+        c, X, a, Up, Uc = CL.force_follow_trajectory(models.force_model(N), ref[:, :4], ref[:, 4:6], x0, ns,
+                                                     n_steps=60)
+        cl[f"force_N{N}_X"], cl[f"force_N{N}_U"], cl[f"force_N{N}_Uplant"], cl[f"force_N{N}_cost"] = X, Uc, Up, c
+        c, X, a, Up, Uc = CL.jerk_follow_trajectory(models.jerk_model(N), ref[:, :6], ref[:, 6:], x0, ns,
+                                                    n_steps=60)
+        cl[f"jerk_N{N}_X"], cl[f"jerk_N{N}_U"], cl[f"jerk_N{N}_Uplant"], cl[f"jerk_N{N}_cost"] = X, Uc, Up, c
+        cl[f"jerk_N{N}_a"] = a
+        cl[f"noise_used_N{N}"] = np.array(ns.i)
+    np.savez_compressed(os.path.join(HERE, "closed_loop.npz"), **cl)
+    print("wrote qp_cases.npz, closed_loop.npz")
+
+
+if __name__ == "__main__":
+    main()

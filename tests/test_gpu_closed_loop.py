@@ -1,0 +1,41 @@
+"""GPU closed-loop parity: the reference's follow_trajectory loops (force/jerk) driven through
+the façade (every QP solve and plant step on the GPU) against the oracle's restatement
+(tests/golden/closed_loop.npz: first 60 steps of main.py, seed-42 noise, x0=[1,0,0,0.62])."""
+import os
+
+import numpy as np
+import pytest
+
+from drone_attitude_control_amd import controllers
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def data(golden_dir):
+    return (np.load(os.path.join(golden_dir, "closed_loop.npz")),
+            np.load(os.path.join(golden_dir, "noise_seed42.npy")),
+            np.load(os.path.join(golden_dir, "circle_ref.npz")))
+
+
+def stream(noise):
+    it = iter(noise)
+    return lambda: float(next(it))
+
+
+@pytest.mark.parametrize("N", [20, 30])
+def test_force_and_jerk_closed_loop(data, N):
+    cl, noise, refs = data
+    ref = refs[f"nh{N}_nx6"]
+    draw = stream(noise)
+    x0 = np.array([1.0, 0, 0, 0.62])
+    c, X, a, Up = controllers.force_follow_trajectory(ref[:, :4], ref[:, 4:6], x0, draw, verbose=False,
+                                                      N=N, n_steps=60)
+    assert np.abs(X - cl[f"force_N{N}_X"]).max() < 1e-6
+    assert np.abs(Up - cl[f"force_N{N}_Uplant"]).max() < 1e-6
+    assert c == pytest.approx(float(cl[f"force_N{N}_cost"]), rel=1e-6)
+    c, X, a, Up = controllers.jerk_follow_trajectory(ref[:, :6], ref[:, 6:], x0, draw, verbose=False,
+                                                     N=N, n_steps=60)
+    assert np.abs(X - cl[f"jerk_N{N}_X"]).max() < 1e-6
+    assert np.abs(a - cl[f"jerk_N{N}_a"]).max() < 1e-6
+    assert c == pytest.approx(float(cl[f"jerk_N{N}_cost"]), rel=1e-6)

@@ -1,0 +1,173 @@
+"""CPU tests: the oracle against the reference's golden vectors, and self-consistency.
+
+The golden params / circle table / noise stream come from the reference's own modules
+(tests/golden/make_golden.py). The QP fixtures come from the oracle and are re-derived
+here so a change in the oracle shows up as a test failure.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import closed_loop as CL
+from oracle import cref, models, qp, trajectory
+from oracle import params as P
+
+
+def test_params_match_reference(golden_dir):
+    g = json.load(open(os.path.join(golden_dir, "params.json")))
+    assert P.MASS == g["MASS"] and P.GRAVITY_ACC == g["GRAVITY_ACC"]
+    assert P.GRAVITY == pytest.approx(g["GRAVITY"], rel=0, abs=0)
+    assert P.MAX_F == g["max_F"] and P.MIN_F == g["min_F"]
+    for k in ("min_p_x", "max_p_x", "min_p_z", "max_p_z", "min_v_x", "max_v_x", "min_v_z", "max_v_z",
+              "min_a_x", "max_a_x", "min_a_z", "max_a_z", "min_jerk", "max_jerk"):
+        assert getattr(P, k.upper()) == g[k], k
+    assert (P.T, P.DT, P.DT_CONV, P.CTRLS_PER_SAMPLE) == (g["T"], g["dt"], g["dt_conv"], g["ctrls_per_sample"])
+    assert (P.N_SIM, P.N_HORIZON, P.NOISE) == (g["N"], g["N_horizon"], g["noise"])
+    assert (P.L_ARM, P.KF, P.KM, P.THRUST2WEIGHT) == (g["L"], g["KF"], g["KM"], g["THRUST2WEIGHT_RATIO"])
+    assert tuple(P.J_DIAG) == tuple(g["J_diag"])
+
+
+def test_product_params_match_reference(golden_dir):
+    from drone_attitude_control_amd.params import DroneData, ExperimentParameters
+    g = json.load(open(os.path.join(golden_dir, "params.json")))
+    dd, p = DroneData(), ExperimentParameters()
+    assert (dd.MASS, dd.GRAVITY, dd.max_F, dd.min_F, dd.min_a_z, dd.max_a_z) == (
+        g["MASS"], g["GRAVITY"], g["max_F"], g["min_F"], g["min_a_z"], g["max_a_z"])
+    assert (p.T, p.dt, p.dt_conv, p.ctrls_per_sample, p.N, p.N_horizon, p.noise) == (
+        g["T"], g["dt"], g["dt_conv"], g["ctrls_per_sample"], g["N"], g["N_horizon"], g["noise"])
+
+
+@pytest.mark.parametrize("nh", [20, 30, 40])
+@pytest.mark.parametrize("nx", [4, 6])
+def test_circle_traj_bit_exact(golden_dir, nh, nx):
+    ref = np.load(os.path.join(golden_dir, "circle_ref.npz"))[f"nh{nh}_nx{nx}"]
+    mine = trajectory.gen_circle_traj(500, nh, nx, 2)
+    assert mine.shape == ref.shape
+    assert np.array_equal(mine, ref)
+    from drone_attitude_control_amd.models import gen_circle_traj
+    assert np.array_equal(gen_circle_traj(500, nh, nx, 2), ref)
+
+
+def test_circle_traj_quirks(golden_dir):
+    ref = np.load(os.path.join(golden_dir, "circle_ref.npz"))["nh30_nx6"]
+    assert np.allclose(ref[499], ref[0], atol=1e-12)      # linspace endpoint == start
+    assert np.array_equal(ref[500:], ref[:30])             # horizon padding copies the head
+    assert ref[0, 5] == pytest.approx(-0.0 + P.GRAVITY_ACC, abs=1e-12)
+
+
+def test_discretisation_exact():
+    # force: IRK (Gauss-Legendre) on a nilpotent generator == exact ZOH
+    s = models.force_model(20)
+    h, m = P.DT, P.MASS
+    A = np.eye(4)
+    A[0, 2] = A[1, 3] = h
+    B = np.array([[h * h / (2 * m), 0], [0, h * h / (2 * m)], [h / m, 0], [0, h / m]])
+    c = np.array([0, -P.GRAVITY_ACC * h * h / 2, 0, -P.GRAVITY_ACC * h])
+    assert np.allclose(s.A, A, atol=1e-15) and np.allclose(s.B, B, rtol=1e-13) and np.allclose(s.c, c, rtol=1e-13)
+    # jerk: ERK 1 stage == explicit Euler
+    j = models.jerk_model(20)
+    assert np.allclose(j.A, np.eye(6) + h * j.A_c) and np.allclose(j.B, h * j.B_c) and np.allclose(j.c, h * j.c_c)
+
+
+def test_product_discretisation_matches_oracle():
+    """The library computes the integrator sensitivities natively (Butcher collocation);
+    check them against the oracle's closed form without a GPU via a tiny ctypes-free path:
+    the façade's affine extraction + the oracle's expm must agree with the C++ tableau,
+    which is exercised on the GPU box by test_gpu_solver.test_discrete_model."""
+    from drone_attitude_control_amd.acados import affine_form
+    from drone_attitude_control_amd.models import OCPS
+    for name in ("force", "jerk", "quad13"):
+        ocp = OCPS[name](20)
+        A, B, c = affine_form(ocp.model)
+        spec = models.MODELS[name](20)
+        assert np.array_equal(A, spec.A_c) and np.array_equal(B, spec.B_c) and np.array_equal(c, spec.c_c)
+
+
+@pytest.mark.parametrize("key", ["force_N20", "force_N30", "jerk_N40", "jerk_N30", "quad13_N20"])
+def test_qp_golden_recertified(golden_dir, key):
+    """Re-solve a few golden instances with the dense oracle; check KKT certificates."""
+    d = np.load(os.path.join(golden_dir, "qp_cases.npz"))
+    name, N = key.split("_N")
+    N = int(N)
+    spec = models.MODELS[name](N)
+    for b in range(0, d[key + "_x0"].shape[0], 12):
+        y = d[key + "_yref"][b]
+        sol = qp.solve_ocp(spec, d[key + "_x0"][b], y[:N * spec.ny].reshape(N, spec.ny), y[N * spec.ny:])
+        assert sol["certified"], sol["kkt"]
+        assert np.allclose(sol["U"], d[key + "_U"][b], atol=1e-9)
+        assert np.allclose(sol["X"], d[key + "_X"][b], atol=1e-9)
+
+
+def test_qp_oracle_edge_cases():
+    spec = models.force_model(20)
+    ref = trajectory.gen_circle_traj(500, 20, 6, 2)
+    # perturbed above the circle: the input saturates exactly on its lower bound
+    y, ye = qp.yref_window(ref[:, :4], ref[:, 4:6], 100, 20)
+    sol = qp.solve_ocp(spec, ref[100, :4] + 0.05, y, ye)
+    assert sol["certified"]
+    assert np.min(sol["U"]) == pytest.approx(P.MIN_F, abs=1e-12)
+    assert np.all(sol["U"] <= P.MAX_F + 1e-12)
+    # starting exactly on a state bound
+    x0 = np.array([1.2, 0.0, 0.0, 0.5])
+    sol = qp.solve_ocp(spec, x0, y, ye)
+    assert sol["certified"]
+    assert np.all(sol["X"][1:-1, 0] <= 1.2 + 1e-9)
+
+
+@pytest.mark.parametrize("key", ["force_N20", "jerk_N40", "quad13_N20"])
+def test_c_riccati_matches_oracle(golden_dir, key):
+    """The plain-C Riccati IPM (CPU baseline, same algorithm as the HIP kernel) against the
+    KKT-certified dense oracle: 1e-6 relative on the x/u trajectories."""
+    d = np.load(os.path.join(golden_dir, "qp_cases.npz"))
+    name, N = key.split("_N")
+    spec = models.MODELS[name](int(N))
+    R = cref.RiccatiIpmRef(spec)
+    X, U, st, it = R.solve(d[key + "_x0"], d[key + "_yref"])
+    assert (st == 0).all()
+    scale = np.maximum(1.0, np.maximum(np.abs(d[key + "_X"]).max(axis=(1, 2)), np.abs(d[key + "_U"]).max(axis=(1, 2))))
+    err = np.maximum(np.abs(X - d[key + "_X"]).max(axis=(1, 2)), np.abs(U - d[key + "_U"]).max(axis=(1, 2)))
+    assert (err / scale).max() < 1e-6, (err / scale).max()
+    assert it.max() < 50
+
+
+def test_c_riccati_threads_deterministic(golden_dir):
+    d = np.load(os.path.join(golden_dir, "qp_cases.npz"))
+    spec = models.force_model(20)
+    R = cref.RiccatiIpmRef(spec)
+    x0 = np.repeat(d["force_N20_x0"], 4, axis=0)
+    y = np.repeat(d["force_N20_yref"], 4, axis=0)
+    X1, U1, _, _ = R.solve(x0, y, nthreads=1)
+    X4, U4, _, _ = R.solve(x0, y, nthreads=4)
+    assert np.array_equal(U1, U4) and np.array_equal(X1, X4)
+
+
+def test_closed_loop_oracle_matches_golden(golden_dir):
+    d = np.load(os.path.join(golden_dir, "closed_loop.npz"))
+    noise = np.load(os.path.join(golden_dir, "noise_seed42.npy"))
+    ref = trajectory.gen_circle_traj(500, 20, 6, 2)
+    ns = CL.NoiseStream(noise)
+    c, X, a, Up, Uc = CL.force_follow_trajectory(models.force_model(20), ref[:, :4], ref[:, 4:6],
+                                                 np.array([1.0, 0, 0, 0.62]), ns, n_steps=60)
+    assert np.allclose(X, d["force_N20_X"], atol=1e-9) and c == pytest.approx(float(d["force_N20_cost"]), rel=1e-9)
+
+
+def test_converters_and_plant():
+    # force converter (force_model/dynamics.py:65-70)
+    th, Fd = CL.force_convert(np.array([0.1, 0.3]))
+    assert th == pytest.approx(np.arctan2(0.1, 0.3)) and Fd == pytest.approx(np.hypot(0.1, 0.3))
+    # jerk converter: sequential adds, 10 sub-steps (jerk_model/dynamics.py:76-82)
+    u, a = CL.jerk_convert(np.array([1.0, -2.0]), [0.0, P.GRAVITY_ACC])
+    a_ref = np.array([0.0, P.GRAVITY_ACC])
+    for _ in range(10):
+        a_ref = a_ref + np.array([1.0, -2.0]) * P.DT_CONV
+    assert np.array_equal(a, a_ref) and u.shape == (10, 2)
+    # RK4 is exact for the constant-acceleration plant
+    x = np.array([0.1, 0.2, 0.3, -0.4])
+    uu = np.array([0.2, 0.35])
+    acc = np.array([uu[1] * np.sin(uu[0]) / P.MASS, uu[1] * np.cos(uu[0]) / P.MASS - P.GRAVITY_ACC])
+    h = P.DT
+    exact = np.concatenate([x[:2] + x[2:] * h + 0.5 * acc * h * h, x[2:] + acc * h])
+    assert np.allclose(CL.rk4_step(x, uu, h), exact, atol=1e-14)
+    assert CL.calc_aed(np.ones((3, 2)), np.zeros((3, 2))) == 1.0
