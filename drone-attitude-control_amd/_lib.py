@@ -45,6 +45,23 @@ class OcpDesc(ctypes.Structure):
     ]
 
 
+NMPC_PLANT_MODEL, NMPC_PLANT_CRAZYFLIE_FORCE, NMPC_PLANT_CRAZYFLIE_JERK = 0, 1, 2
+
+
+class ClosedLoopDesc(ctypes.Structure):
+    _fields_ = [
+        ("plant", ctypes.c_int), ("ref_table", _dp),
+        ("ref_rows", ctypes.c_int), ("ref_cols", ctypes.c_int), ("ref_period", ctypes.c_int),
+        ("offsets", ctypes.POINTER(ctypes.c_int32)), ("x_init", _dp),
+        ("instance_base", ctypes.c_longlong), ("seed", ctypes.c_ulonglong),
+        ("noise_std", ctypes.c_double), ("noise_dims", ctypes.c_int),
+        ("noise_table", _dp), ("noise_len", ctypes.c_int),
+        ("cost_stage", ctypes.c_int), ("ncl", ctypes.c_int), ("w_cl", _dp), ("aed_dims", ctypes.c_int),
+        ("mass", ctypes.c_double), ("g", ctypes.c_double), ("dt", ctypes.c_double), ("dt_conv", ctypes.c_double),
+        ("substeps", ctypes.c_int),
+    ]
+
+
 # every symbol include/nmpc.h declares, with (restype, argtypes)
 SIGNATURES = {
     "nmpc_abi_version": (ctypes.c_int, []),
@@ -70,6 +87,10 @@ SIGNATURES = {
     "nmpc_get_cost": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _dp]),
     "nmpc_get_stats": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_int]),
     "nmpc_get_launch_info": (ctypes.c_int, [ctypes.c_void_p, _ip, ctypes.c_int]),
+    "nmpc_closed_loop_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ClosedLoopDesc)]),
+    "nmpc_closed_loop_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "nmpc_closed_loop_stats": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_int]),
+    "nmpc_closed_loop_get_state": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_size_t]),
     "nmpc_sim_plant": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                       ctypes.c_double, _dp, _dp, _dp]),
 }

@@ -211,6 +211,15 @@ struct nmpc_solver {
     int *d_status = nullptr, *d_iters = nullptr;
     size_t off_AB = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
     std::vector<float> tmp_x0f, tmp_yf;
+    // closed loop
+    bool cl_ready = false;
+    nmpc_closed_loop_desc cl{};
+    void *d_table = nullptr, *d_state = nullptr, *d_plant = nullptr, *d_wcl = nullptr;
+    int *d_offsets = nullptr;
+    double *d_acc = nullptr, *d_noise = nullptr;
+    int cl_step = 0, cl_last_launches = 0;
+    std::vector<hipEvent_t> cl_events;
+    double cl_last_ms = 0.0;
     double cost_s = 1.0;  // stage cost factor (time step or 1)
 
     size_t ystride() const { return (size_t)N * ny + ny_e; }
@@ -234,15 +243,17 @@ void free_all(nmpc_solver *h)
 {
     hipSetDevice(h->device);
     for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
-                    (void *)h->d_iters})
+                    (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
+                    (void *)h->d_acc, (void *)h->d_noise})
         if (p) hipFree(p);
+    for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
 }
 
 template <typename T>
-int launch(nmpc_solver *h)
+int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
     nmpc::IpmParams<T> p;
     p.B = h->batch;
@@ -271,9 +282,9 @@ int launch(nmpc_solver *h)
     p.status = h->d_status;
     p.iters = h->d_iters;
     p.scratch = (T *)h->d_scratch;
-    hipEventRecord(h->ev0, h->stream);
+    hipEventRecord(e0 ? e0 : h->ev0, h->stream);
     hipError_t e = nmpc::ipm_launch<T>(h->kidx, p, h->stream);
-    hipEventRecord(h->ev1, h->stream);
+    hipEventRecord(e1 ? e1 : h->ev1, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "ipm kernel launch");
     return 0;
 }
@@ -879,6 +890,216 @@ int nmpc_sim_plant(int device, int batch, int num_stages, double T, double mass,
         g_err = std::string("nmpc_sim_plant: ") + hipGetErrorString(e);
         return NMPC_EDEVICE;
     }
+    return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+nmpc::ClParams<T> cl_params(nmpc_solver *h)
+{
+    nmpc::ClParams<T> p{};
+    const nmpc_closed_loop_desc &d = h->cl;
+    p.B = h->batch;
+    p.N = h->N;
+    p.ny = h->ny;
+    p.ny_e = h->ny_e;
+    p.nx = h->nx;
+    p.nu = h->nu;
+    p.plant = d.plant;
+    p.period = d.ref_period;
+    p.table_cols = d.ref_cols;
+    p.step = h->cl_step;
+    p.cost_stage = d.cost_stage;
+    p.ncl = d.ncl;
+    p.aed_dims = d.aed_dims;
+    p.noise_dims = d.noise_dims;
+    p.substeps = d.substeps;
+    p.inst_base = d.instance_base;
+    p.seed = d.seed;
+    p.noise_std = d.noise_std;
+    p.mass = d.mass;
+    p.g = d.g;
+    p.dt = d.dt;
+    p.dt_conv = d.dt_conv;
+    p.table = (const T *)h->d_table;
+    p.offset = h->d_offsets;
+    p.state = (T *)h->d_state;
+    p.x0 = (T *)h->d_x0;
+    p.yref = (T *)h->d_yref;
+    p.xout = (const T *)h->d_x;
+    p.uout = (const T *)h->d_u;
+    p.status = h->d_status;
+    const T *pm = (const T *)h->d_plant;
+    p.A = pm;
+    p.Bm = pm + h->nx * h->nx;
+    p.c = pm + h->nx * h->nx + h->nx * h->nu;
+    p.wcl = (const T *)h->d_wcl;
+    p.noise_table = h->d_noise;
+    p.noise_len = d.noise_len;
+    p.acc = h->d_acc;
+    return p;
+}
+
+template <typename T>
+int cl_step_enqueue(nmpc_solver *h, int launch_idx)
+{
+    nmpc::ClParams<T> p = cl_params<T>(h);
+    hipError_t e = nmpc::cl_prepare_launch<T>(p, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "closed-loop prepare");
+    const int r = launch<T>(h, h->cl_events[2 * launch_idx], h->cl_events[2 * launch_idx + 1]);
+    if (r < 0) return r;
+    e = nmpc::cl_advance_launch<T>(p, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "closed-loop advance");
+    h->cl_step++;
+    return 0;
+}
+
+hipError_t put_typed(void *dst, const double *src, size_t n, bool f64)
+{
+    if (f64) return hipMemcpy(dst, src, n * sizeof(double), hipMemcpyHostToDevice);
+    std::vector<float> t(src, src + n);
+    return hipMemcpy(dst, t.data(), n * sizeof(float), hipMemcpyHostToDevice);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d)
+{
+    if (!h || !d) return NMPC_EINVAL;
+    if (!d->ref_table || !d->offsets || !d->x_init || d->ref_rows < 1 || d->ref_period < 1)
+        return h->fail(NMPC_EINVAL, "nmpc_closed_loop_init: table, offsets and x_init are required");
+    if (d->ref_cols < std::max(h->ny, h->ny_e) || d->ref_cols < d->ncl || d->ref_cols < d->aed_dims)
+        return h->fail(NMPC_EINVAL, "nmpc_closed_loop_init: ref_cols too small for ny / ny_e / ncl");
+    if (d->ref_period - 1 + h->N >= d->ref_rows)
+        return h->fail(NMPC_EINVAL, "nmpc_closed_loop_init: ref_rows must cover ref_period - 1 + N");
+    if (d->plant < 0 || d->plant > 2) return h->fail(NMPC_EINVAL, "nmpc_closed_loop_init: unknown plant");
+    if (d->plant == NMPC_PLANT_CRAZYFLIE_FORCE && (h->nx != 4 || h->nu != 2))
+        return h->fail(NMPC_EINVAL, "force plant needs the force controller model (nx=4, nu=2)");
+    if (d->plant == NMPC_PLANT_CRAZYFLIE_JERK && (h->nx != 6 || h->nu != 2))
+        return h->fail(NMPC_EINVAL, "jerk plant needs the jerk controller model (nx=6, nu=2)");
+    if (h->nx > 32) return h->fail(NMPC_EUNSUPPORTED, "closed loop supports nx <= 32");
+    if (d->ncl > h->nx || d->aed_dims > h->nx || d->cost_stage < 0 || d->cost_stage > h->N)
+        return h->fail(NMPC_EINVAL, "nmpc_closed_loop_init: ncl / aed_dims / cost_stage out of range");
+    for (int b = 0; b < h->batch; b++)
+        if (d->offsets[b] < 0) return h->fail(NMPC_EINVAL, "nmpc_closed_loop_init: negative offset");
+    hipSetDevice(h->device);
+    const bool f64 = h->precision == NMPC_FP64;
+    const size_t es = h->esz();
+    for (void **p : {&h->d_table, &h->d_state, &h->d_plant, &h->d_wcl, (void **)&h->d_offsets, (void **)&h->d_acc,
+                     (void **)&h->d_noise})
+        if (*p) {
+            hipFree(*p);
+            *p = nullptr;
+        }
+    const int nx = h->nx, nu = h->nu;
+    bool ok = hipMalloc(&h->d_table, (size_t)d->ref_rows * d->ref_cols * es) == hipSuccess &&
+              hipMalloc(&h->d_state, (size_t)h->batch * nx * es) == hipSuccess &&
+              hipMalloc(&h->d_plant, (size_t)(nx * nx + nx * nu + nx) * es) == hipSuccess &&
+              hipMalloc(&h->d_wcl, (size_t)std::max(d->ncl, 1) * es) == hipSuccess &&
+              hipMalloc((void **)&h->d_offsets, (size_t)h->batch * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_acc, (size_t)h->batch * 4 * sizeof(double)) == hipSuccess;
+    if (ok && d->noise_table && d->noise_len > 0)
+        ok = hipMalloc((void **)&h->d_noise, (size_t)h->batch * d->noise_len * sizeof(double)) == hipSuccess;
+    if (!ok) return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: device allocation failed");
+    std::vector<double> plant(h->A);
+    plant.insert(plant.end(), h->B.begin(), h->B.end());
+    plant.insert(plant.end(), h->c.begin(), h->c.end());
+    std::vector<double> w(std::max(d->ncl, 1), 0.0);
+    for (int i = 0; i < d->ncl; i++) w[i] = d->w_cl ? d->w_cl[i] : 1.0;
+    hipError_t e = put_typed(h->d_table, d->ref_table, (size_t)d->ref_rows * d->ref_cols, f64);
+    if (e == hipSuccess) e = put_typed(h->d_state, d->x_init, (size_t)h->batch * nx, f64);
+    if (e == hipSuccess) e = put_typed(h->d_plant, plant.data(), plant.size(), f64);
+    if (e == hipSuccess) e = put_typed(h->d_wcl, w.data(), w.size(), f64);
+    if (e == hipSuccess) e = hipMemcpy(h->d_offsets, d->offsets, h->batch * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(h->d_acc, 0, (size_t)h->batch * 4 * sizeof(double));
+    if (e == hipSuccess && h->d_noise)
+        e = hipMemcpy(h->d_noise, d->noise_table, (size_t)h->batch * d->noise_len * sizeof(double),
+                      hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init upload");
+    h->cl = *d;
+    h->cl.ref_table = nullptr;
+    h->cl.offsets = nullptr;
+    h->cl.x_init = nullptr;
+    h->cl.noise_table = nullptr;
+    h->cl.w_cl = nullptr;
+    h->cl_step = 0;
+    h->cl_ready = true;
+    return 0;
+}
+
+int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
+{
+    if (!h) return NMPC_EINVAL;
+    if (!h->cl_ready) return h->fail(NMPC_ESTATE, "nmpc_closed_loop_run: call nmpc_closed_loop_init first");
+    if (steps < 0) return h->fail(NMPC_EINVAL, "nmpc_closed_loop_run: steps < 0");
+    hipSetDevice(h->device);
+    while ((int)h->cl_events.size() < 2 * steps) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return h->fail(NMPC_EDEVICE, "hipEventCreate");
+        h->cl_events.push_back(e);
+    }
+    h->out_valid = false;
+    for (int s = 0; s < steps; s++) {
+        const int r = h->precision == NMPC_FP64 ? cl_step_enqueue<double>(h, s) : cl_step_enqueue<float>(h, s);
+        if (r < 0) return r;
+    }
+    h->cl_last_launches = steps;
+    if (sync) {
+        hipError_t e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_run");
+    }
+    return 0;
+}
+
+int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
+{
+    if (!h || !out) return NMPC_EINVAL;
+    if (!h->cl_ready) return h->fail(NMPC_ESTATE, "nmpc_closed_loop_stats: closed loop not initialised");
+    hipSetDevice(h->device);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_stats");
+    std::vector<double> acc((size_t)h->batch * 4);
+    hipMemcpy(acc.data(), h->d_acc, acc.size() * sizeof(double), hipMemcpyDeviceToHost);
+    double v[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int b = 0; b < h->batch; b++)
+        for (int j = 0; j < 4; j++) v[j] += acc[(size_t)b * 4 + j];
+    double ms = 0.0;
+    for (int s = 0; s < h->cl_last_launches; s++) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, h->cl_events[2 * s], h->cl_events[2 * s + 1]) == hipSuccess) ms += t;
+    }
+    v[4] = ms;
+    v[5] = h->cl_last_launches;
+    std::vector<int32_t> it(h->batch);
+    hipMemcpy(it.data(), h->d_iters, h->batch * sizeof(int32_t), hipMemcpyDeviceToHost);
+    double mean = 0.0;
+    for (int b = 0; b < h->batch; b++) mean += it[b];
+    v[6] = mean / h->batch;
+    for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+    return 0;
+}
+
+int nmpc_closed_loop_get_state(nmpc_solver *h, double *out, size_t count)
+{
+    if (!h || !out) return NMPC_EINVAL;
+    if (!h->cl_ready) return h->fail(NMPC_ESTATE, "nmpc_closed_loop_get_state: closed loop not initialised");
+    if (count != (size_t)h->batch * h->nx) return h->fail(NMPC_EINVAL, "nmpc_closed_loop_get_state: size mismatch");
+    hipSetDevice(h->device);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_get_state");
+    if (h->precision == NMPC_FP64) {
+        e = hipMemcpy(out, h->d_state, count * sizeof(double), hipMemcpyDeviceToHost);
+    } else {
+        std::vector<float> t(count);
+        e = hipMemcpy(t.data(), h->d_state, count * sizeof(float), hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < count; i++) out[i] = t[i];
+    }
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_get_state");
     return 0;
 }
 

@@ -42,6 +42,37 @@ int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out);
 template <typename T>
 hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s);
 
+// closed-loop step kernels (nmpc_closed_loop.hip)
+template <typename T>
+struct ClParams {
+    int B, N, ny, ny_e, nx, nu;
+    int plant;        // 0 controller model, 1 Crazyflie + force converter, 2 Crazyflie + jerk converter
+    int period;       // reference rows per period (start row = (offset + step) % period)
+    int table_cols;
+    int step;
+    int cost_stage;   // X_opt = x_{cost_stage} (0: force_model/controller.py:39, 1: jerk :39)
+    int ncl, aed_dims, noise_dims, substeps;
+    long long inst_base;
+    unsigned long long seed;
+    double noise_std, mass, g, dt, dt_conv;
+    const T *table;   // [rows][table_cols]
+    const int *offset;
+    T *state;         // [B][nx]
+    T *x0;            // engine input [B][nx]
+    T *yref;          // engine input [B][N*ny + ny_e]
+    const T *xout, *uout;
+    const int *status;
+    const T *A, *Bm, *c;   // plant == 0
+    const T *wcl;     // [ncl]
+    const double *noise_table;   // optional [B][noise_len] (replaces Philox draws)
+    int noise_len;
+    double *acc;      // [B][4] cost, aed numerator, failures, steps
+};
+template <typename T>
+hipError_t cl_prepare_launch(const ClParams<T> &p, hipStream_t s);
+template <typename T>
+hipError_t cl_advance_launch(const ClParams<T> &p, hipStream_t s);
+
 // plant simulator (nmpc_plant.hip)
 hipError_t plant_step_launch(int batch, int num_stages, double T, double mass, double g,
                              const double *x_in, const double *u, double *x_out, hipStream_t s);

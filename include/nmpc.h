@@ -23,7 +23,7 @@
  *     [ext: ocp_nlp_out_get(..., "u")]
  *   ocp_solver.get_cost(), print_statistics()              nmpc_get_cost(), nmpc_get_stats()
  *     force_model/ocp.py:164, force_model/controller.py:34
- *   AcadosSimSolver.set/solve/get (plant step)             nmpc_sim_step()
+ *   AcadosSimSolver.set/solve/get (plant step)             nmpc_sim_plant()
  *     force_model/ocp.py:108-112, jerk_model/ocp.py:110-113
  *
  * Every handle carries a batch dimension: `instance` selects one of `batch` independent
@@ -177,6 +177,47 @@ int nmpc_get_stats(nmpc_solver *h, double *stats, int n);
 /* kernel geometry chosen for this handle: out[0] = instances per wavefront,
  * out[1] = workgroups per launch, out[2] = threads per workgroup, out[3] = LDS bytes/WG */
 int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n);
+
+/* ------------------------------------------------------------------ batched closed loop
+ * On-device closed loop around the solve: every step builds each instance's
+ * yref window from a shared reference table (set_up_ocp, force_model/ocp.py:117-122), pins
+ * x0 = current state, solves, accumulates the closed-loop cost (controller.py:40-41) and the
+ * AED numerator (store_results.py:233-236), and advances the plant with one scalar noise draw
+ * per step (ocp.py:114). Instances never exchange data; results are independent of sharding. */
+#define NMPC_PLANT_MODEL 0           /* the controller's own discrete model x+ = A x + B u0 + c */
+#define NMPC_PLANT_CRAZYFLIE_FORCE 1 /* src/plant.py, force converter, ERK4 over dt */
+#define NMPC_PLANT_CRAZYFLIE_JERK 2  /* src/plant.py, jerk converter, substeps x Euler over dt_conv */
+
+typedef struct nmpc_closed_loop_desc {
+    int plant;
+    const double *ref_table; /* ref_rows x ref_cols; yref_k = row[t+k][0:ny], yref_N = row[t+N][0:ny_e] */
+    int ref_rows, ref_cols, ref_period; /* start row t = (offset + step) % ref_period */
+    const int32_t *offsets;  /* batch start rows */
+    const double *x_init;    /* batch*nx initial states (controller state: plant state [+ acceleration]) */
+    long long instance_base; /* global id of this handle's instance 0 (noise stream key) */
+    unsigned long long seed;
+    double noise_std;
+    int noise_dims;            /* NMPC_PLANT_MODEL: noise added to the first noise_dims states */
+    const double *noise_table; /* optional batch*noise_len draws used instead of Philox (parity runs) */
+    int noise_len;
+    int cost_stage;            /* closed-loop cost on x_{cost_stage} of the solution (force 0, jerk 1) */
+    int ncl;
+    const double *w_cl;        /* ncl diagonal weights of the closed-loop cost */
+    int aed_dims;              /* AED over the first aed_dims state components */
+    double mass, g, dt, dt_conv;
+    int substeps;
+} nmpc_closed_loop_desc;
+
+/* bind the closed loop to a solver handle (allocates the table/state/accumulators on the device) */
+int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d);
+/* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion */
+int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync);
+/* out[0] sum closed-loop cost, out[1] sum AED numerator, out[2] failed solves, out[3] instance-steps,
+ * out[4] total device ms of the solve kernel over the last run (HIP events around each launch),
+ * out[5] solve launches in the last run, out[6] mean qp_iter of the last step */
+int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n);
+/* current closed-loop states, batch*nx */
+int nmpc_closed_loop_get_state(nmpc_solver *h, double *out, size_t count);
 
 /* plant simulator (AcadosSimSolver for src/plant.py:27-43): one step of the nonlinear 2-D
  * Crazyflie plant x=[px,pz,vx,vz], u=[theta, F_d] on the device for `batch` states.

@@ -415,7 +415,7 @@ int riccati_ipm_solve_batch(const ocp_ref_desc *d, int batch, const double *x0, 
     const size_t ystride = (size_t)N * d->ny + d->ny_e;
     int nfail = 0;
 #ifdef _OPENMP
-    if (nthreads <= 0) nthreads = omp_get_num_procs();
+    if (nthreads <= 0) nthreads = omp_get_max_threads(); /* honours OMP_NUM_THREADS */
 #else
     nthreads = 1;
 #endif
@@ -444,7 +444,7 @@ int riccati_ipm_solve_batch(const ocp_ref_desc *d, int batch, const double *x0, 
 int riccati_ipm_max_threads(void)
 {
 #ifdef _OPENMP
-    return omp_get_num_procs();
+    return omp_get_max_threads();
 #else
     return 1;
 #endif

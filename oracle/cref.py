@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "c", "riccati_ipm.c")
 LIB = os.path.join(HERE, "build", "libriccati_ipm.so")
 # x86-64-v3 (AVX2+FMA) runs on both this container's Xeon and the GPU box's EPYC hosts
-CFLAGS = ["-O3", "-march=x86-64-v3", "-ffp-contract=off", "-fopenmp", "-shared", "-fPIC", "-std=c99"]
+CFLAGS = ["-O3", "-march=x86-64-v3", "-fopenmp", "-shared", "-fPIC", "-std=c99"]
 
 
 def build(force=False):
@@ -84,9 +84,15 @@ class RiccatiIpmRef:
                           tol_comp, tol_res, mu0, max_iter)
 
     def max_threads(self):
-        return self.lib.riccati_ipm_max_threads()
+        """Host threads this process may use: the CPU affinity mask, capped by OMP_NUM_THREADS
+        (the GPU box exports 16 = its CPU share although nproc shows the whole machine)."""
+        n = len(os.sched_getaffinity(0))
+        env = os.environ.get("OMP_NUM_THREADS")
+        if env and env.isdigit() and int(env) > 0:
+            n = min(n, int(env))
+        return max(1, n)
 
-    def solve(self, x0, yref, nthreads=0):
+    def solve(self, x0, yref, nthreads=None):
         """x0: (B, nx); yref: (B, N*ny + ny_e). Returns X (B,N+1,nx), U (B,N,nu), status, iters."""
         sp = self.spec
         x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, sp.nx)
@@ -100,7 +106,8 @@ class RiccatiIpmRef:
         rc = self.lib.riccati_ipm_solve_batch(
             ctypes.byref(self.desc), B, ctypes.c_void_p(x0.ctypes.data), ctypes.c_void_p(yref.ctypes.data),
             ctypes.c_void_p(X.ctypes.data), ctypes.c_void_p(U.ctypes.data),
-            ctypes.c_void_p(st.ctypes.data), ctypes.c_void_p(it.ctypes.data), int(nthreads))
+            ctypes.c_void_p(st.ctypes.data), ctypes.c_void_p(it.ctypes.data),
+            int(nthreads) if nthreads else self.max_threads())
         if rc < 0:
             raise ValueError("riccati_ipm_solve_batch rejected the problem dimensions")
         return X, U, st, it

