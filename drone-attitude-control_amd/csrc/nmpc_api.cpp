@@ -192,7 +192,7 @@ struct nmpc_solver {
     std::string name, err;
     int device = 0, precision = NMPC_FP64, batch = 0;
     int nx = 0, nu = 0, N = 0, ny = 0, ny_e = 0;
-    int kidx = -1, ipw = 1, lds = 0, yref_is_z = 0;
+    int kidx = -1, ipw = 1, wpb = 1, lds = 0, yref_is_z = 0;
     int max_iter = 50;
     double tol_comp = 0, tol_res = 0, mu0 = 0, inv_m = 1, ts = 0, scale_e = 1;
     hipStream_t own_stream = nullptr, stream = nullptr;
@@ -351,8 +351,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
 
     int ipw_req = 0;
     if (const char *e = std::getenv("NMPC_IPW")) ipw_req = std::atoi(e);
-    h->kidx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, -1, &h->ipw, &h->lds)
-                                     : nmpc::ipm_find<float>(nx, nu, -1, &h->ipw, &h->lds);
+    h->kidx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, -1, &h->ipw, &h->lds, &h->wpb)
+                                     : nmpc::ipm_find<float>(nx, nu, -1, &h->ipw, &h->lds, &h->wpb);
     if (h->kidx < 0) {
         std::string msg = "nmpc_create: no compiled kernel for nx=" + std::to_string(nx) + " nu=" + std::to_string(nu);
         delete h;
@@ -364,8 +364,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         int cand[4] = {8, 4, 2, 1}, chosen = -1;
         for (int ipw : cand) {
             int ip, ld;
-            const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw, &ip, &ld)
-                                                   : nmpc::ipm_find<float>(nx, nu, ipw, &ip, &ld);
+            const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw, &ip, &ld, nullptr)
+                                                   : nmpc::ipm_find<float>(nx, nu, ipw, &ip, &ld, nullptr);
             if (idx < 0) continue;
             if (chosen < 0) chosen = ipw;  // widest compiled
             if ((batch + ipw - 1) / ipw >= 2048) {
@@ -377,8 +377,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         ipw_req = chosen;
     }
     {
-        const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw_req, &h->ipw, &h->lds)
-                                               : nmpc::ipm_find<float>(nx, nu, ipw_req, &h->ipw, &h->lds);
+        const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw_req, &h->ipw, &h->lds, &h->wpb)
+                                               : nmpc::ipm_find<float>(nx, nu, ipw_req, &h->ipw, &h->lds, &h->wpb);
         if (idx >= 0) h->kidx = idx;
     }
 
@@ -557,8 +557,9 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
     const size_t model_bytes = off;
-    const size_t ngroups = (size_t)(batch + h->ipw - 1) / h->ipw;
-    const size_t scratch_bytes = ngroups * h->ipw * nmpc::scratch_elems_per_instance(N, nx, nu) * es;
+    const size_t per_wg = (size_t)h->ipw * h->wpb;
+    const size_t nslots = ((size_t)batch + per_wg - 1) / per_wg * per_wg;   // tail wavefronts included
+    const size_t scratch_bytes = nslots * nmpc::scratch_elems_per_instance(N, nx, nu) * es;
     bool ok = hipMalloc(&h->d_model, model_bytes) == hipSuccess &&
               hipMalloc(&h->d_x0, (size_t)batch * nx * es) == hipSuccess &&
               hipMalloc(&h->d_yref, (size_t)batch * h->ystride() * es) == hipSuccess &&
@@ -860,7 +861,8 @@ int nmpc_get_stats(nmpc_solver *h, double *st, int n)
 int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
 {
     if (!h || !out) return NMPC_EINVAL;
-    const int v[4] = {h->ipw, (h->batch + h->ipw - 1) / h->ipw, 64, h->lds};
+    const int waves = (h->batch + h->ipw - 1) / h->ipw;
+    const int v[4] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds};
     for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
     return 0;
 }

@@ -30,15 +30,16 @@ struct IpmParams {
     T *uout;        // [B][N][nu]
     int *status;    // [B]
     int *iters;     // [B]
-    T *scratch;     // [ceil(B/IPW)*IPW][scratch_elems_per_instance]
+    T *scratch;     // [ceil(B/(IPW*WPB))*IPW*WPB][scratch_elems_per_instance]
 };
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);
 
-// returns an index into the kernel table (or -1), the chosen instances-per-wave and the
-// static LDS bytes per workgroup. ipw_req <= 0 picks the widest packing compiled.
+// returns an index into the kernel table (or -1), the chosen instances-per-wave, the
+// static LDS bytes per workgroup and the wavefronts per workgroup. ipw_req <= 0 picks the
+// widest packing compiled. Scratch must cover ceil(B / (ipw*wpb)) * ipw * wpb instances.
 template <typename T>
-int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out);
+int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_out);
 template <typename T>
 hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s);
 
