@@ -228,15 +228,16 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
         clb[(e / NZ) * LDZ + e % NZ] = p.lbnd[e];
         cub[(e / NZ) * LDZ + e % NZ] = p.ubnd[e];
     }
-    T abcol[NX];
+    // column `col` of [A B]: re-read from LDS where it is used (a register copy kept across
+    // all sweeps would cost 2*NX VGPRs at the kernel's register peak)
+    auto load_abcol = [&](T (&ac)[NX]) {
 #pragma unroll
-    for (int l = 0; l < NX; l++) abcol[l] = p.AB[l * NZ + col];
+        for (int l = 0; l < NX; l++) ac[l] = cab[l * LDZ + col];
+    };
     __syncthreads();
     if (!__any(inst_ok)) return;   // tail wavefront of the last workgroup: nothing to solve
     // bounds of this lane's component for the three stage types (0, 1..N-1, N)
     const int lc = ll < NZ ? ll : 0;
-    const T lb0 = clb[lc], lb1 = clb[LDZ + lc], lb2 = clb[2 * LDZ + lc];
-    const T ub0 = cub[lc], ub1 = cub[LDZ + lc], ub2 = cub[2 * LDZ + lc];
 
     const ScratchLayout L(N, NX, NU);
     // wave-uniform bases (SGPRs) + 32-bit lane offsets: global loads take the saddr form
@@ -252,8 +253,8 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
     const T *x0 = p.x0 + (size_t)inst * NX;
     const int nel = (N + 1) * NZ;
     auto stype = [&](int k) { return k == 0 ? 0 : (k == N ? 2 : 1); };
-    auto LBR = [&](int k) { return k == 0 ? lb0 : (k == N ? lb2 : lb1); };
-    auto UBR = [&](int k) { return k == 0 ? ub0 : (k == N ? ub2 : ub1); };
+    auto LBR = [&](int k) { return clb[stype(k) * LDZ + lc]; };
+    auto UBR = [&](int k) { return cub[stype(k) * LDZ + lc]; };
 
     // ------------------------------------------------------------------ initial point
     for (int e = ll; e < nel; e += G) {
@@ -380,18 +381,17 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
     struct Pre {
         T z, l, u, dz, dza, gc;
     };
+    // Prefetches are unconditional (no phi at a branch join, so the compiler does not drain
+    // vmcnt there); lanes / stages outside the valid range read harmless data or, past the
+    // end of the buffer resource, zeros.
     auto prefetch_a = [&](int k, Pre &q) {
-        if (k >= 0 && ll < nzk(k)) {
-            const unsigned e = k * NZ;
-            q.z = S.ld(Lz + e, ll);
-            q.l = S.ld(Lll + e, ll);
-            q.u = S.ld(Llu + e, ll);
-            q.gc = S.ld(Lgc + e, ll);
-            if (pending) {
-                q.dz = S.ld(Ldz + e, ll);
-                q.dza = S.ld(Ldza + e, ll);
-            }
-        }
+        const unsigned e = (unsigned)(k < 0 ? 0 : k) * NZ;
+        q.z = S.ld(Lz + e, ll);
+        q.l = S.ld(Lll + e, ll);
+        q.u = S.ld(Llu + e, ll);
+        q.gc = S.ld(Lgc + e, ll);
+        q.dz = S.ld(Ldz + e, ll);
+        q.dza = S.ld(Ldza + e, ll);
     };
 
     // forward sweep shared by predictor (corr = false) and corrector (corr = true);
@@ -404,23 +404,18 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
         // stage-0 data; every later stage is fetched one stage ahead (K after its last use)
         T krow[NX], kff = 0, re = 0, z = 0, lam_l = 0, lam_u = 0, dza = 0;
         auto fetch_k = [&](int k) {
-            if (ll < NU) {
 #pragma unroll
-                for (int i = 0; i < NX; i++) krow[i] = S.ld(Lkst + k * NU * NX + i, ll * NX);
-            }
+            for (int i = 0; i < NX; i++) krow[i] = S.ld(Lkst + k * NU * NX + i, ll * NX);
         };
         auto fetch_v = [&](int k, T &kf, T &r, T &zz, T &la, T &lu, T &da) {
-            if (k < N) {
-                if (ll < NU) kf = S.ld(Lkff + k * NU, ll);
-                if (ll < NX) r = S.ld(Lre + k * NX, ll);
-            }
-            if (ll < nzk(k)) {
-                const unsigned e = k * NZ;
-                zz = S.ld(Lz + e, ll);
-                la = S.ld(Lll + e, ll);
-                lu = S.ld(Llu + e, ll);
-                if (corr) da = S.ld(Ldza + e, ll);
-            }
+            const unsigned kk = (unsigned)(k < N ? k : N - 1);
+            kf = S.ld(Lkff + kk * NU, ll);
+            r = S.ld(Lre + kk * NX, ll);
+            const unsigned e = k * NZ;
+            zz = S.ld(Lz + e, ll);
+            la = S.ld(Lll + e, ll);
+            lu = S.ld(Llu + e, ll);
+            da = S.ld(Ldza + e, ll);
         };
         fetch_k(0);
         fetch_v(0, kff, re, z, lam_l, lam_u, dza);
@@ -439,7 +434,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                     for (int i = 0; i < NX; i++) s += krow[i] * dxc[i];
                     du_l[ll] = s;
                 }
-                if (k + 1 < N) fetch_k(k + 1);
+                fetch_k(k + 1 < N ? k + 1 : N - 1);
                 WAVE_SYNC();
                 if (ll < NX) {
                     T s = re;
@@ -550,7 +545,6 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
             WAVE_SYNC();
             stage_p2(N - 1, gc_km1, zreg_k, greg);
             WAVE_SYNC();
-            T freg[RF];
             for (int k = N - 1; k >= 0; k--) {
                 const int b = k & 1;
                 const T *rv = w + Gm::I_RV + b * LDX;
@@ -559,6 +553,8 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                 Pre qk{};
                 prefetch_a(k - 1, qk);
                 // B: Pr = P re, v = Pr + p, M^T = (P [A B])^T
+                T abcol[NX];
+                load_abcol(abcol);
                 if (ll < NX) {
                     T s = 0;
 #pragma unroll
@@ -567,7 +563,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                     vv[ll] = s + pv[ll];
                 }
                 if (gridl) {
-#pragma unroll
+#pragma unroll 1
                     for (int qq = 0; qq < RM; qq++) {
                         const int i = rg + R * qq;
                         if (i < NX) {
@@ -581,7 +577,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                 WAVE_SYNC();
                 // C: F = [A B]' M + H + Sigma (row col), h = [A B]' v + g
                 if (gridl) {
-#pragma unroll
+#pragma unroll 1
                     for (int qq = 0; qq < RF; qq++) {
                         const int bb = rg + R * qq;
                         if (bb < NZ) {
@@ -589,7 +585,6 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
 #pragma unroll
                             for (int l = 0; l < NX; l++) s += abcol[l] * mt[bb * LDX + l];
                             if (bb == col) s += sv[col];
-                            freg[qq] = s;
                             fp[col * LDZ + bb] = s;
                         }
                     }
@@ -661,11 +656,11 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                         T fu[NU];
 #pragma unroll
                         for (int u = 0; u < NU; u++) fu[u] = fp[col * LDZ + NX + u];
-#pragma unroll
+#pragma unroll 1
                         for (int qq = 0; qq < RF; qq++) {
                             const int i = rg + R * qq;
                             if (i < NX) {
-                                T s = freg[qq];
+                                T s = fp[col * LDZ + i];   // F_xx entry, overwritten in place by P
 #pragma unroll
                                 for (int u = 0; u < NU; u++) s += fu[u] * kl[u * LDX + i];
                                 fp[col * LDZ + i] = s;
@@ -710,16 +705,14 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                 T gf, z, l, u, dza, pr;
             };
             auto fetch_c = [&](int k, PreC &q) {
-                if (k < 0) return;
-                if (ll < nzk(k)) {
-                    const unsigned e = k * NZ;
-                    q.gf = S.ld(Lgf + e, ll);
-                    q.z = S.ld(Lz + e, ll);
-                    q.l = S.ld(Lll + e, ll);
-                    q.u = S.ld(Llu + e, ll);
-                    q.dza = S.ld(Ldza + e, ll);
-                }
-                if (k < N && ll < NX) q.pr = S.ld(Lpr + k * NX, ll);
+                const unsigned kc_ = (unsigned)(k < 0 ? 0 : k);
+                const unsigned e = kc_ * NZ;
+                q.gf = S.ld(Lgf + e, ll);
+                q.z = S.ld(Lz + e, ll);
+                q.l = S.ld(Lll + e, ll);
+                q.u = S.ld(Llu + e, ll);
+                q.dza = S.ld(Ldza + e, ll);
+                q.pr = S.ld(Lpr + (kc_ < (unsigned)N ? kc_ : N - 1) * NX, ll);
             };
             PreC qN{};
             fetch_c(N, qN);
@@ -728,14 +721,14 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
             fetch_c(N - 1, q);
             WAVE_SYNC();
             for (int k = N - 1; k >= 0; k--) {
+                T abcol[NX];
+                load_abcol(abcol);
                 // this stage's factors (used two phases later) and the next stage's vectors
                 T lf[NUT], kc[NU];
 #pragma unroll
                 for (int j = 0; j < NUT; j++) lf[j] = S.ld(Lfinv + k * NUT + j, 0);
-                if (ll < NX) {
 #pragma unroll
-                    for (int u = 0; u < NU; u++) kc[u] = S.ld(Lkst + k * NU * NX + u * NX, ll);
-                }
+                for (int u = 0; u < NU; u++) kc[u] = S.ld(Lkst + k * NU * NX + u * NX, ll);
                 PreC qn{};
                 fetch_c(k - 1, qn);
                 T greg = 0;
@@ -831,7 +824,9 @@ static const IpmEntry<T> *table(int *n)
     static const IpmEntry<T> t[] = {
         entry<T, 4, 2, 1, 4>(), entry<T, 4, 2, 2, 4>(), entry<T, 4, 2, 4, 4>(), entry<T, 4, 2, 8, 4>(),
         entry<T, 6, 2, 1, 4>(), entry<T, 6, 2, 2, 4>(), entry<T, 6, 2, 4, 4>(),
-        entry<T, 13, 4, 1, 4>(), entry<T, 13, 4, 1, 1, 2>(), entry<T, 13, 4, 1, 1, 3>(),
+        // quad13: the first entry is the default (measured fastest, profiles/); the rest are
+        // selectable with NMPC_VARIANT for tuning runs
+        entry<T, 13, 4, 1, 1, 3>(), entry<T, 13, 4, 1, 4>(), entry<T, 13, 4, 1, 1, 2>(),
         entry<T, 13, 4, 1, 4, 3>(),
     };
     *n = (int)(sizeof(t) / sizeof(t[0]));
