@@ -77,6 +77,36 @@ __device__ __forceinline__ T group_max(T v)
     return v;
 }
 
+// init + sum_l a(l) b(l) with two interleaved accumulators: halves the dependent-FMA
+// chain of the stage products, which are latency- rather than throughput-bound
+template <int N, typename T, typename FA, typename FB>
+__device__ __forceinline__ T dot2(T init, FA a, FB b)
+{
+    T s0 = init, s1 = T(0);
+#pragma unroll
+    for (int l = 0; l + 1 < N; l += 2) {
+        s0 = fma(a(l), b(l), s0);
+        s1 = fma(a(l + 1), b(l + 1), s1);
+    }
+    if constexpr (N % 2) s0 = fma(a(N - 1), b(N - 1), s0);
+    return s0 + s1;
+}
+
+// 1/sqrt(x) for x > 0: hardware estimate + two Newton steps (no IEEE sqrt scaling path)
+__device__ __forceinline__ double frsq(double x)
+{
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = fma(y, fma(-h, y * y, 0.5), y);
+    y = fma(y, fma(-h, y * y, 0.5), y);
+    return y;
+}
+__device__ __forceinline__ float frsq(float x)
+{
+    float y = __builtin_amdgcn_rsqf(x);
+    return fmaf(y, fmaf(-0.5f * x, y * y, 0.5f), y);
+}
+
 template <typename T>
 __device__ __forceinline__ bool has_bound(T b)
 {
@@ -359,21 +389,18 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
     auto stage_p2 = [&](int k, T gc, T zprev, T &greg) {
         const T *zv = w + Gm::I_ZV + (k & 1) * LDZ;
         if (ll < nzk(k)) {
-            T g = gc;
+            T g;
             if (k < N) {
-#pragma unroll
-                for (int b = 0; b < NZ; b++) g += (ch[ll * LDZ + b]) * zv[b];
+                g = dot2<NZ>(gc, [&](int b) { return ch[ll * LDZ + b]; }, [&](int b) { return zv[b]; });
             } else {
-#pragma unroll
-                for (int b = 0; b < NX; b++) g += (che[ll * LDX + b]) * zv[b];
+                g = dot2<NX>(gc, [&](int b) { return che[ll * LDX + b]; }, [&](int b) { return zv[b]; });
             }
             greg = g;
             S.st(Lgf + k * NZ, ll, g);
         }
         if (k < N && ll < NX) {
-            T r = (cc[ll]) - zprev;
-#pragma unroll
-            for (int j = 0; j < NZ; j++) r += (cab[ll * LDZ + j]) * zv[j];
+            const T r = dot2<NZ>(cc[ll] - zprev, [&](int j) { return cab[ll * LDZ + j]; },
+                                 [&](int j) { return zv[j]; });
             w[Gm::I_RV + (k & 1) * LDX + ll] = r;
             S.st(Lre + k * NX, ll, r);
         }
@@ -429,20 +456,13 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                 fetch_v(k + 1, kff_n, re_n, z_n, ll_n, lu_n, dza_n);
                 // du = kff + K dx
                 if (ll < NU) {
-                    T s = kff;
-#pragma unroll
-                    for (int i = 0; i < NX; i++) s += krow[i] * dxc[i];
-                    du_l[ll] = s;
+                    du_l[ll] = dot2<NX>(kff, [&](int i) { return krow[i]; }, [&](int i) { return dxc[i]; });
                 }
                 fetch_k(k + 1 < N ? k + 1 : N - 1);
                 WAVE_SYNC();
                 if (ll < NX) {
-                    T s = re;
-#pragma unroll
-                    for (int j = 0; j < NX; j++) s += (cab[ll * LDZ + j]) * dxc[j];
-#pragma unroll
-                    for (int j = 0; j < NU; j++) s += (cab[ll * LDZ + NX + j]) * du_l[j];
-                    dxn[ll] = s;
+                    dxn[ll] = dot2<NZ>(re, [&](int j) { return cab[ll * LDZ + j]; },
+                                       [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
                 }
             }
             // stage k direction component + ratio test / sums
@@ -556,9 +576,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                 T abcol[NX];
                 load_abcol(abcol);
                 if (ll < NX) {
-                    T s = 0;
-#pragma unroll
-                    for (int l = 0; l < NX; l++) s += fp[ll * LDZ + l] * rv[l];
+                    const T s = dot2<NX>(T(0), [&](int l) { return fp[ll * LDZ + l]; }, [&](int l) { return rv[l]; });
                     S.st(Lpr + k * NX, ll, s);
                     vv[ll] = s + pv[ll];
                 }
@@ -567,10 +585,8 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                     for (int qq = 0; qq < RM; qq++) {
                         const int i = rg + R * qq;
                         if (i < NX) {
-                            T s = 0;
-#pragma unroll
-                            for (int l = 0; l < NX; l++) s += fp[i * LDZ + l] * abcol[l];
-                            mt[col * LDX + i] = s;
+                            mt[col * LDX + i] = dot2<NX>(T(0), [&](int l) { return fp[i * LDZ + l]; },
+                                                         [&](int l) { return abcol[l]; });
                         }
                     }
                 }
@@ -581,18 +597,14 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                     for (int qq = 0; qq < RF; qq++) {
                         const int bb = rg + R * qq;
                         if (bb < NZ) {
-                            T s = (ch[col * LDZ + bb]);
-#pragma unroll
-                            for (int l = 0; l < NX; l++) s += abcol[l] * mt[bb * LDX + l];
+                            T s = dot2<NX>(ch[col * LDZ + bb], [&](int l) { return abcol[l]; },
+                                           [&](int l) { return mt[bb * LDX + l]; });
                             if (bb == col) s += sv[col];
                             fp[col * LDZ + bb] = s;
                         }
                     }
                     if (rg == 0) {
-                        T s = greg;
-#pragma unroll
-                        for (int l = 0; l < NX; l++) s += abcol[l] * vv[l];
-                        hv[col] = s;
+                        hv[col] = dot2<NX>(greg, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
                     }
                 }
                 WAVE_SYNC();
@@ -607,11 +619,9 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
 #pragma unroll
                         for (int l = 0; l < j; l++) s -= lf[tri(i, l)] * lf[tri(j, l)];
                         if (i == j) {
-                            if (!(s > T(0))) {
-                                fail = fail || active;
-                                s = T(1);
-                            }
-                            lf[tri(i, i)] = frcp(sqrt(s));
+                            const bool pd = s > T(0);
+                            fail |= active & !pd;
+                            lf[tri(i, i)] = frsq(pd ? s : T(1));
                         } else {
                             lf[tri(i, j)] = s * lf[tri(j, j)];
                         }
@@ -736,10 +746,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                 if (ll < NX) vv[ll] = q.pr + pv[ll];
                 WAVE_SYNC();
                 if (ll < NZ) {
-                    T s = greg;
-#pragma unroll
-                    for (int l = 0; l < NX; l++) s += abcol[l] * vv[l];
-                    hv[ll] = s;
+                    hv[ll] = dot2<NX>(greg, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
                 }
                 WAVE_SYNC();
                 T hu[NU], x[NU];
