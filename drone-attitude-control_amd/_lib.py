@@ -107,7 +107,8 @@ def load(path=None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or LIB_PATH
+    # NMPC_LIB: an experimental build of the same library (tools/, tuning runs only)
+    p = path or os.environ.get("NMPC_LIB") or LIB_PATH
     if not os.path.exists(p):
         try:
             _build.build()

@@ -43,6 +43,15 @@ def build(force=False, verbose=True):
     return LIB
 
 
+def build_experiment(tag, defines):
+    """Tuning aid: the same library compiled with extra -D flags into lib/exp/ (select it at
+    run time with NMPC_LIB=<path>)."""
+    out = os.path.join(PKG, "lib", "exp", f"libnmpc_hip_{tag}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.check_call(["hipcc", *FLAGS, *[f"-D{d}" for d in defines], *sources(), "-o", out])
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
     print(LIB)

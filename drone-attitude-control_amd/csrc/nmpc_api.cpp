@@ -209,6 +209,7 @@ struct nmpc_solver {
     void *d_model = nullptr, *d_x0 = nullptr, *d_yref = nullptr, *d_x = nullptr, *d_u = nullptr;
     void *d_scratch = nullptr;
     int *d_status = nullptr, *d_iters = nullptr;
+    unsigned long long *d_cycles = nullptr;
     size_t off_AB = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
@@ -244,7 +245,7 @@ void free_all(nmpc_solver *h)
     hipSetDevice(h->device);
     for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
-                    (void *)h->d_acc, (void *)h->d_noise})
+                    (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -282,10 +283,30 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
     p.status = h->d_status;
     p.iters = h->d_iters;
     p.scratch = (T *)h->d_scratch;
+    p.cycles = nullptr;
+    static const bool sweep_cycles = std::getenv("NMPC_SWEEP_CYCLES") != nullptr;
+    if (sweep_cycles) {
+        if (!h->d_cycles && hipMalloc(&h->d_cycles, (size_t)h->batch * 9 * sizeof(unsigned long long)) != hipSuccess)
+            h->d_cycles = nullptr;
+        p.cycles = h->d_cycles;
+    }
     hipEventRecord(e0 ? e0 : h->ev0, h->stream);
     hipError_t e = nmpc::ipm_launch<T>(h->kidx, p, h->stream);
     hipEventRecord(e1 ? e1 : h->ev1, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "ipm kernel launch");
+    if (sweep_cycles && h->d_cycles) {
+        // tuning aid (experiment builds with NMPC_SWEEP_TIMING): mean clock cycles per instance
+        // spent in each phase
+        std::vector<unsigned long long> c((size_t)h->batch * 9);
+        hipStreamSynchronize(h->stream);
+        hipMemcpy(c.data(), h->d_cycles, c.size() * sizeof(c[0]), hipMemcpyDeviceToHost);
+        double s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int b = 0; b < h->batch; b++)
+            for (int j = 0; j < 9; j++) s[j] += (double)c[(size_t)b * 9 + j] / h->batch;
+        std::fprintf(stderr, "[nmpc cycles] B=%d mean per instance: E_A %.0f A %.0f B %.0f E_B %.0f E_C %.0f C %.0f"
+                     " D %.0f E_D %.0f total %.0f\n",
+                     h->batch, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8]);
+    }
     return 0;
 }
 

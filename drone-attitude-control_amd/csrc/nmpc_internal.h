@@ -31,6 +31,7 @@ struct IpmParams {
     int *status;    // [B]
     int *iters;     // [B]
     T *scratch;     // [ceil(B/(IPW*WPB))*IPW*WPB][scratch_elems_per_instance]
+    unsigned long long *cycles;   // optional [B][5] clock cycles per sweep type A..D + total (tuning, env NMPC_SWEEP_CYCLES)
 };
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);

@@ -9,26 +9,30 @@
 //   * one 64-lane wavefront owns IPW instances (G = 64/IPW lanes each; IPW = 1 for the
 //     nx=13, nu=4 headline model: one wavefront per trajectory instance); WPB wavefronts
 //     share a workgroup only to share the model constants in LDS;
-//   * Mehrotra predictor-corrector IPM. Each iteration is four sweeps over the N stages:
-//       A  backward: Riccati factorisation + predictor right-hand side (and the lazily
-//          applied step of the previous iteration),
-//       B  forward: predictor direction + its ratio test and centring sums,
-//       C  backward: corrector right-hand side,
-//       D  forward: corrector direction + step length + the new complementarity measure
-//          (closed form in alpha, so no extra elementwise sweep is needed);
+//   * Mehrotra predictor-corrector IPM. Each iteration alternates lane-parallel elementwise
+//     phases over all (N+1)*nz components of the instance with the three stage recursions
+//     that actually couple stages:
+//       E_A  lazily applied step of the previous iteration, barrier Hessian Sigma, objective
+//            gradient g and dynamics residual re of every stage;
+//       A    backward Riccati factorisation + predictor right-hand side;
+//       B    forward predictor direction, then E_B: its ratio test and centring sums;
+//       E_C  corrector right-hand side of every stage, then C: backward corrector vector;
+//       D    forward corrector direction, then E_D: step length and the new complementarity
+//            measure (closed form in alpha, so no extra sweep is needed).
+//     The elementwise work runs on ~all 64 lanes instead of the nz lanes of one stage, and
+//     the recursions' stage-to-stage dependency chains carry only the linear algebra;
 //   * the stage matrices (P, M = P[A B] stored transposed, F = [A B]'M + H + Sigma) live in
 //     LDS; the lanes form a (column c, row group rg) grid and each lane keeps its column of
 //     [A B] in registers, so every LDS operand is a broadcast read;
 //   * input-block gains in explicit form, K = -F_uu^{-1} F_ux and F_uu^{-1}: the forward
 //     sweeps are then a matrix-vector product per stage, with no triangular solve on the
 //     stage-to-stage dependency chain;
-//   * per-stage iterates and gains stream through a per-instance HBM scratch region; every
-//     sweep prefetches the next stage's data one stage ahead so global latency overlaps
-//     the current stage's LDS/VALU work;
+//   * per-stage iterates and gains stream through a per-instance scratch region (buffer
+//     resource addressing); the recursions prefetch the next stage's data one stage ahead;
 //   * lanes of one wavefront exchange LDS data without barriers: LDS operations of one
 //     wavefront execute in issue order, so a wavefront-scope fence (compiler ordering only)
 //     between writer and reader phases suffices. Global scratch hand-offs between lanes are
-//     ordered by one workgroup-scope fence per sweep.
+//     ordered by one workgroup-scope fence per phase.
 //
 // The algorithm is the one in oracle/c/riccati_ipm.c (the CPU baseline), step for step; its
 // results are checked against the KKT-certified dense oracle (oracle/qp.py).
@@ -38,6 +42,13 @@
 #include <cstdlib>
 
 #include "nmpc_internal.h"
+
+// unroll factor of the row-round loops of the backward factorisation (M, F, P products)
+#ifndef NMPC_UNROLL_A
+#define NMPC_UNROLL_A 2
+#endif
+#define NMPC_STR2(x) #x
+#define NMPC_STR(x) NMPC_STR2(x)
 
 namespace nmpc {
 
@@ -176,18 +187,20 @@ __device__ __forceinline__ void chol_solve(const T (&lf)[NU * (NU + 1) / 2], T (
     }
 }
 
+
 // per-instance scratch (elements of T)
 struct ScratchLayout {
-    size_t z, ll, lu, gc, gf, dza, dz, re, pr, kst, finv, kff, total;
+    size_t z, ll, lu, gc, gf, sg, dza, dz, re, pr, kst, finv, kff, total;
     __host__ __device__ ScratchLayout(int N, int nx, int nu)
     {
         const size_t nz = (size_t)nx + nu, S = (size_t)(N + 1) * nz;
         z = 0;
         ll = z + S;
         lu = ll + S;
-        gc = lu + S;
-        gf = gc + S;
-        dza = gf + S;
+        gc = lu + S;    // G yref (constant per solve)
+        gf = gc + S;    // predictor rhs g = H z + gc; overwritten in place by the corrector rhs
+        sg = gf + S;    // barrier Hessian Sigma
+        dza = sg + S;
         dz = dza + S;
         re = dz + S;
         pr = re + (size_t)N * nx;
@@ -215,20 +228,30 @@ struct Geometry {
     // block-shared constants
     static constexpr int C_AB = 0, C_H = C_AB + NX * LDZ, C_HE = C_H + NZ * LDZ, C_C = C_HE + NX * LDX,
                          C_LB = C_C + LDX, C_UB = C_LB + 3 * LDZ, C_TOT = C_UB + 3 * LDZ;
-    // per-instance work area
-    static constexpr int I_FP = 0, I_MT = I_FP + NZ * LDZ, I_ZV = I_MT + NZ * LDX, I_SV = I_ZV + 2 * LDZ,
-                         I_RV = I_SV + 2 * LDZ, I_VV = I_RV + 2 * LDX, I_HV = I_VV + LDX, I_PV = I_HV + LDZ,
-                         I_KL = I_PV + LDX, I_DX = I_KL + NU * LDX, I_DU = I_DX + 2 * LDX, I_TOT = I_DU + LDU;
+    // per-instance work area; FP and MT are contiguous and double as the stage-z window of
+    // the elementwise phase E_A (ZW elements)
+    static constexpr int I_FP = 0, I_MT = I_FP + NZ * LDZ, I_RV = I_MT + NZ * LDX, I_SV = I_RV + LDX,
+                         I_VV = I_SV + LDZ, I_HV = I_VV + LDX, I_PV = I_HV + LDZ, I_KL = I_PV + LDX,
+                         I_DX = I_KL + NU * LDX, I_DU = I_DX + 2 * LDX, I_TOT = I_DU + LDU;
+    static constexpr int ZW = NZ * LDZ + NZ * LDX;
+    static constexpr int CH = ZW / NZ - 1;     // stages per E_A chunk (+1 stage of overlap)
     static constexpr int LDS_ELEMS = C_TOT + WPB * IPW * I_TOT;
     static_assert(R >= 1, "lane group narrower than the stage width");
+    static_assert(CH >= 1, "stage-z window too small");
 };
 
+#ifdef NMPC_SWEEP_TIMING
+#define NMPC_TICK(slot) tick(slot)
+#else
+#define NMPC_TICK(slot) ((void)0)
+#endif
+
 template <typename T, int NX, int NU, int IPW, int WPB, int MW>
-__global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8))) void ipm_kernel(IpmParams<T> p)
 {
     using Gm = Geometry<T, NX, NU, IPW, WPB>;
     constexpr int NZ = Gm::NZ, G = Gm::G, R = Gm::R, RM = Gm::RM, RF = Gm::RF;
-    constexpr int LDZ = Gm::LDZ, LDX = Gm::LDX;
+    constexpr int LDZ = Gm::LDZ, LDX = Gm::LDX, NUT = NU * (NU + 1) / 2;
 
     __shared__ __attribute__((aligned(16))) T lds[Gm::LDS_ELEMS];
     T *cab = lds + Gm::C_AB, *ch = lds + Gm::C_H, *che = lds + Gm::C_HE, *cc = lds + Gm::C_C;
@@ -247,7 +270,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
     const int N = p.N;
     T *w = lds + Gm::C_TOT + (wave * IPW + grp) * Gm::I_TOT;
     T *fp = w + Gm::I_FP, *mt = w + Gm::I_MT, *hv = w + Gm::I_HV, *vv = w + Gm::I_VV, *pv = w + Gm::I_PV;
-    T *kl = w + Gm::I_KL, *du_l = w + Gm::I_DU;
+    T *rv = w + Gm::I_RV, *sv = w + Gm::I_SV, *kl = w + Gm::I_KL, *du_l = w + Gm::I_DU, *zw = w + Gm::I_FP;
 
     // ---- model constants -> LDS (once per workgroup)
     for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) cab[(e / NZ) * LDZ + e % NZ] = p.AB[e];
@@ -266,25 +289,21 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
     };
     __syncthreads();
     if (!__any(inst_ok)) return;   // tail wavefront of the last workgroup: nothing to solve
-    // bounds of this lane's component for the three stage types (0, 1..N-1, N)
-    const int lc = ll < NZ ? ll : 0;
 
     const ScratchLayout L(N, NX, NU);
-    // wave-uniform bases (SGPRs) + 32-bit lane offsets: global loads take the saddr form
+    // wave-uniform bases (SGPRs) + 32-bit lane offsets
     const unsigned wave_u = __builtin_amdgcn_readfirstlane(wave);
     const size_t inst0 = ((size_t)blockIdx.x * WPB + wave_u) * IPW;
     Scr<T> S;
     S.r = __builtin_amdgcn_make_buffer_rsrc(p.scratch + inst0 * L.total, 0,
                                             (int)(IPW * L.total * sizeof(T)), 0x00020000);
     S.go = (unsigned)grp * (unsigned)(L.total * sizeof(T));
-    const unsigned Lz = L.z, Lll = L.ll, Llu = L.lu, Lgc = L.gc, Lgf = L.gf, Ldza = L.dza, Ldz = L.dz;
+    const unsigned Lz = L.z, Lll = L.ll, Llu = L.lu, Lgc = L.gc, Lgf = L.gf, Lsg = L.sg, Ldza = L.dza, Ldz = L.dz;
     const unsigned Lre = L.re, Lpr = L.pr, Lkst = L.kst, Lfinv = L.finv, Lkff = L.kff;
     const T *yref = p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
     const T *x0 = p.x0 + (size_t)inst * NX;
     const int nel = (N + 1) * NZ;
     auto stype = [&](int k) { return k == 0 ? 0 : (k == N ? 2 : 1); };
-    auto LBR = [&](int k) { return clb[stype(k) * LDZ + lc]; };
-    auto UBR = [&](int k) { return cub[stype(k) * LDZ + lc]; };
 
     // ------------------------------------------------------------------ initial point
     for (int e = ll; e < nel; e += G) {
@@ -355,174 +374,55 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
     bool fail = false, pending = false;
     T alpha = 0, smu = 0;      // step and sigma*mu of the pending (lazily applied) update
 
-    // component lanes: lane ll owns component ll of every stage vector
-    auto nzk = [&](int k) { return k == N ? NX : NZ; };
+#ifdef NMPC_SWEEP_TIMING
+    // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per phase
+    const bool timed = p.cycles != nullptr;
+    unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = 0;
+    auto tick = [&](int slot) {
+        if (timed) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (slot >= 0) tcy[slot] += t - tmark;
+            tmark = t;
+        }
+    };
+    const unsigned long long tstart = timed ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
 
-    // P1: (lazy update,) Sigma and z of stage k -> LDS buffer (k & 1)
-    auto stage_p1 = [&](int k, T z, T lam_l, T lam_u, T dz, T dza, T &zreg) {
-        if (ll < nzk(k)) {
-            const int e = k * NZ + ll;
-            const T lb = LBR(k), ub = UBR(k);
-            if (pending) {
-                if (lam_l > T(0)) {
-                    const T t = z - lb, it_ = frcp(t), dla = -lam_l * (T(1) + dza * it_);
-                    lam_l += alpha * ((smu - lam_l * t - dla * dza - lam_l * dz) * it_);
-                }
-                if (lam_u > T(0)) {
-                    const T t = ub - z, it_ = frcp(t), dla = -lam_u * (T(1) - dza * it_);
-                    lam_u += alpha * ((smu - lam_u * t + dla * dza + lam_u * dz) * it_);
-                }
-                z += alpha * dz;
-                S.st(Lz + k * NZ, ll, z);
-                S.st(Lll + k * NZ, ll, lam_l);
-                S.st(Llu + k * NZ, ll, lam_u);
-            }
-            T sig = 0;
-            if (lam_l > T(0)) sig += lam_l * frcp(z - lb);
-            if (lam_u > T(0)) sig += lam_u * frcp(ub - z);
-            w[Gm::I_ZV + (k & 1) * LDZ + ll] = z;
-            w[Gm::I_SV + (k & 1) * LDZ + ll] = sig;
-            zreg = z;
-        }
-    };
-    // P2: objective gradient g_k (predictor rhs) and dynamics residual re_k -> LDS (k & 1)
-    auto stage_p2 = [&](int k, T gc, T zprev, T &greg) {
-        const T *zv = w + Gm::I_ZV + (k & 1) * LDZ;
-        if (ll < nzk(k)) {
-            T g;
-            if (k < N) {
-                g = dot2<NZ>(gc, [&](int b) { return ch[ll * LDZ + b]; }, [&](int b) { return zv[b]; });
-            } else {
-                g = dot2<NX>(gc, [&](int b) { return che[ll * LDX + b]; }, [&](int b) { return zv[b]; });
-            }
-            greg = g;
-            S.st(Lgf + k * NZ, ll, g);
-        }
-        if (k < N && ll < NX) {
-            const T r = dot2<NZ>(cc[ll] - zprev, [&](int j) { return cab[ll * LDZ + j]; },
-                                 [&](int j) { return zv[j]; });
-            w[Gm::I_RV + (k & 1) * LDX + ll] = r;
-            S.st(Lre + k * NX, ll, r);
-        }
-    };
-    struct Pre {
-        T z, l, u, dz, dza, gc;
-    };
-    // Prefetches are unconditional (no phi at a branch join, so the compiler does not drain
-    // vmcnt there); lanes / stages outside the valid range read harmless data or, past the
-    // end of the buffer resource, zeros.
-    auto prefetch_a = [&](int k, Pre &q) {
-        const unsigned e = (unsigned)(k < 0 ? 0 : k) * NZ;
-        q.z = S.ld(Lz + e, ll);
-        q.l = S.ld(Lll + e, ll);
-        q.u = S.ld(Llu + e, ll);
-        q.gc = S.ld(Lgc + e, ll);
-        q.dz = S.ld(Ldz + e, ll);
-        q.dza = S.ld(Ldza + e, ll);
-    };
-
-    // forward sweep shared by predictor (corr = false) and corrector (corr = true);
-    // returns the group's step bound and, for the corrector, the closed-form mu sums
-    auto forward = [&](bool corr, unsigned dst, T &amax, T &s0, T &s1, T &s2) {
+    // ---- forward recursion shared by predictor (dst = dza) and corrector (dst = dz):
+    // dx_0 = 0 (x0 pinned), du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx; du] + re_k
+    auto forward = [&](unsigned dst) {
         T *dxb = w + Gm::I_DX;
         if (ll < NX) dxb[ll] = T(0);
-        amax = T(1);
-        s0 = s1 = s2 = T(0);
-        // stage-0 data; every later stage is fetched one stage ahead (K after its last use)
-        T krow[NX], kff = 0, re = 0, z = 0, lam_l = 0, lam_u = 0, dza = 0;
+        T krow[NX], kff = 0, re = 0;
         auto fetch_k = [&](int k) {
 #pragma unroll
             for (int i = 0; i < NX; i++) krow[i] = S.ld(Lkst + k * NU * NX + i, ll * NX);
         };
-        auto fetch_v = [&](int k, T &kf, T &r, T &zz, T &la, T &lu, T &da) {
-            const unsigned kk = (unsigned)(k < N ? k : N - 1);
-            kf = S.ld(Lkff + kk * NU, ll);
-            r = S.ld(Lre + kk * NX, ll);
-            const unsigned e = k * NZ;
-            zz = S.ld(Lz + e, ll);
-            la = S.ld(Lll + e, ll);
-            lu = S.ld(Llu + e, ll);
-            da = S.ld(Ldza + e, ll);
-        };
         fetch_k(0);
-        fetch_v(0, kff, re, z, lam_l, lam_u, dza);
+        kff = S.ld(Lkff, ll);
+        re = S.ld(Lre, ll);
         WAVE_SYNC();
         int cur = 0;
-        for (int k = 0; k <= N; k++) {
+        for (int k = 0; k < N; k++) {
             const T *dxc = dxb + cur * LDX;
             T *dxn = dxb + (1 - cur) * LDX;
-            T kff_n = 0, re_n = 0, z_n = 0, ll_n = 0, lu_n = 0, dza_n = 0;
-            if (k < N) {
-                fetch_v(k + 1, kff_n, re_n, z_n, ll_n, lu_n, dza_n);
-                // du = kff + K dx
-                if (ll < NU) {
-                    du_l[ll] = dot2<NX>(kff, [&](int i) { return krow[i]; }, [&](int i) { return dxc[i]; });
-                }
-                fetch_k(k + 1 < N ? k + 1 : N - 1);
-                WAVE_SYNC();
-                if (ll < NX) {
-                    dxn[ll] = dot2<NZ>(re, [&](int j) { return cab[ll * LDZ + j]; },
-                                       [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
-                }
+            const unsigned kn = (unsigned)(k + 1 < N ? k + 1 : N - 1);
+            const T kff_n = S.ld(Lkff + kn * NU, ll), re_n = S.ld(Lre + kn * NX, ll);
+            if (ll < NU) du_l[ll] = dot2<NX>(kff, [&](int i) { return krow[i]; }, [&](int i) { return dxc[i]; });
+            WAVE_SYNC();
+            fetch_k(kn);
+            if (ll < NX) {
+                dxn[ll] = dot2<NZ>(re, [&](int j) { return cab[ll * LDZ + j]; },
+                                   [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
             }
-            // stage k direction component + ratio test / sums
-            if (ll < nzk(k)) {
-                const T dz = ll < NX ? dxc[ll] : du_l[ll - NX];
-                S.st(dst + k * NZ, ll, dz);
-                const T lb = LBR(k), ub = UBR(k);
-                if (lam_l > T(0)) {
-                    const T t = z - lb, it_ = frcp(t);
-                    if (!corr) {
-                        const T dl = -lam_l * (T(1) + dz * it_);
-                        if (dz < T(0)) amax = fmin(amax, -t * frcp(dz));
-                        if (dl < T(0)) amax = fmin(amax, -lam_l * frcp(dl));
-                        s0 += lam_l * t;
-                        s2 += lam_l * dz * (t + dz) * it_;
-                    } else {
-                        const T dla = -lam_l * (T(1) + dza * it_);
-                        const T dl = (smu - lam_l * t - dla * dza - lam_l * dz) * it_;
-                        if (dz < T(0)) amax = fmin(amax, -t * frcp(dz));
-                        if (dl < T(0)) amax = fmin(amax, -lam_l * frcp(dl));
-                        s0 += lam_l * t;
-                        s1 += dla * dza;
-                        s2 += dl * dz;
-                    }
-                }
-                if (lam_u > T(0)) {
-                    const T t = ub - z, it_ = frcp(t);
-                    if (!corr) {
-                        const T dl = -lam_u * (T(1) - dz * it_);
-                        if (dz > T(0)) amax = fmin(amax, t * frcp(dz));
-                        if (dl < T(0)) amax = fmin(amax, -lam_u * frcp(dl));
-                        s0 += lam_u * t;
-                        s2 += lam_u * dz * (dz - t) * it_;
-                    } else {
-                        const T dla = -lam_u * (T(1) - dza * it_);
-                        const T dl = (smu - lam_u * t + dla * dza + lam_u * dz) * it_;
-                        if (dz > T(0)) amax = fmin(amax, t * frcp(dz));
-                        if (dl < T(0)) amax = fmin(amax, -lam_u * frcp(dl));
-                        s0 += lam_u * t;
-                        s1 += -dla * dza;
-                        s2 += -dl * dz;
-                    }
-                }
-            }
-            if (k < N) {
-                kff = kff_n;
-                re = re_n;
-                z = z_n;
-                lam_l = ll_n;
-                lam_u = lu_n;
-                dza = dza_n;
-                cur = 1 - cur;
-                WAVE_SYNC();
-            }
+            if (ll < NZ) S.st(dst + k * NZ, ll, ll < NX ? dxc[ll] : du_l[ll - NX]);
+            kff = kff_n;
+            re = re_n;
+            cur = 1 - cur;
+            WAVE_SYNC();
         }
+        if (ll < NX) S.st(dst + N * NZ, ll, dxb[cur * LDX + ll]);
         SWEEP_FENCE();
-        amax = group_min<G>(amax);
-        s0 = group_sum<G>(s0);
-        s1 = group_sum<G>(s1);
-        s2 = group_sum<G>(s2);
     };
 
     int it = 0;
@@ -540,39 +440,107 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
             iters = it;
         }
         if (!__any(active)) break;
+        NMPC_TICK(-1);
 
-        // ============================ A: backward factorisation + predictor vector
-        {
-            Pre q{}, qn{};
-            T zreg_k = 0, zreg_km1 = 0, greg = 0, greg_n = 0;
-            prefetch_a(N, q);
-            stage_p1(N, q.z, q.l, q.u, q.dz, q.dza, zreg_k);
-            prefetch_a(N - 1, qn);
+        // ============================ E_A: lazy step, Sigma, g = H z + gc, re = [A B] z_k + c - x_{k+1}
+        // stage chunks whose z (plus one stage of overlap) fit the LDS window zw
+        for (int k0 = 0; k0 <= N; k0 += Gm::CH) {
+            const int k1 = min(k0 + Gm::CH, N + 1);       // stages owned by this chunk
+            const int kz = min(k0 + Gm::CH + 1, N + 1);   // stages whose z the chunk reads
+            for (int e = k0 * NZ + ll; e < kz * NZ; e += G) {
+                const int k = e / NZ, i = e - k * NZ;
+                T z = 0;
+                if (k < N || i < NX) {
+                    z = S.ld(Lz, e);
+                    T lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
+                    const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+                    if (pending) {
+                        const T dz = S.ld(Ldz, e), dza = S.ld(Ldza, e);
+                        if (lam_l > T(0)) {
+                            const T t = z - lb, it_ = frcp(t), dla = -lam_l * (T(1) + dza * it_);
+                            lam_l += alpha * ((smu - lam_l * t - dla * dza - lam_l * dz) * it_);
+                        }
+                        if (lam_u > T(0)) {
+                            const T t = ub - z, it_ = frcp(t), dla = -lam_u * (T(1) - dza * it_);
+                            lam_u += alpha * ((smu - lam_u * t + dla * dza + lam_u * dz) * it_);
+                        }
+                        z += alpha * dz;
+                    }
+                    if (k < k1) {
+                        if (pending) {
+                            S.st(Lz, e, z);
+                            S.st(Lll, e, lam_l);
+                            S.st(Llu, e, lam_u);
+                        }
+                        T sig = 0;
+                        if (lam_l > T(0)) sig += lam_l * frcp(z - lb);
+                        if (lam_u > T(0)) sig += lam_u * frcp(ub - z);
+                        S.st(Lsg, e, sig);
+                    }
+                }
+                zw[e - k0 * NZ] = z;
+            }
             WAVE_SYNC();
-            stage_p2(N, q.gc, T(0), greg);
-            stage_p1(N - 1, qn.z, qn.l, qn.u, qn.dz, qn.dza, zreg_km1);
+            for (int e = k0 * NZ + ll; e < k1 * NZ; e += G) {
+                const int k = e / NZ, i = e - k * NZ;
+                const T *zk = zw + (k - k0) * NZ;
+                if (k < N) {
+                    S.st(Lgf, e, dot2<NZ>(S.ld(Lgc, e), [&](int b) { return ch[i * LDZ + b]; },
+                                          [&](int b) { return zk[b]; }));
+                } else if (i < NX) {
+                    S.st(Lgf, e, dot2<NX>(S.ld(Lgc, e), [&](int b) { return che[i * LDX + b]; },
+                                          [&](int b) { return zk[b]; }));
+                }
+            }
+            for (int e = k0 * NX + ll; e < min(k1, N) * NX; e += G) {
+                const int k = e / NX, i = e - k * NX;
+                const T *zk = zw + (k - k0) * NZ;
+                S.st(Lre, e, dot2<NZ>(cc[i] - zk[NZ + i], [&](int j) { return cab[i * LDZ + j]; },
+                                      [&](int j) { return zk[j]; }));
+            }
+            WAVE_SYNC();
+        }
+        pending = false;
+        SWEEP_FENCE();
+        NMPC_TICK(0);
+
+        // ============================ A: backward Riccati factorisation + predictor vector
+        {
+            struct PreA {
+                T sg, g, re;
+            };
+            auto fetch_a = [&](int k, PreA &q) {
+                const unsigned kk = (unsigned)(k < 0 ? 0 : k);
+                q.sg = S.ld(Lsg + kk * NZ, ll);
+                q.g = S.ld(Lgf + kk * NZ, ll);
+                q.re = S.ld(Lre + (kk < (unsigned)N ? kk : N - 1) * NX, ll);
+            };
             // P_N = He + Sigma_N, p_N = g_N
+            {
+                const T sgN = S.ld(Lsg + N * NZ, ll), gN = S.ld(Lgf + N * NZ, ll);
+                if (ll < NX) {
+                    sv[ll] = sgN;
+                    pv[ll] = gN;
+                }
+            }
+            PreA q{};
+            fetch_a(N - 1, q);
+            WAVE_SYNC();
             if (gridl && col < NX) {
 #pragma unroll
                 for (int qq = 0; qq < RM; qq++) {
                     const int i = rg + R * qq;
-                    if (i < NX)
-                        fp[i * LDZ + col] = (che[i * LDX + col]) + (i == col ? w[Gm::I_SV + (N & 1) * LDZ + col] : T(0));
+                    if (i < NX) fp[i * LDZ + col] = che[i * LDX + col] + (i == col ? sv[col] : T(0));
                 }
             }
-            if (ll < NX) pv[ll] = greg;
-            const T gc_km1 = qn.gc;
             WAVE_SYNC();
-            stage_p2(N - 1, gc_km1, zreg_k, greg);
+            if (ll < NX) rv[ll] = q.re;
+            if (ll < NZ) sv[ll] = q.sg;
             WAVE_SYNC();
             for (int k = N - 1; k >= 0; k--) {
-                const int b = k & 1;
-                const T *rv = w + Gm::I_RV + b * LDX;
-                const T *sv = w + Gm::I_SV + b * LDZ;
-                // next stage's (k-1) global data in flight during this stage
-                Pre qk{};
-                prefetch_a(k - 1, qk);
-                // B: Pr = P re, v = Pr + p, M^T = (P [A B])^T
+                PreA qn{};
+                fetch_a(k - 1, qn);
+                // 1: Pr = P re, v = Pr + p, M^T = (P [A B])^T
                 T abcol[NX];
                 load_abcol(abcol);
                 if (ll < NX) {
@@ -581,7 +549,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                     vv[ll] = s + pv[ll];
                 }
                 if (gridl) {
-#pragma unroll 1
+_Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     for (int qq = 0; qq < RM; qq++) {
                         const int i = rg + R * qq;
                         if (i < NX) {
@@ -591,9 +559,9 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                     }
                 }
                 WAVE_SYNC();
-                // C: F = [A B]' M + H + Sigma (row col), h = [A B]' v + g
+                // 2: F = [A B]' M + H + Sigma (row col), h = [A B]' v + g
                 if (gridl) {
-#pragma unroll 1
+_Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     for (int qq = 0; qq < RF; qq++) {
                         const int bb = rg + R * qq;
                         if (bb < NZ) {
@@ -603,13 +571,10 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                             fp[col * LDZ + bb] = s;
                         }
                     }
-                    if (rg == 0) {
-                        hv[col] = dot2<NX>(greg, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
-                    }
+                    if (rg == 0) hv[col] = dot2<NX>(q.g, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
                 }
                 WAVE_SYNC();
-                // D: F_uu^-1 (wave-uniform Cholesky), K = -F_uu^-1 F_ux, kff, p_k; P1(k-1)
-                constexpr int NUT = NU * (NU + 1) / 2;
+                // 3: F_uu^-1 (wave-uniform Cholesky), K = -F_uu^-1 F_ux, kff, p_k
                 T lf[NUT];
 #pragma unroll
                 for (int i = 0; i < NU; i++)
@@ -657,83 +622,107 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                     if (ll < NU) S.st(Lkff + k * NU, ll, mine);
                     if (ll < NUT) S.st(Lfinv + k * NUT, ll, lmine);
                 }
-                T zreg_km2 = 0;
-                if (k > 0) stage_p1(k - 1, qk.z, qk.l, qk.u, qk.dz, qk.dza, zreg_km2);
                 WAVE_SYNC();
-                // E: P_k = F_xx + F_xu K ; P2(k-1)
+                // 4: P_k = F_xx + F_xu K (in place); next stage's re and Sigma -> LDS
                 if (k > 0) {
                     if (gridl && col < NX) {
                         T fu[NU];
 #pragma unroll
                         for (int u = 0; u < NU; u++) fu[u] = fp[col * LDZ + NX + u];
-#pragma unroll 1
-                        for (int qq = 0; qq < RF; qq++) {
+_Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
+                        for (int qq = 0; qq < RM; qq++) {
                             const int i = rg + R * qq;
                             if (i < NX) {
-                                T s = fp[col * LDZ + i];   // F_xx entry, overwritten in place by P
+                                T s = fp[col * LDZ + i];
 #pragma unroll
                                 for (int u = 0; u < NU; u++) s += fu[u] * kl[u * LDX + i];
                                 fp[col * LDZ + i] = s;
                             }
                         }
                     }
-                    stage_p2(k - 1, qk.gc, zreg_km1, greg);
-                    zreg_km1 = zreg_km2;
+                    if (ll < NX) rv[ll] = qn.re;
+                    if (ll < NZ) sv[ll] = qn.sg;
                 }
+                q = qn;
                 WAVE_SYNC();
             }
-            pending = false;
         }
         SWEEP_FENCE();
+        NMPC_TICK(1);
 
-        // ============================ B: forward predictor
-        T a_aff, S0, S1, S2;
-        forward(false, Ldza, a_aff, S0, S1, S2);
+        // ============================ B: forward predictor; E_B: ratio test + centring sums
+        forward(Ldza);
+        NMPC_TICK(2);
+        T a_aff = 1, S0 = 0, S2 = 0;
+        for (int e = ll; e < nel; e += G) {
+            const int k = e / NZ, i = e - k * NZ;
+            if (k == N && i >= NX) continue;
+            const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), dz = S.ld(Ldza, e);
+            if (lam_l > T(0)) {
+                const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t);
+                const T dl = -lam_l * (T(1) + dz * it_);
+                if (dz < T(0)) a_aff = fmin(a_aff, -t * frcp(dz));
+                if (dl < T(0)) a_aff = fmin(a_aff, -lam_l * frcp(dl));
+                S0 += lam_l * t;
+                S2 += lam_l * dz * (t + dz) * it_;
+            }
+            if (lam_u > T(0)) {
+                const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t);
+                const T dl = -lam_u * (T(1) - dz * it_);
+                if (dz > T(0)) a_aff = fmin(a_aff, t * frcp(dz));
+                if (dl < T(0)) a_aff = fmin(a_aff, -lam_u * frcp(dl));
+                S0 += lam_u * t;
+                S2 += lam_u * dz * (dz - t) * it_;
+            }
+        }
+        a_aff = group_min<G>(a_aff);
+        S0 = group_sum<G>(S0);
+        S2 = group_sum<G>(S2);
         // mu_aff = [(1 - a) S0 - a^2 S2'] / m  with S2' = sum lam dz (t + dz) / t (closed form)
         const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
-        const T sg = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
-        const T smu_new = sg * sg * sg * mu;
+        const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
+        smu = sgm * sgm * sgm * mu;
+        NMPC_TICK(3);
 
-        // ============================ C: backward corrector vector
+        // ============================ E_C: corrector rhs g^ = g + (dlam_a dz_a -/+ sigma mu) / t
+        for (int e = ll; e < nel; e += G) {
+            const int k = e / NZ, i = e - k * NZ;
+            if (k == N && i >= NX) continue;
+            const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), dza = S.ld(Ldza, e);
+            T g = S.ld(Lgf, e);
+            if (lam_l > T(0)) {
+                const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t), dl = -lam_l * (T(1) + dza * it_);
+                g += (dl * dza - smu) * it_;
+            }
+            if (lam_u > T(0)) {
+                const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t), dl = -lam_u * (T(1) - dza * it_);
+                g += (dl * dza + smu) * it_;
+            }
+            S.st(Lgf, e, g);
+        }
+        SWEEP_FENCE();
+        NMPC_TICK(4);
+
+        // ============================ C: backward corrector vector (kff, p)
         {
-            smu = smu_new;
-            auto corr_grad = [&](int k, T gf, T z, T lam_l, T lam_u, T dza) -> T {
-                T g = gf;
-                const T lb = LBR(k), ub = UBR(k);
-                if (lam_l > T(0)) {
-                    const T t = z - lb, it_ = frcp(t), dl = -lam_l * (T(1) + dza * it_);
-                    g += (dl * dza - smu) * it_;
-                }
-                if (lam_u > T(0)) {
-                    const T t = ub - z, it_ = frcp(t), dl = -lam_u * (T(1) - dza * it_);
-                    g += (dl * dza + smu) * it_;
-                }
-                return g;
-            };
-            constexpr int NUT = NU * (NU + 1) / 2;
             struct PreC {
-                T gf, z, l, u, dza, pr;
+                T g, pr;
             };
             auto fetch_c = [&](int k, PreC &q) {
-                const unsigned kc_ = (unsigned)(k < 0 ? 0 : k);
-                const unsigned e = kc_ * NZ;
-                q.gf = S.ld(Lgf + e, ll);
-                q.z = S.ld(Lz + e, ll);
-                q.l = S.ld(Lll + e, ll);
-                q.u = S.ld(Llu + e, ll);
-                q.dza = S.ld(Ldza + e, ll);
-                q.pr = S.ld(Lpr + (kc_ < (unsigned)N ? kc_ : N - 1) * NX, ll);
+                const unsigned kk = (unsigned)(k < 0 ? 0 : k);
+                q.g = S.ld(Lgf + kk * NZ, ll);
+                q.pr = S.ld(Lpr + (kk < (unsigned)N ? kk : N - 1) * NX, ll);
             };
-            PreC qN{};
-            fetch_c(N, qN);
-            if (ll < NX) pv[ll] = corr_grad(N, qN.gf, qN.z, qN.l, qN.u, qN.dza);
+            {
+                const T gN = S.ld(Lgf + N * NZ, ll);
+                if (ll < NX) pv[ll] = gN;
+            }
             PreC q{};
             fetch_c(N - 1, q);
             WAVE_SYNC();
             for (int k = N - 1; k >= 0; k--) {
                 T abcol[NX];
                 load_abcol(abcol);
-                // this stage's factors (used two phases later) and the next stage's vectors
                 T lf[NUT], kc[NU];
 #pragma unroll
                 for (int j = 0; j < NUT; j++) lf[j] = S.ld(Lfinv + k * NUT + j, 0);
@@ -741,13 +730,9 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
                 for (int u = 0; u < NU; u++) kc[u] = S.ld(Lkst + k * NU * NX + u * NX, ll);
                 PreC qn{};
                 fetch_c(k - 1, qn);
-                T greg = 0;
-                if (ll < NZ) greg = corr_grad(k, q.gf, q.z, q.l, q.u, q.dza);
                 if (ll < NX) vv[ll] = q.pr + pv[ll];
                 WAVE_SYNC();
-                if (ll < NZ) {
-                    hv[ll] = dot2<NX>(greg, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
-                }
+                if (ll < NZ) hv[ll] = dot2<NX>(q.g, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
                 WAVE_SYNC();
                 T hu[NU], x[NU];
 #pragma unroll
@@ -768,10 +753,42 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
             }
         }
         SWEEP_FENCE();
+        NMPC_TICK(5);
 
-        // ============================ D: forward corrector, step length, new mu
-        T amax, T0, C1, C2;
-        forward(true, Ldz, amax, T0, C1, C2);
+        // ============================ D: forward corrector; E_D: step length + new mu
+        forward(Ldz);
+        NMPC_TICK(6);
+        T amax = 1, T0 = 0, C1 = 0, C2 = 0;
+        for (int e = ll; e < nel; e += G) {
+            const int k = e / NZ, i = e - k * NZ;
+            if (k == N && i >= NX) continue;
+            const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
+            const T dz = S.ld(Ldz, e), dza = S.ld(Ldza, e);
+            if (lam_l > T(0)) {
+                const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t);
+                const T dla = -lam_l * (T(1) + dza * it_);
+                const T dl = (smu - lam_l * t - dla * dza - lam_l * dz) * it_;
+                if (dz < T(0)) amax = fmin(amax, -t * frcp(dz));
+                if (dl < T(0)) amax = fmin(amax, -lam_l * frcp(dl));
+                T0 += lam_l * t;
+                C1 += dla * dza;
+                C2 += dl * dz;
+            }
+            if (lam_u > T(0)) {
+                const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t);
+                const T dla = -lam_u * (T(1) - dza * it_);
+                const T dl = (smu - lam_u * t + dla * dza + lam_u * dz) * it_;
+                if (dz > T(0)) amax = fmin(amax, t * frcp(dz));
+                if (dl < T(0)) amax = fmin(amax, -lam_u * frcp(dl));
+                T0 += lam_u * t;
+                C1 += -dla * dza;
+                C2 += -dl * dz;
+            }
+        }
+        amax = group_min<G>(amax);
+        T0 = group_sum<G>(T0);
+        C1 = group_sum<G>(C1);
+        C2 = group_sum<G>(C2);
         const T a = fmin(T(1), T(0.995) * amax);
         if (active) {
             // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
@@ -780,6 +797,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
             alpha = a;
             pending = true;
         }
+        NMPC_TICK(7);
     }
 
     // ------------------------------------------------------------------ apply pending step, outputs
@@ -797,6 +815,13 @@ __global__ __launch_bounds__(64 * WPB, MW) void ipm_kernel(IpmParams<T> p)
     if (ll == 0) {
         p.status[inst] = status;
         p.iters[inst] = iters;
+#ifdef NMPC_SWEEP_TIMING
+        if (timed) {
+            unsigned long long *c = p.cycles + (size_t)inst * 9;
+            for (int j = 0; j < 8; j++) c[j] = tcy[j];
+            c[8] = __builtin_amdgcn_s_memtime() - tstart;
+        }
+#endif
     }
 }
 
@@ -834,7 +859,7 @@ static const IpmEntry<T> *table(int *n)
         // quad13: the first entry is the default (measured fastest, profiles/); the rest are
         // selectable with NMPC_VARIANT for tuning runs
         entry<T, 13, 4, 1, 1, 3>(), entry<T, 13, 4, 1, 4>(), entry<T, 13, 4, 1, 1, 2>(),
-        entry<T, 13, 4, 1, 4, 3>(),
+        entry<T, 13, 4, 1, 4, 3>(), entry<T, 13, 4, 1, 2, 4>(),
     };
     *n = (int)(sizeof(t) / sizeof(t[0]));
     return t;
