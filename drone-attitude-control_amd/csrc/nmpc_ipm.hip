@@ -47,6 +47,10 @@
 #ifndef NMPC_UNROLL_A
 #define NMPC_UNROLL_A 2
 #endif
+// stage records in flight ahead of the B/C/D recursions
+#ifndef NMPC_STREAM_DEPTH
+#define NMPC_STREAM_DEPTH 4
+#endif
 #define NMPC_STR2(x) #x
 #define NMPC_STR(x) NMPC_STR2(x)
 
@@ -189,25 +193,30 @@ __device__ __forceinline__ void chol_solve(const T (&lf)[NU * (NU + 1) / 2], T (
 
 
 // per-instance scratch (elements of T)
+// Stage records, each contiguous so that a recursion streams one stage with one load per lane
+// and record slot (per G lanes):
+//   frec[k] = [ K_k (nu x nx, row-major) | kff_k (nu) | re_k (nx) ]       forward sweeps B, D
+//   crec[k] = [ F_uu^-1 factor (packed, inverse diagonal) | Pr_k (nx) | corrector rhs (nz) ]
+//                                                                         backward sweep C
 struct ScratchLayout {
-    size_t z, ll, lu, gc, gf, sg, dza, dz, re, pr, kst, finv, kff, total;
+    size_t z, ll, lu, gc, gf, sg, dza, dz, frec, crec, total;
+    int rsf, rsc;   // record sizes (elements)
     __host__ __device__ ScratchLayout(int N, int nx, int nu)
     {
         const size_t nz = (size_t)nx + nu, S = (size_t)(N + 1) * nz;
+        rsf = nu * nx + nu + nx;
+        rsc = nu * (nu + 1) / 2 + nx + (int)nz;
         z = 0;
         ll = z + S;
         lu = ll + S;
         gc = lu + S;    // G yref (constant per solve)
-        gf = gc + S;    // predictor rhs g = H z + gc; overwritten in place by the corrector rhs
+        gf = gc + S;    // predictor rhs g = H z + gc (terminal stage: corrector rhs in C)
         sg = gf + S;    // barrier Hessian Sigma
         dza = sg + S;
         dz = dza + S;
-        re = dz + S;
-        pr = re + (size_t)N * nx;
-        kst = pr + (size_t)N * nx;            // K_k  [nu][nx] row-major
-        finv = kst + (size_t)N * nu * nx;     // Cholesky factor of F_uu, packed (inverse diagonal)
-        kff = finv + (size_t)N * (nu * (nu + 1) / 2);   // feed-forward -F_uu^-1 h_u [nu]
-        total = kff + (size_t)N * nu;
+        frec = dz + S;
+        crec = frec + (size_t)N * rsf;
+        total = crec + (size_t)N * rsc;
         total = (total + 31) & ~size_t(31);
     }
 };
@@ -235,15 +244,32 @@ struct Geometry {
                          I_DX = I_KL + NU * LDX, I_DU = I_DX + 2 * LDX, I_TOT = I_DU + LDU;
     static constexpr int ZW = NZ * LDZ + NZ * LDX;
     static constexpr int CH = ZW / NZ - 1;     // stages per E_A chunk (+1 stage of overlap)
-    static constexpr int LDS_ELEMS = C_TOT + WPB * IPW * I_TOT;
+    // stage-record ring of the B/C/D recursions: two buffers of (NSF + NSC) slots of G elements;
+    // it shares the FP/MT area when that is large enough (E_A and A do not overlap B/C/D)
+    static constexpr int NUT = NU * (NU + 1) / 2;
+    static constexpr int RSF = NU * NX + NU + NX, RSC = NUT + NX + NZ;
+    static constexpr int NSF = (RSF + G - 1) / G, NSC = (RSC + G - 1) / G;
+    static constexpr int RB1 = (NSF + NSC) * G;
+    static constexpr bool RB_ALIAS = 2 * RB1 <= ZW;
+    static constexpr int I_RB = RB_ALIAS ? I_FP : I_TOT;
+    static constexpr int I_ALL = RB_ALIAS ? I_TOT : I_TOT + 2 * RB1;
+    static constexpr int LDS_ELEMS = C_TOT + WPB * IPW * I_ALL;
     static_assert(R >= 1, "lane group narrower than the stage width");
     static_assert(CH >= 1, "stage-z window too small");
 };
 
-#ifdef NMPC_SWEEP_TIMING
+// timing builds (tools/exp.sh): NMPC_SWEEP_TIMING = cycles per phase of the iteration;
+// NMPC_PHASE_TIMING = cycles of the four phases of the Riccati stage loop (slots 0..3)
+#if defined(NMPC_PHASE_TIMING)
+#define NMPC_SWEEP_TIMING 1
+#define NMPC_TICK(slot) ((void)0)
+#define NMPC_PTICK(slot) tick(slot)
+#elif defined(NMPC_SWEEP_TIMING)
 #define NMPC_TICK(slot) tick(slot)
+#define NMPC_PTICK(slot) ((void)0)
 #else
 #define NMPC_TICK(slot) ((void)0)
+#define NMPC_PTICK(slot) ((void)0)
 #endif
 
 template <typename T, int NX, int NU, int IPW, int WPB, int MW>
@@ -251,7 +277,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 {
     using Gm = Geometry<T, NX, NU, IPW, WPB>;
     constexpr int NZ = Gm::NZ, G = Gm::G, R = Gm::R, RM = Gm::RM, RF = Gm::RF;
-    constexpr int LDZ = Gm::LDZ, LDX = Gm::LDX, NUT = NU * (NU + 1) / 2;
+    constexpr int LDZ = Gm::LDZ, LDX = Gm::LDX, NUT = Gm::NUT;
+    constexpr int RSF = Gm::RSF, RSC = Gm::RSC, NSF = Gm::NSF, NSC = Gm::NSC, RB1 = Gm::RB1;
+    constexpr int FK = 0, FKFF = NU * NX, FRE = NU * NX + NU;   // frec fields
+    constexpr int CFI = 0, CPR = NUT, CGH = NUT + NX;           // crec fields
+    constexpr int DF = NMPC_STREAM_DEPTH;                        // records in flight
 
     __shared__ __attribute__((aligned(16))) T lds[Gm::LDS_ELEMS];
     T *cab = lds + Gm::C_AB, *ch = lds + Gm::C_H, *che = lds + Gm::C_HE, *cc = lds + Gm::C_C;
@@ -268,7 +298,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     const int rg = ll / NZ;
     const bool gridl = rg < R;
     const int N = p.N;
-    T *w = lds + Gm::C_TOT + (wave * IPW + grp) * Gm::I_TOT;
+    T *w = lds + Gm::C_TOT + (wave * IPW + grp) * Gm::I_ALL;
     T *fp = w + Gm::I_FP, *mt = w + Gm::I_MT, *hv = w + Gm::I_HV, *vv = w + Gm::I_VV, *pv = w + Gm::I_PV;
     T *rv = w + Gm::I_RV, *sv = w + Gm::I_SV, *kl = w + Gm::I_KL, *du_l = w + Gm::I_DU, *zw = w + Gm::I_FP;
 
@@ -299,7 +329,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                                             (int)(IPW * L.total * sizeof(T)), 0x00020000);
     S.go = (unsigned)grp * (unsigned)(L.total * sizeof(T));
     const unsigned Lz = L.z, Lll = L.ll, Llu = L.lu, Lgc = L.gc, Lgf = L.gf, Lsg = L.sg, Ldza = L.dza, Ldz = L.dz;
-    const unsigned Lre = L.re, Lpr = L.pr, Lkst = L.kst, Lfinv = L.finv, Lkff = L.kff;
+    const unsigned Lfrec = L.frec, Lcrec = L.crec;
+    T *rb = w + Gm::I_RB;
     const T *yref = p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
     const T *x0 = p.x0 + (size_t)inst * NX;
     const int nel = (N + 1) * NZ;
@@ -388,36 +419,62 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     const unsigned long long tstart = timed ? __builtin_amdgcn_s_memtime() : 0ull;
 #endif
 
+    // ---- stage-record streaming for the B/C/D recursions: records are loaded DF stages ahead
+    // into registers and written to the LDS ring one stage before use
+    auto rec_issue = [&](T (&r)[NSF + NSC], int k, bool with_c) {
+        const unsigned kk = (unsigned)(k < 0 ? 0 : (k < N ? k : N - 1));
+#pragma unroll
+        for (int s_ = 0; s_ < NSF; s_++) r[s_] = S.ld(Lfrec + kk * RSF + s_ * G, ll);
+        if (with_c) {
+#pragma unroll
+            for (int s_ = 0; s_ < NSC; s_++) r[NSF + s_] = S.ld(Lcrec + kk * RSC + s_ * G, ll);
+        }
+    };
+    auto rec_put = [&](const T (&r)[NSF + NSC], int buf, bool with_c) {
+        T *dstp = rb + buf * RB1;
+#pragma unroll
+        for (int s_ = 0; s_ < NSF; s_++) dstp[s_ * G + ll] = r[s_];
+        if (with_c) {
+#pragma unroll
+            for (int s_ = 0; s_ < NSC; s_++) dstp[(NSF + s_) * G + ll] = r[NSF + s_];
+        }
+    };
+    // The ring registers r[j] hold the records m = j (mod DF); the stage loops are unrolled by DF
+    // so that every slot is a fixed register set (moving an in-flight load's destination would
+    // force a wait on it).
+
     // ---- forward recursion shared by predictor (dst = dza) and corrector (dst = dz):
     // dx_0 = 0 (x0 pinned), du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx; du] + re_k
     auto forward = [&](unsigned dst) {
         T *dxb = w + Gm::I_DX;
         if (ll < NX) dxb[ll] = T(0);
-        T krow[NX], kff = 0, re = 0;
-        auto fetch_k = [&](int k) {
+        T r[DF][NSF + NSC];
 #pragma unroll
-            for (int i = 0; i < NX; i++) krow[i] = S.ld(Lkst + k * NU * NX + i, ll * NX);
-        };
-        fetch_k(0);
-        kff = S.ld(Lkff, ll);
-        re = S.ld(Lre, ll);
+        for (int j = 0; j < DF; j++) rec_issue(r[j], j, false);
+        rec_put(r[0], 0, false);
+        rec_issue(r[0], DF, false);
         WAVE_SYNC();
         int cur = 0;
-        for (int k = 0; k < N; k++) {
+        for (int kb = 0; kb < N; kb += DF)
+#pragma unroll
+        for (int j = 0; j < DF; j++) {
+            const int k = kb + j;
+            if (k >= N) break;
+            const T *rec = rb + (k & 1) * RB1;
             const T *dxc = dxb + cur * LDX;
             T *dxn = dxb + (1 - cur) * LDX;
-            const unsigned kn = (unsigned)(k + 1 < N ? k + 1 : N - 1);
-            const T kff_n = S.ld(Lkff + kn * NU, ll), re_n = S.ld(Lre + kn * NX, ll);
-            if (ll < NU) du_l[ll] = dot2<NX>(kff, [&](int i) { return krow[i]; }, [&](int i) { return dxc[i]; });
+            if (ll < NU) {
+                du_l[ll] = dot2<NX>(rec[FKFF + ll], [&](int i) { return rec[FK + ll * NX + i]; },
+                                    [&](int i) { return dxc[i]; });
+            }
             WAVE_SYNC();
-            fetch_k(kn);
             if (ll < NX) {
-                dxn[ll] = dot2<NZ>(re, [&](int j) { return cab[ll * LDZ + j]; },
+                dxn[ll] = dot2<NZ>(rec[FRE + ll], [&](int j) { return cab[ll * LDZ + j]; },
                                    [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
             }
             if (ll < NZ) S.st(dst + k * NZ, ll, ll < NX ? dxc[ll] : du_l[ll - NX]);
-            kff = kff_n;
-            re = re_n;
+            rec_put(r[(j + 1) % DF], (k + 1) & 1, false);
+            rec_issue(r[(j + 1) % DF], k + 1 + DF, false);
             cur = 1 - cur;
             WAVE_SYNC();
         }
@@ -495,8 +552,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             for (int e = k0 * NX + ll; e < min(k1, N) * NX; e += G) {
                 const int k = e / NX, i = e - k * NX;
                 const T *zk = zw + (k - k0) * NZ;
-                S.st(Lre, e, dot2<NZ>(cc[i] - zk[NZ + i], [&](int j) { return cab[i * LDZ + j]; },
-                                      [&](int j) { return zk[j]; }));
+                S.st(Lfrec + k * RSF + FRE, i, dot2<NZ>(cc[i] - zk[NZ + i], [&](int j) { return cab[i * LDZ + j]; },
+                                                        [&](int j) { return zk[j]; }));
             }
             WAVE_SYNC();
         }
@@ -513,7 +570,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 const unsigned kk = (unsigned)(k < 0 ? 0 : k);
                 q.sg = S.ld(Lsg + kk * NZ, ll);
                 q.g = S.ld(Lgf + kk * NZ, ll);
-                q.re = S.ld(Lre + (kk < (unsigned)N ? kk : N - 1) * NX, ll);
+                q.re = S.ld(Lfrec + (kk < (unsigned)N ? kk : N - 1) * RSF + FRE, ll);
             };
             // P_N = He + Sigma_N, p_N = g_N
             {
@@ -540,12 +597,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             for (int k = N - 1; k >= 0; k--) {
                 PreA qn{};
                 fetch_a(k - 1, qn);
+                NMPC_PTICK(-1);
                 // 1: Pr = P re, v = Pr + p, M^T = (P [A B])^T
                 T abcol[NX];
                 load_abcol(abcol);
                 if (ll < NX) {
                     const T s = dot2<NX>(T(0), [&](int l) { return fp[ll * LDZ + l]; }, [&](int l) { return rv[l]; });
-                    S.st(Lpr + k * NX, ll, s);
+                    S.st(Lcrec + k * RSC + CPR, ll, s);
                     vv[ll] = s + pv[ll];
                 }
                 if (gridl) {
@@ -559,6 +617,7 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     }
                 }
                 WAVE_SYNC();
+                NMPC_PTICK(0);
                 // 2: F = [A B]' M + H + Sigma (row col), h = [A B]' v + g
                 if (gridl) {
 _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
@@ -574,6 +633,7 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     if (rg == 0) hv[col] = dot2<NX>(q.g, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
                 }
                 WAVE_SYNC();
+                NMPC_PTICK(1);
                 // 3: F_uu^-1 (wave-uniform Cholesky), K = -F_uu^-1 F_ux, kff, p_k
                 T lf[NUT];
 #pragma unroll
@@ -604,7 +664,7 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     for (int u = 0; u < NU; u++) {
                         kc[u] = -kc[u];
                         kl[u * LDX + ll] = kc[u];
-                        S.st(Lkst + k * NU * NX + u * NX, ll, kc[u]);
+                        S.st(Lfrec + k * RSF + FK + u * NX, ll, kc[u]);
                         s += kc[u] * hu[u];
                     }
                     if (k > 0) pv[ll] = s;
@@ -619,10 +679,11 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     for (int j = 0; j < NU; j++) mine = (ll == j) ? -x[j] : mine;
 #pragma unroll
                     for (int j = 0; j < NUT; j++) lmine = (ll == j) ? lf[j] : lmine;
-                    if (ll < NU) S.st(Lkff + k * NU, ll, mine);
-                    if (ll < NUT) S.st(Lfinv + k * NUT, ll, lmine);
+                    if (ll < NU) S.st(Lfrec + k * RSF + FKFF, ll, mine);
+                    if (ll < NUT) S.st(Lcrec + k * RSC + CFI, ll, lmine);
                 }
                 WAVE_SYNC();
+                NMPC_PTICK(2);
                 // 4: P_k = F_xx + F_xu K (in place); next stage's re and Sigma -> LDS
                 if (k > 0) {
                     if (gridl && col < NX) {
@@ -645,6 +706,7 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                 }
                 q = qn;
                 WAVE_SYNC();
+                NMPC_PTICK(3);
             }
         }
         SWEEP_FENCE();
@@ -698,57 +760,54 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                 const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t), dl = -lam_u * (T(1) - dza * it_);
                 g += (dl * dza + smu) * it_;
             }
-            S.st(Lgf, e, g);
+            if (k < N) S.st(Lcrec + k * RSC + CGH, i, g);
+            else S.st(Lgf, e, g);
         }
         SWEEP_FENCE();
         NMPC_TICK(4);
 
         // ============================ C: backward corrector vector (kff, p)
         {
-            struct PreC {
-                T g, pr;
-            };
-            auto fetch_c = [&](int k, PreC &q) {
-                const unsigned kk = (unsigned)(k < 0 ? 0 : k);
-                q.g = S.ld(Lgf + kk * NZ, ll);
-                q.pr = S.ld(Lpr + (kk < (unsigned)N ? kk : N - 1) * NX, ll);
-            };
             {
                 const T gN = S.ld(Lgf + N * NZ, ll);
                 if (ll < NX) pv[ll] = gN;
             }
-            PreC q{};
-            fetch_c(N - 1, q);
+            T r[DF][NSF + NSC];
+#pragma unroll
+            for (int j = 0; j < DF; j++) rec_issue(r[j], N - 1 - j, true);
+            rec_put(r[0], 0, true);
+            rec_issue(r[0], N - 1 - DF, true);
             WAVE_SYNC();
-            for (int k = N - 1; k >= 0; k--) {
+            for (int kb = N - 1; kb >= 0; kb -= DF)
+#pragma unroll
+            for (int j = 0; j < DF; j++) {
+                const int k = kb - j;
+                if (k < 0) break;
+                const T *fr = rb + ((N - 1 - k) & 1) * RB1, *cr = fr + NSF * G;
                 T abcol[NX];
                 load_abcol(abcol);
-                T lf[NUT], kc[NU];
-#pragma unroll
-                for (int j = 0; j < NUT; j++) lf[j] = S.ld(Lfinv + k * NUT + j, 0);
-#pragma unroll
-                for (int u = 0; u < NU; u++) kc[u] = S.ld(Lkst + k * NU * NX + u * NX, ll);
-                PreC qn{};
-                fetch_c(k - 1, qn);
-                if (ll < NX) vv[ll] = q.pr + pv[ll];
+                if (ll < NX) vv[ll] = cr[CPR + ll] + pv[ll];
                 WAVE_SYNC();
-                if (ll < NZ) hv[ll] = dot2<NX>(q.g, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
+                if (ll < NZ) hv[ll] = dot2<NX>(cr[CGH + ll], [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
                 WAVE_SYNC();
-                T hu[NU], x[NU];
+                T lf[NUT], hu[NU], x[NU];
+#pragma unroll
+                for (int j = 0; j < NUT; j++) lf[j] = cr[CFI + j];
 #pragma unroll
                 for (int j = 0; j < NU; j++) x[j] = hu[j] = hv[NX + j];
                 chol_solve<T, NU>(lf, x);
                 T mine = 0;
 #pragma unroll
                 for (int j = 0; j < NU; j++) mine = (ll == j) ? -x[j] : mine;
-                if (ll < NU) S.st(Lkff + k * NU, ll, mine);
+                if (ll < NU) S.st(Lfrec + k * RSF + FKFF, ll, mine);
                 if (k > 0 && ll < NX) {
-                    T s = hv[ll];
+                    T s_ = hv[ll];
 #pragma unroll
-                    for (int u = 0; u < NU; u++) s += kc[u] * hu[u];
-                    pv[ll] = s;
+                    for (int u = 0; u < NU; u++) s_ += fr[FK + u * NX + ll] * hu[u];
+                    pv[ll] = s_;
                 }
-                q = qn;
+                rec_put(r[(j + 1) % DF], (N - k) & 1, true);
+                rec_issue(r[(j + 1) % DF], k - 1 - DF, true);
                 WAVE_SYNC();
             }
         }
