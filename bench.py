@@ -16,8 +16,12 @@ Also reported (one JSON line on rank 0):
   roofline — the solve kernel (the dominant kernel): algorithmic flops per launch = SURVEY
     §8d F_iter x n_ipm (mean IPM iterations of the CPU baseline on the same inputs) x B,
     divided by the kernel's mean duration from HIP events around each launch;
-    peak = MI355X FP64 78.6 TFLOP/s (FP32 157.3); traffic = HBM bytes per launch from the
-    rocprofv3 PMC pass committed under profiles/ when one matches this config, else null.
+    bound "mfma" = the dense FP64 FMA roofline: peak = MI355X FP64 78.6 TFLOP/s, the rate of
+    both the FP64 matrix and the FP64 vector pipe (half the 157.3 TFLOP/s F32 rate of
+    MI355X_MICROARCH.md); the kernel issues its FP64 FMAs on the vector pipe (DESIGN.md §4
+    explains why 17-wide stage operands do not pay on MFMA). traffic = memory-side bytes per
+    launch (FETCH_SIZE + WRITE_SIZE) from the rocprofv3 PMC passes committed under profiles/
+    (profiles/pmc_traffic.json) when one matches this config, else null.
   cpu_baseline — oracle/c/riccati_ipm.c (same algorithm, fp64, OpenMP over instances) on the
     host cores, rank 0 at N=1 only, on a bounded sample of the same instances.
 """
@@ -173,7 +177,7 @@ def main():
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"instance-sharded x{world}, RCCL stats reduce",
                        "instances_per_wave": cl.solver.launch_info()["instances_per_wave"]},
-            "roofline": {"bound": "fp64-valu" if args.precision == "fp64" else "fp32-valu",
+            "roofline": {"bound": "mfma", "pipe": "fp64 FMA on VALU" if args.precision == "fp64" else "fp32 FMA on VALU",
                          "kernel": "ipm_kernel", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic,
                          "flops_per_launch": fl_launch, "kernel_ms": kernel_ms,

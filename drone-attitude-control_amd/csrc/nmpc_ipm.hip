@@ -947,7 +947,7 @@ int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_o
     for (int i = 0; i < n; i++) {
         if (t[i].nx != nx || t[i].nu != nu) continue;
         if (ipw_req > 0) {
-            if (t[i].ipw == ipw_req) best = i;
+            if (t[i].ipw == ipw_req && best < 0) best = i;   // first listed = preferred variant
         } else if (best < 0 || t[i].ipw > t[best].ipw) {
             best = i;
         }

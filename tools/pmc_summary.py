@@ -1,0 +1,82 @@
+"""Summarise the rocprofv3 PMC passes of tools/pmc.sh for one kernel.
+
+    python tools/pmc_summary.py TAG [--kernel ipm_kernel] [--out profiles/r1_pmc_TAG.json]
+        [--traffic model,N,batch,precision]
+
+Reads gpurun_out/pmc_<TAG>_<i>/run_counter_collection.csv (one counter group per pass),
+averages each counter over the dispatches of the kernel, and writes the per-dispatch means.
+With --traffic it also records, in profiles/pmc_traffic.json, the memory-side bytes per
+launch that bench.py reports as roofline.traffic:
+
+    traffic = (FETCH_SIZE + WRITE_SIZE) * 1024   [both counters are in KiB]
+
+FETCH_SIZE/WRITE_SIZE count L2 <-> fabric requests, so Infinity-Cache (MALL) hits are
+included. The gfx950 x2 correction of MICROARCH.md applies to 16-B-per-lane streaming reads;
+this kernel's scratch reads are 8-B-per-lane buffer loads, so FETCH_SIZE is used as reported
+(uncalibrated for that width, as the guide warns).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def collect(tag, kernel):
+    vals = defaultdict(lambda: defaultdict(float))   # counter -> dispatch -> value (summed over dims)
+    meta = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_*", "*counter_collection.csv"))):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel not in row["Kernel_Name"]:
+                    continue
+                d = (f, row["Dispatch_Id"])
+                vals[row["Counter_Name"]][d] += float(row["Counter_Value"])
+                meta = {"kernel": row["Kernel_Name"][:160], "grid": int(row["Grid_Size"]),
+                        "workgroup": int(row["Workgroup_Size"]), "vgpr": int(row["VGPR_Count"]),
+                        "sgpr": int(row["SGPR_Count"]), "lds_block": int(row["LDS_Block_Size"])}
+    means = {c: sum(v.values()) / len(v) for c, v in vals.items() if v}
+    ndisp = {c: len(v) for c, v in vals.items()}
+    return means, ndisp, meta
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--kernel", default="ipm_kernel")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--traffic", default=None, help="model,N,batch,precision")
+    a = ap.parse_args()
+    means, ndisp, meta = collect(a.tag, a.kernel)
+    if not means:
+        raise SystemExit(f"no {a.kernel} dispatches found for tag {a.tag}")
+    res = {"tag": a.tag, "kernel": meta, "dispatches_per_counter": ndisp, "mean_per_dispatch": means}
+    if "SQ_WAVE_CYCLES" in means and means.get("SQ_WAVES"):
+        w = means["SQ_WAVES"]
+        res["per_wave"] = {k: v / w for k, v in means.items() if k.startswith("SQ_")}
+    if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
+        res["traffic_bytes_per_launch"] = (means["FETCH_SIZE"] + means["WRITE_SIZE"]) * 1024.0
+    out = a.out or os.path.join(ROOT, "profiles", f"pmc_{a.tag}.json")
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({k: res[k] for k in res if k != "per_wave"}, indent=1))
+    if a.traffic and "traffic_bytes_per_launch" in res:
+        model, N, batch, prec = a.traffic.split(",")
+        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        d = json.load(open(path)) if os.path.exists(path) else {"entries": []}
+        d["note"] = ("memory-side bytes per ipm_kernel launch = (FETCH_SIZE + WRITE_SIZE) x 1024 from "
+                     "rocprofv3 PMC passes (tools/pmc.sh, tools/pmc_summary.py); includes Infinity-Cache hits")
+        key = (model, int(N), int(batch), prec)
+        d["entries"] = [e for e in d["entries"] if (e["model"], e["N"], e["batch"], e["precision"]) != key]
+        d["entries"].append({"model": model, "N": int(N), "batch": int(batch), "precision": prec,
+                             "hbm_bytes_per_launch": res["traffic_bytes_per_launch"],
+                             "source": os.path.relpath(out, ROOT)})
+        with open(path, "w") as fh:
+            json.dump(d, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
