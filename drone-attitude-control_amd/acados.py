@@ -167,6 +167,66 @@ def _arr(v, n=None, dtype=float):
     return a
 
 
+def describe_ocp(ocp):
+    """Numeric description of an AcadosOcp as the engine consumes it (no GPU needed):
+    dynamics (continuous affine + integrator, or discrete), LINEAR_LS weights/selectors,
+    bounds with acados's infinity mapped to none, horizon, tolerances. Raises for anything
+    outside the supported class (the reference's OCPs, force_model/ocp.py:21-93,
+    jerk_model/ocp.py:20-92, are inside it)."""
+    opts, cost, cons, model = ocp.solver_options, ocp.cost, ocp.constraints, ocp.model
+    if cost.cost_type != "LINEAR_LS" or cost.cost_type_e != "LINEAR_LS":
+        raise NotImplementedError("only LINEAR_LS costs are supported (force_model/ocp.py:28-29)")
+    if opts.hessian_approx != "GAUSS_NEWTON":
+        raise NotImplementedError("only GAUSS_NEWTON Hessians are supported")
+    if opts.nlp_solver_type not in ("SQP", "SQP_RTI"):
+        raise NotImplementedError(f"nlp_solver_type {opts.nlp_solver_type}")
+    N = opts.N_horizon if opts.N_horizon is not None else ocp.dims.N
+    if N is None or opts.tf is None:
+        raise ValueError("solver_options.N_horizon and solver_options.tf must be set")
+    if cons.x0 is None:
+        raise NotImplementedError("the engine pins x0 at stage 0 (constraints.x0 must be set)")
+    if opts.integrator_type == "DISCRETE":
+        A, B, c = (np.atleast_2d(np.asarray(model.disc_dyn_A, float)),
+                   np.atleast_2d(np.asarray(model.disc_dyn_B, float)),
+                   np.asarray(model.disc_dyn_c, float).ravel())
+        dyn_type, integ = _lib.NMPC_DYN_DISCRETE_AFFINE, _lib.NMPC_ERK
+    else:
+        A, B, c = affine_form(model)
+        dyn_type = _lib.NMPC_DYN_CONTINUOUS_AFFINE
+        integ = {"IRK": _lib.NMPC_IRK, "ERK": _lib.NMPC_ERK}.get(opts.integrator_type)
+        if integ is None:
+            raise NotImplementedError(f"integrator_type {opts.integrator_type}")
+    nx, nu = B.shape
+    W = np.atleast_2d(np.asarray(cost.W, float))
+    W_e = np.atleast_2d(np.asarray(cost.W_e, float)) if cost.W_e is not None else np.zeros((0, 0))
+
+    def bounds(lb, ub, idx):
+        idx = _arr(idx, None, np.int32)
+        lb, ub = _arr(lb, idx.size), _arr(ub, idx.size)
+        # acados_template's ACADOS_INFTY magnitude means "no bound"
+        lb = np.where(np.abs(lb) >= ACADOS_INFTY, -1e30, lb)
+        ub = np.where(np.abs(ub) >= ACADOS_INFTY, 1e30, ub)
+        return lb, ub, idx
+
+    lbu, ubu, idxbu = bounds(cons.lbu, cons.ubu, cons.idxbu)
+    lbx, ubx, idxbx = bounds(cons.lbx, cons.ubx, cons.idxbx)
+    lbx_e, ubx_e, idxbx_e = bounds(cons.lbx_e, cons.ubx_e, cons.idxbx_e)
+    return dict(
+        name=model.name or "ocp", nx=nx, nu=nu, N=int(N), ny=W.shape[0], ny_e=W_e.shape[0],
+        dyn_type=dyn_type, A=A, B=B, c=c, integrator_type=integ,
+        integrator=opts.integrator_type, num_stages=int(opts.sim_method_num_stages),
+        num_steps=int(opts.sim_method_num_steps), tf=float(opts.tf),
+        W=W, Vx=np.asarray(cost.Vx, float), Vu=np.asarray(cost.Vu, float), W_e=W_e,
+        Vx_e=np.asarray(cost.Vx_e, float) if cost.Vx_e is not None else np.zeros((0, nx)),
+        yref=cost.yref, yref_e=cost.yref_e, cost_scaling=opts.cost_scaling,
+        lbu=lbu, ubu=ubu, idxbu=idxbu, lbx=lbx, ubx=ubx, idxbx=idxbx,
+        lbx_e=lbx_e, ubx_e=ubx_e, idxbx_e=idxbx_e, x0=_arr(cons.x0, nx),
+        qp_solver_iter_max=int(opts.qp_solver_iter_max or 0),
+        qp_solver_tol_comp=float(opts.qp_solver_tol_comp or (opts.qp_tol or 0.0) or 0.0),
+        qp_solver_tol_res=float(opts.qp_solver_tol_stat or 0.0),
+        qp_solver_mu0=float(opts.qp_solver_mu0 or 0.0))
+
+
 class AcadosOcpSolver:
     """Batched drop-in for acados_template.AcadosOcpSolver (force_model/ocp.py:95-96)."""
 
@@ -174,37 +234,11 @@ class AcadosOcpSolver:
                  *, batch=1, device=0, precision="fp64"):
         ocp = acados_ocp
         self.lib = _lib.load()
-        opts, cost, cons, model = ocp.solver_options, ocp.cost, ocp.constraints, ocp.model
-        if cost.cost_type != "LINEAR_LS" or cost.cost_type_e != "LINEAR_LS":
-            raise NotImplementedError("only LINEAR_LS costs are supported (force_model/ocp.py:28-29)")
-        if opts.hessian_approx != "GAUSS_NEWTON":
-            raise NotImplementedError("only GAUSS_NEWTON Hessians are supported")
-        if opts.nlp_solver_type not in ("SQP", "SQP_RTI"):
-            raise NotImplementedError(f"nlp_solver_type {opts.nlp_solver_type}")
-        N = opts.N_horizon if opts.N_horizon is not None else ocp.dims.N
-        if N is None or opts.tf is None:
-            raise ValueError("solver_options.N_horizon and solver_options.tf must be set")
-        if cons.x0 is None:
-            raise NotImplementedError("the engine pins x0 at stage 0 (constraints.x0 must be set)")
-        if opts.integrator_type == "DISCRETE":
-            A, B, c = (np.atleast_2d(np.asarray(model.disc_dyn_A, float)),
-                       np.atleast_2d(np.asarray(model.disc_dyn_B, float)),
-                       np.asarray(model.disc_dyn_c, float).ravel())
-            dyn_type, integ = _lib.NMPC_DYN_DISCRETE_AFFINE, _lib.NMPC_ERK
-        else:
-            A, B, c = affine_form(model)
-            dyn_type = _lib.NMPC_DYN_CONTINUOUS_AFFINE
-            integ = {"IRK": _lib.NMPC_IRK, "ERK": _lib.NMPC_ERK}.get(opts.integrator_type)
-            if integ is None:
-                raise NotImplementedError(f"integrator_type {opts.integrator_type}")
-        nx, nu = B.shape
-        W = np.atleast_2d(np.asarray(cost.W, float))
-        ny = W.shape[0]
-        W_e = np.atleast_2d(np.asarray(cost.W_e, float)) if cost.W_e is not None else np.zeros((0, 0))
-        ny_e = W_e.shape[0]
-        self.nx, self.nu, self.N, self.ny, self.ny_e = nx, nu, int(N), ny, ny_e
+        D = describe_ocp(ocp)
+        nx, nu, N, ny, ny_e = D["nx"], D["nu"], D["N"], D["ny"], D["ny_e"]
+        self.nx, self.nu, self.N, self.ny, self.ny_e = nx, nu, N, ny, ny_e
         self.batch = int(batch)
-        self.name = model.name or "ocp"
+        self.name = D["name"]
         self.precision = precision
         prec = {"fp64": _lib.NMPC_FP64, "fp32": _lib.NMPC_FP32}[precision]
 
@@ -214,47 +248,37 @@ class AcadosOcpSolver:
             keep[name] = _arr(v, n, dtype)
             return _lib.iptr(keep[name]) if dtype is np.int32 else _lib.dptr(keep[name])
 
-        def bounds(lb, ub, idx):
-            idx = _arr(idx, None, np.int32)
-            lb, ub = _arr(lb, idx.size), _arr(ub, idx.size)
-            # acados_template's ACADOS_INFTY magnitude means "no bound"
-            lb = np.where(np.abs(lb) >= ACADOS_INFTY, -1e30, lb)
-            ub = np.where(np.abs(ub) >= ACADOS_INFTY, 1e30, ub)
-            return lb, ub, idx
-
-        lbu, ubu, idxbu = bounds(cons.lbu, cons.ubu, cons.idxbu)
-        lbx, ubx, idxbx = bounds(cons.lbx, cons.ubx, cons.idxbx)
-        lbx_e, ubx_e, idxbx_e = bounds(cons.lbx_e, cons.ubx_e, cons.idxbx_e)
-        tol_comp = opts.qp_solver_tol_comp or (opts.qp_tol or 0.0)
         d = _lib.OcpDesc()
         d.abi_version = _lib.NMPC_ABI_VERSION
         keep["name"] = self.name.encode()
         d.name = keep["name"]
-        d.nx, d.nu, d.N, d.ny, d.ny_e = nx, nu, int(N), ny, ny_e
-        d.dyn_type = dyn_type
-        d.A, d.B, d.c = P("A", A, nx * nx), P("B", B, nx * nu), P("c", c, nx)
-        d.integrator_type = integ
-        d.num_stages = int(opts.sim_method_num_stages)
-        d.num_steps = int(opts.sim_method_num_steps)
-        d.tf = float(opts.tf)
-        d.W, d.Vx, d.Vu = P("W", W, ny * ny), P("Vx", cost.Vx, ny * nx), P("Vu", cost.Vu, ny * nu)
+        d.nx, d.nu, d.N, d.ny, d.ny_e = nx, nu, N, ny, ny_e
+        d.dyn_type = D["dyn_type"]
+        d.A, d.B, d.c = P("A", D["A"], nx * nx), P("B", D["B"], nx * nu), P("c", D["c"], nx)
+        d.integrator_type = D["integrator_type"]
+        d.num_stages = D["num_stages"]
+        d.num_steps = D["num_steps"]
+        d.tf = D["tf"]
+        d.W, d.Vx, d.Vu = P("W", D["W"], ny * ny), P("Vx", D["Vx"], ny * nx), P("Vu", D["Vu"], ny * nu)
         if ny_e:
-            d.W_e, d.Vx_e = P("W_e", W_e, ny_e * ny_e), P("Vx_e", cost.Vx_e, ny_e * nx)
-        if cost.yref is not None:
-            d.yref = P("yref", cost.yref, ny)
-        if cost.yref_e is not None and ny_e:
-            d.yref_e = P("yref_e", cost.yref_e, ny_e)
-        d.cost_scaling = (_lib.NMPC_COST_SCALING_TIME_STEPS if opts.cost_scaling == "time_steps"
+            d.W_e, d.Vx_e = P("W_e", D["W_e"], ny_e * ny_e), P("Vx_e", D["Vx_e"], ny_e * nx)
+        if D["yref"] is not None:
+            d.yref = P("yref", D["yref"], ny)
+        if D["yref_e"] is not None and ny_e:
+            d.yref_e = P("yref_e", D["yref_e"], ny_e)
+        d.cost_scaling = (_lib.NMPC_COST_SCALING_TIME_STEPS if D["cost_scaling"] == "time_steps"
                           else _lib.NMPC_COST_SCALING_NONE)
-        d.nbu, d.idxbu, d.lbu, d.ubu = idxbu.size, P("idxbu", idxbu, None, np.int32), P("lbu", lbu), P("ubu", ubu)
-        d.nbx, d.idxbx, d.lbx, d.ubx = idxbx.size, P("idxbx", idxbx, None, np.int32), P("lbx", lbx), P("ubx", ubx)
-        d.nbx_e, d.idxbx_e = idxbx_e.size, P("idxbx_e", idxbx_e, None, np.int32)
-        d.lbx_e, d.ubx_e = P("lbx_e", lbx_e), P("ubx_e", ubx_e)
-        d.x0 = P("x0", cons.x0, nx)
-        d.qp_solver_iter_max = int(opts.qp_solver_iter_max or 0)
-        d.qp_solver_tol_comp = float(tol_comp or 0.0)
-        d.qp_solver_tol_res = float(opts.qp_solver_tol_stat or 0.0)
-        d.qp_solver_mu0 = float(opts.qp_solver_mu0 or 0.0)
+        d.nbu, d.idxbu = D["idxbu"].size, P("idxbu", D["idxbu"], None, np.int32)
+        d.lbu, d.ubu = P("lbu", D["lbu"]), P("ubu", D["ubu"])
+        d.nbx, d.idxbx = D["idxbx"].size, P("idxbx", D["idxbx"], None, np.int32)
+        d.lbx, d.ubx = P("lbx", D["lbx"]), P("ubx", D["ubx"])
+        d.nbx_e, d.idxbx_e = D["idxbx_e"].size, P("idxbx_e", D["idxbx_e"], None, np.int32)
+        d.lbx_e, d.ubx_e = P("lbx_e", D["lbx_e"]), P("ubx_e", D["ubx_e"])
+        d.x0 = P("x0", D["x0"], nx)
+        d.qp_solver_iter_max = D["qp_solver_iter_max"]
+        d.qp_solver_tol_comp = D["qp_solver_tol_comp"]
+        d.qp_solver_tol_res = D["qp_solver_tol_res"]
+        d.qp_solver_mu0 = D["qp_solver_mu0"]
         h = ctypes.c_void_p()
         rc = self.lib.nmpc_create(ctypes.byref(d), self.batch, int(device), prec, ctypes.byref(h))
         if rc != 0:
@@ -427,6 +451,10 @@ class AcadosSimSolver:
         m = sim.model
         mass = getattr(m, "plant_mass", None)
         g = getattr(m, "plant_g", None)
+        if (mass is None or g is None) and m.f_expl_expr is not None and hasattr(m.f_expl_expr, "affine_coefficients"):
+            # CasADi-SX model (the reference's plant.py through the shim): recognise the plant
+            from .casadi_shim import crazyflie_plant_params
+            mass, g = crazyflie_plant_params(m.f_expl_expr, m.x, m.u)
         if mass is None or g is None:
             raise NotImplementedError("AcadosSimSolver supports the 2-D Crazyflie plant model (src/plant.py)")
         self.mass, self.g = float(mass), float(g)
