@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, the default); gloo only to rehearse several ranks "
+                         "on a one-GPU box (ranks then share the visible GPUs round-robin)")
     return ap.parse_args()
 
 
@@ -102,28 +105,33 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local_rank
     if world > 1:
         # torch first: its HIP runtime (soname libamdhip64.so.7) is then shared by libnmpc_hip
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            device = local_rank % max(1, torch.cuda.device_count())
+            dist.init_process_group("gloo")
 
-    from drone_attitude_control_amd.batched import DEFAULT_N, ClosedLoop, flops_per_iter, workload
+    from drone_attitude_control_amd.batched import DEFAULT_N, ClosedLoop, flops_per_iter
+    from drone_attitude_control_amd.sharding import rank_workload, reduce_run
 
     model = args.model
     N = args.horizon or DEFAULT_N[model]
     B = args.batch
-    table, offsets_g, x_g = workload(model, N, B * world, args.seed)
-    sl = slice(rank * B, (rank + 1) * B)
-    cl = ClosedLoop(model, B, N=N, device=local_rank if world > 1 else 0, precision=args.precision,
-                    table=table, offsets=offsets_g[sl], x_init=x_g[sl], instance_base=rank * B, seed=args.seed)
+    table, offsets_r, x_r, base = rank_workload(model, N, B, world, rank, args.seed)
+    cl = ClosedLoop(model, B, N=N, device=device if world > 1 else 0, precision=args.precision,
+                    table=table, offsets=offsets_r, x_init=x_r, instance_base=base, seed=args.seed)
     nx, nu = cl.solver.nx, cl.solver.nu
 
     # CPU baseline first (rank 0, single-GPU runs only), on this rank's first-step inputs
     cpu, n_ipm_cpu = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, n_ipm_cpu = cpu_baseline(model, N, table, offsets_g[sl], x_g[sl], args.cpu_seconds)
+        cpu, n_ipm_cpu = cpu_baseline(model, N, table, offsets_r, x_r, args.cpu_seconds)
 
     def barrier():
         if dist is not None:
@@ -138,19 +146,9 @@ def main():
     elapsed = t1 - t0
     st = cl.stats()
     red = np.array([st["cost_sum"], st["aed_sum"], st["failed"], st["instance_steps"]])
-    if dist is not None:
-        import torch
-        te = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed = float(te.item())
-        tr = torch.tensor(red, dtype=torch.float64, device="cuda")
-        dist.all_reduce(tr, op=dist.ReduceOp.SUM)
-        red = tr.cpu().numpy()
-        tk = torch.tensor([st["solve_kernel_ms"] / max(1, st["solve_launches"])], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tk, op=dist.ReduceOp.MAX)
-        kernel_ms = float(tk.item())
-    else:
-        kernel_ms = st["solve_kernel_ms"] / max(1, st["solve_launches"])
+    # one SUM of the statistics and one MAX of the timings over RCCL, after the timed region
+    red, elapsed, kernel_ms = reduce_run(dist, red, elapsed, st["solve_kernel_ms"] / max(1, st["solve_launches"]),
+                                         device="cuda" if dist is not None and args.dist_backend == "nccl" else None)
 
     if rank == 0:
         value = world * B * args.steps / elapsed
@@ -182,6 +180,8 @@ def main():
                          "frac": achieved / peak, "traffic": traffic,
                          "flops_per_launch": fl_launch, "kernel_ms": kernel_ms,
                          "n_ipm": n_ipm, "gpu_mean_qp_iter": st["mean_qp_iter"]},
+            "solve_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "QP solves/s",
+                           "note": "ipm_kernel alone (mean launch duration from HIP events), all ranks"},
             "cpu_baseline": cpu,
             "closed_loop": {"mean_cost_per_step": red[0] / max(1.0, red[3]),
                             "aed": red[1] / max(1.0, red[3]) / (2 if model != "quad13" else 3),

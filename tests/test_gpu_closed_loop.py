@@ -67,3 +67,23 @@ def test_device_closed_loop_matches_oracle(data, N):
         assert np.abs(X - cl_gold[f"{model}_N{N}_X"][1:61]).max() < 1e-6
         st = loop.stats()
         assert st["failed"] == 0 and st["instance_steps"] == B * 60
+
+
+@pytest.mark.parametrize("model", ["force", "quad13"])
+def test_device_sharding_invariance(model):
+    """Two shards (instance_base 0 and 4) reproduce one 8-instance closed loop exactly: the
+    device noise is keyed by the global instance id, so results do not depend on
+    how instances are split over GPUs."""
+    from drone_attitude_control_amd.batched import ClosedLoop, DEFAULT_N
+    from drone_attitude_control_amd.sharding import rank_workload
+    N = DEFAULT_N[model]
+    table, off, x, _ = rank_workload(model, N, 8, 1, 0, seed=7)
+    full = ClosedLoop(model, 8, N=N, table=table, offsets=off, x_init=x, instance_base=0, seed=7)
+    full.run(5)
+    parts = []
+    for r in range(2):
+        t, o, xr, base = rank_workload(model, N, 4, 2, r, seed=7)
+        cl = ClosedLoop(model, 4, N=N, table=t, offsets=o, x_init=xr, instance_base=base, seed=7)
+        cl.run(5)
+        parts.append(cl.state())
+    assert np.abs(np.vstack(parts) - full.state()).max() <= 1e-12
