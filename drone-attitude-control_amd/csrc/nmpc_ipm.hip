@@ -240,8 +240,23 @@ struct Geometry {
     // per-instance work area; FP and MT are contiguous and double as the stage-z window of
     // the elementwise phase E_A (ZW elements)
     static constexpr int I_FP = 0, I_MT = I_FP + NZ * LDZ, I_RV = I_MT + NZ * LDX, I_SV = I_RV + LDX,
-                         I_VV = I_SV + LDZ, I_HV = I_VV + LDX, I_PV = I_HV + LDZ, I_KL = I_PV + LDX,
-                         I_DX = I_KL + NU * LDX, I_DU = I_DX + 2 * LDX, I_TOT = I_DU + LDU;
+                         I_VV = I_SV + LDZ, I_HV = I_VV + LDX, I_PV = I_HV + LDZ, I_GV = I_PV + LDX,
+                         I_DX = I_GV + LDZ, I_DU = I_DX + 2 * LDX, I_TOT = I_DU + LDU;
+    // symmetric stage matrices are computed as lower triangles: column c owns rows c..n-1 in
+    // chunks of E consecutive rows, one chunk per lane, E the smallest that fits G lanes
+    static constexpr int tri_lanes(int n, int E)
+    {
+        int s = 0;
+        for (int c = 0; c < n; c++) s += (n - c + E - 1) / E;
+        return s;
+    }
+    static constexpr int tri_chunk(int n)
+    {
+        int E = 1;
+        while (tri_lanes(n, E) > G) E++;
+        return E;
+    }
+    static constexpr int EF = tri_chunk(NZ), EP = tri_chunk(NX);
     static constexpr int ZW = NZ * LDZ + NZ * LDX;
     static constexpr int CH = ZW / NZ - 1;     // stages per E_A chunk (+1 stage of overlap)
     // stage-record ring of the B/C/D recursions: two buffers of (NSF + NSC) slots of G elements;
@@ -300,7 +315,26 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     const int N = p.N;
     T *w = lds + Gm::C_TOT + (wave * IPW + grp) * Gm::I_ALL;
     T *fp = w + Gm::I_FP, *mt = w + Gm::I_MT, *hv = w + Gm::I_HV, *vv = w + Gm::I_VV, *pv = w + Gm::I_PV;
-    T *rv = w + Gm::I_RV, *sv = w + Gm::I_SV, *kl = w + Gm::I_KL, *du_l = w + Gm::I_DU, *zw = w + Gm::I_FP;
+    T *rv = w + Gm::I_RV, *sv = w + Gm::I_SV, *gv = w + Gm::I_GV, *du_l = w + Gm::I_DU, *zw = w + Gm::I_FP;
+    // this lane's lower-triangle chunk of F (column fc, rows fb0..fb0+fn-1) and of P (pj, pi0, pn)
+    int fc = -1, fb0 = 0, fn = 0, pj = -1, pi0 = 0, pn = 0;
+    {
+        auto assign = [&](int n, int E, int &c_, int &r0, int &cnt) {
+            int idx = ll;
+#pragma unroll
+            for (int c = 0; c < n; c++) {
+                const int m = (n - c + E - 1) / E;
+                if (c_ < 0 && idx < m) {
+                    c_ = c;
+                    r0 = c + idx * E;
+                    cnt = min(E, n - r0);
+                }
+                idx -= m;
+            }
+        };
+        assign(NZ, Gm::EF, fc, fb0, fn);
+        assign(NX, Gm::EP, pj, pi0, pn);
+    }
 
     // ---- model constants -> LDS (once per workgroup)
     for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) cab[(e / NZ) * LDZ + e % NZ] = p.AB[e];
@@ -448,6 +482,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     auto forward = [&](unsigned dst) {
         T *dxb = w + Gm::I_DX;
         if (ll < NX) dxb[ll] = T(0);
+        T arow[NZ];   // row ll of [A B], register-resident for the whole sweep
+#pragma unroll
+        for (int j = 0; j < NZ; j++) arow[j] = cab[(ll < NX ? ll : 0) * LDZ + j];
         T r[DF][NSF + NSC];
 #pragma unroll
         for (int j = 0; j < DF; j++) rec_issue(r[j], j, false);
@@ -469,7 +506,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             }
             WAVE_SYNC();
             if (ll < NX) {
-                dxn[ll] = dot2<NZ>(rec[FRE + ll], [&](int j) { return cab[ll * LDZ + j]; },
+                dxn[ll] = dot2<NZ>(rec[FRE + ll], [&](int j) { return arow[j]; },
                                    [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
             }
             if (ll < NZ) S.st(dst + k * NZ, ll, ll < NX ? dxc[ll] : du_l[ll - NX]);
@@ -606,6 +643,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     S.st(Lcrec + k * RSC + CPR, ll, s);
                     vv[ll] = s + pv[ll];
                 }
+                if (ll < NZ) gv[ll] = q.g;
                 if (gridl) {
 _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     for (int qq = 0; qq < RM; qq++) {
@@ -618,57 +656,48 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                 }
                 WAVE_SYNC();
                 NMPC_PTICK(0);
-                // 2: F = [A B]' M + H + Sigma (row col), h = [A B]' v + g
-                if (gridl) {
-_Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
-                    for (int qq = 0; qq < RF; qq++) {
-                        const int bb = rg + R * qq;
-                        if (bb < NZ) {
-                            T s = dot2<NX>(ch[col * LDZ + bb], [&](int l) { return abcol[l]; },
-                                           [&](int l) { return mt[bb * LDX + l]; });
-                            if (bb == col) s += sv[col];
-                            fp[col * LDZ + bb] = s;
+                // 2: F = [A B]' M + H + Sigma, lower triangle by column chunks, mirrored;
+                //    h = [A B]' v + g by the first chunk of each column
+                if (fc >= 0) {
+                    T ac[NX];
+#pragma unroll
+                    for (int l = 0; l < NX; l++) ac[l] = cab[l * LDZ + fc];
+#pragma unroll
+                    for (int t = 0; t < Gm::EF; t++) {
+                        const int bb = fb0 + t;
+                        if (t < fn) {
+                            T s_ = dot2<NX>(ch[fc * LDZ + bb], [&](int l) { return ac[l]; },
+                                            [&](int l) { return mt[bb * LDX + l]; });
+                            if (bb == fc) s_ += sv[fc];
+                            fp[fc * LDZ + bb] = s_;
+                            fp[bb * LDZ + fc] = s_;
                         }
                     }
-                    if (rg == 0) hv[col] = dot2<NX>(q.g, [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
+                    if (fb0 == fc) hv[fc] = dot2<NX>(gv[fc], [&](int l) { return ac[l]; }, [&](int l) { return vv[l]; });
                 }
                 WAVE_SYNC();
                 NMPC_PTICK(1);
-                // 3: F_uu^-1 (wave-uniform Cholesky), K = -F_uu^-1 F_ux, kff, p_k
+                // 3: F_uu = L L' (wave-uniform), kff = -F_uu^-1 h_u; per P column j: K(:, j) =
+                //    -F_uu^-1 F_ux(:, j), p_j = h_j + K(:, j)' h_u, P(i, j) = F(i, j) + F_xu(i, :) K(:, j)
                 T lf[NUT];
 #pragma unroll
                 for (int i = 0; i < NU; i++)
 #pragma unroll
                     for (int j = 0; j <= i; j++) {
-                        T s = fp[(NX + i) * LDZ + NX + j];
+                        T s_ = fp[(NX + i) * LDZ + NX + j];
 #pragma unroll
-                        for (int l = 0; l < j; l++) s -= lf[tri(i, l)] * lf[tri(j, l)];
+                        for (int l = 0; l < j; l++) s_ -= lf[tri(i, l)] * lf[tri(j, l)];
                         if (i == j) {
-                            const bool pd = s > T(0);
+                            const bool pd = s_ > T(0);
                             fail |= active & !pd;
-                            lf[tri(i, i)] = frsq(pd ? s : T(1));
+                            lf[tri(i, i)] = frsq(pd ? s_ : T(1));
                         } else {
-                            lf[tri(i, j)] = s * lf[tri(j, j)];
+                            lf[tri(i, j)] = s_ * lf[tri(j, j)];
                         }
                     }
                 T hu[NU];
 #pragma unroll
                 for (int j = 0; j < NU; j++) hu[j] = hv[NX + j];
-                if (ll < NX) {
-                    T kc[NU];
-#pragma unroll
-                    for (int j = 0; j < NU; j++) kc[j] = fp[ll * LDZ + NX + j];
-                    chol_solve<T, NU>(lf, kc);
-                    T s = hv[ll];
-#pragma unroll
-                    for (int u = 0; u < NU; u++) {
-                        kc[u] = -kc[u];
-                        kl[u * LDX + ll] = kc[u];
-                        S.st(Lfrec + k * RSF + FK + u * NX, ll, kc[u]);
-                        s += kc[u] * hu[u];
-                    }
-                    if (k > 0) pv[ll] = s;
-                }
                 {
                     T x[NU];
 #pragma unroll
@@ -682,25 +711,38 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     if (ll < NU) S.st(Lfrec + k * RSF + FKFF, ll, mine);
                     if (ll < NUT) S.st(Lcrec + k * RSC + CFI, ll, lmine);
                 }
-                WAVE_SYNC();
-                NMPC_PTICK(2);
-                // 4: P_k = F_xx + F_xu K (in place); next stage's re and Sigma -> LDS
-                if (k > 0) {
-                    if (gridl && col < NX) {
-                        T fu[NU];
+                if (pj >= 0) {
+                    T kc[NU];
 #pragma unroll
-                        for (int u = 0; u < NU; u++) fu[u] = fp[col * LDZ + NX + u];
-_Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
-                        for (int qq = 0; qq < RM; qq++) {
-                            const int i = rg + R * qq;
-                            if (i < NX) {
-                                T s = fp[col * LDZ + i];
+                    for (int u = 0; u < NU; u++) kc[u] = fp[(NX + u) * LDZ + pj];
+                    chol_solve<T, NU>(lf, kc);
 #pragma unroll
-                                for (int u = 0; u < NU; u++) s += fu[u] * kl[u * LDX + i];
-                                fp[col * LDZ + i] = s;
+                    for (int u = 0; u < NU; u++) kc[u] = -kc[u];
+                    if (pi0 == pj) {
+                        T s_ = hv[pj];
+#pragma unroll
+                        for (int u = 0; u < NU; u++) {
+                            S.st(Lfrec + k * RSF + FK + u * NX, pj, kc[u]);
+                            s_ += kc[u] * hu[u];
+                        }
+                        if (k > 0) pv[pj] = s_;
+                    }
+                    if (k > 0) {
+#pragma unroll
+                        for (int t = 0; t < Gm::EP; t++) {
+                            const int i = pi0 + t;
+                            if (t < pn) {
+                                T s_ = fp[i * LDZ + pj];
+#pragma unroll
+                                for (int u = 0; u < NU; u++) s_ += fp[i * LDZ + NX + u] * kc[u];
+                                fp[i * LDZ + pj] = s_;
+                                fp[pj * LDZ + i] = s_;
                             }
                         }
                     }
+                }
+                // next stage's re and Sigma -> LDS (their last readers ran in phases 1 and 2)
+                if (k > 0) {
                     if (ll < NX) rv[ll] = qn.re;
                     if (ll < NZ) sv[ll] = qn.sg;
                 }
@@ -772,6 +814,8 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                 const T gN = S.ld(Lgf + N * NZ, ll);
                 if (ll < NX) pv[ll] = gN;
             }
+            T abcol[NX];   // column ll of [A B], register-resident for the whole sweep
+            load_abcol(abcol);
             T r[DF][NSF + NSC];
 #pragma unroll
             for (int j = 0; j < DF; j++) rec_issue(r[j], N - 1 - j, true);
@@ -784,8 +828,6 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                 const int k = kb - j;
                 if (k < 0) break;
                 const T *fr = rb + ((N - 1 - k) & 1) * RB1, *cr = fr + NSF * G;
-                T abcol[NX];
-                load_abcol(abcol);
                 if (ll < NX) vv[ll] = cr[CPR + ll] + pv[ll];
                 WAVE_SYNC();
                 if (ll < NZ) hv[ll] = dot2<NX>(cr[CGH + ll], [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
