@@ -210,7 +210,7 @@ struct nmpc_solver {
     void *d_scratch = nullptr;
     int *d_status = nullptr, *d_iters = nullptr;
     unsigned long long *d_cycles = nullptr;
-    size_t off_AB = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
+    size_t off_AB = 0, off_ABt = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
     bool cl_ready = false;
@@ -269,6 +269,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
     p.inv_m = (T)h->inv_m;
     const char *m = (const char *)h->d_model;
     p.AB = (const T *)(m + h->off_AB);
+    p.ABt = (const T *)(m + h->off_ABt);
     p.c = (const T *)(m + h->off_c);
     p.H = (const T *)(m + h->off_H);
     p.He = (const T *)(m + h->off_He);
@@ -570,6 +571,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         return o;
     };
     h->off_AB = carve((size_t)nx * nz);
+    h->off_ABt = carve((size_t)nx * nz);
     h->off_c = carve(nx);
     h->off_H = carve((size_t)nz * nz);
     h->off_He = carve((size_t)nx * nx);
@@ -578,9 +580,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
     const size_t model_bytes = off;
-    const size_t per_wg = (size_t)h->ipw * h->wpb;
-    const size_t nslots = ((size_t)batch + per_wg - 1) / per_wg * per_wg;   // tail wavefronts included
-    const size_t scratch_bytes = nslots * nmpc::scratch_elems_per_instance(N, nx, nu) * es;
+    const size_t scratch_bytes = (precision == NMPC_FP64 ? nmpc::ipm_scratch_elems<double>(h->kidx, batch, N)
+                                                         : nmpc::ipm_scratch_elems<float>(h->kidx, batch, N)) * es;
     bool ok = hipMalloc(&h->d_model, model_bytes) == hipSuccess &&
               hipMalloc(&h->d_x0, (size_t)batch * nx * es) == hipSuccess &&
               hipMalloc(&h->d_yref, (size_t)batch * h->ystride() * es) == hipSuccess &&
@@ -601,6 +602,9 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         for (int q = 0; q < nx; q++) AB[r * nz + q] = h->A[r * nx + q];
         for (int q = 0; q < nu; q++) AB[r * nz + nx + q] = h->B[r * nu + q];
     }
+    std::vector<double> ABt((size_t)nx * nz);
+    for (int r = 0; r < nx; r++)
+        for (int q = 0; q < nz; q++) ABt[q * nx + r] = AB[r * nz + q];
     char *dm = (char *)h->d_model;
     auto put = [&](size_t o, const std::vector<double> &v) {
         if (f64) {
@@ -611,6 +615,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         }
     };
     put(h->off_AB, AB);
+    put(h->off_ABt, ABt);
     put(h->off_c, h->c);
     put(h->off_H, h->H);
     put(h->off_He, h->He);

@@ -17,6 +17,7 @@ struct IpmParams {
     int max_iter;
     T tol_comp, tol_res, mu0, inv_m;
     const T *AB;    // [nx][nx+nu]   discrete [A B], row-major
+    const T *ABt;   // [nx+nu][nx]   its transpose
     const T *c;     // [nx]
     const T *H;     // [nz][nz]      stage Hessian (cost-scaled), z = [x; u]
     const T *He;    // [nx][nx]
@@ -43,6 +44,9 @@ template <typename T>
 int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_out);
 template <typename T>
 hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s);
+// scratch elements (of T) the kernel `idx` needs for a batch of B instances, horizon N
+template <typename T>
+size_t ipm_scratch_elems(int idx, int B, int N);
 
 // closed-loop step kernels (nmpc_closed_loop.hip)
 template <typename T>

@@ -42,6 +42,7 @@
 #include <cstdlib>
 
 #include "nmpc_internal.h"
+#include "nmpc_lpc_geom.h"
 
 // unroll factor of the row-round loops of the backward factorisation (M, F, P products)
 #ifndef NMPC_UNROLL_A
@@ -938,17 +939,34 @@ static hipError_t launch_ipm(const IpmParams<T> &p, hipStream_t s)
 
 template <typename T>
 struct IpmEntry {
+    int kind;   // 0: one wavefront per IPW-instance lane block (ipm_kernel), 1: lane per component (ipm_lpc_kernel)
     int nx, nu, ipw, wpb, mw;
     hipError_t (*fn)(const IpmParams<T> &, hipStream_t);
     int lds_bytes;
+    size_t (*scratch)(int B, int N);
 };
+
+template <typename T, int NX, int NU, int IPW, int WPB>
+static size_t wave_scratch_elems(int B, int N)
+{
+    const size_t per_wg = (size_t)IPW * WPB;
+    return ((size_t)B + per_wg - 1) / per_wg * per_wg * ScratchLayout(N, NX, NU).total;
+}
 
 // MW: minimum wavefronts per SIMD requested from the register allocator (__launch_bounds__)
 template <typename T, int NX, int NU, int IPW, int WPB, int MW = 1>
 static constexpr IpmEntry<T> entry()
 {
-    return IpmEntry<T>{NX, NU, IPW, WPB, MW, &launch_ipm<T, NX, NU, IPW, WPB, MW>,
-                       (int)(sizeof(T) * Geometry<T, NX, NU, IPW, WPB>::LDS_ELEMS)};
+    return IpmEntry<T>{0, NX, NU, IPW, WPB, MW, &launch_ipm<T, NX, NU, IPW, WPB, MW>,
+                       (int)(sizeof(T) * Geometry<T, NX, NU, IPW, WPB>::LDS_ELEMS),
+                       &wave_scratch_elems<T, NX, NU, IPW, WPB>};
+}
+
+template <typename T, int NX, int NU, int WPB, int MW>
+static constexpr IpmEntry<T> entry_lpc()
+{
+    return IpmEntry<T>{1, NX, NU, lpc::Geom<T, NX, NU, WPB>::IPW, WPB, MW, &launch_ipm_lpc<T, NX, NU, WPB, MW>,
+                       (int)(sizeof(T) * lpc::Geom<T, NX, NU, WPB>::LDS_ELEMS), &lpc::scratch_elems<T, NX, NU, WPB>};
 }
 
 template <typename T>
@@ -961,9 +979,21 @@ static const IpmEntry<T> *table(int *n)
         // selectable with NMPC_VARIANT for tuning runs
         entry<T, 13, 4, 1, 1, 3>(), entry<T, 13, 4, 1, 4>(), entry<T, 13, 4, 1, 1, 2>(),
         entry<T, 13, 4, 1, 4, 3>(), entry<T, 13, 4, 1, 2, 4>(),
+        // lane-per-component kernels (NMPC_KERNEL=lpc)
+        entry_lpc<T, 13, 4, 4, 3>(), entry_lpc<T, 13, 4, 1, 3>(), entry_lpc<T, 13, 4, 2, 2>(),
+        entry_lpc<T, 4, 2, 4, 2>(), entry_lpc<T, 6, 2, 4, 2>(),
     };
     *n = (int)(sizeof(t) / sizeof(t[0]));
     return t;
+}
+
+// kernel family: NMPC_KERNEL=lpc selects the lane-per-component kernels, =wave the
+// wavefront-per-instance ones; default = wave
+static int kernel_kind()
+{
+    const char *k = getenv("NMPC_KERNEL");
+    if (k && (k[0] == 'l' || k[0] == 'L')) return 1;
+    return 0;
 }
 
 template <typename T>
@@ -971,13 +1001,14 @@ int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_o
 {
     int n;
     const IpmEntry<T> *t = table<T>(&n);
+    const int kind = kernel_kind();
     int best = -1;
-    // NMPC_VARIANT=k picks the k-th compiled kernel of this (nx, nu) (tuning runs)
+    // NMPC_VARIANT=k picks the k-th compiled kernel of this (nx, nu) and family (tuning runs)
     const char *var = getenv("NMPC_VARIANT");
     if (var) {
         int want = atoi(var), seen = 0;
         for (int i = 0; i < n; i++) {
-            if (t[i].nx != nx || t[i].nu != nu) continue;
+            if (t[i].nx != nx || t[i].nu != nu || t[i].kind != kind) continue;
             if (seen++ == want) {
                 *ipw_out = t[i].ipw;
                 *lds_out = t[i].lds_bytes;
@@ -987,8 +1018,10 @@ int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_o
         }
     }
     for (int i = 0; i < n; i++) {
-        if (t[i].nx != nx || t[i].nu != nu) continue;
-        if (ipw_req > 0) {
+        if (t[i].nx != nx || t[i].nu != nu || t[i].kind != kind) continue;
+        if (kind == 1) {   // lane-per-component: instances per wave fixed by nx + nu, first listed
+            if (best < 0) best = i;
+        } else if (ipw_req > 0) {
             if (t[i].ipw == ipw_req && best < 0) best = i;   // first listed = preferred variant
         } else if (best < 0 || t[i].ipw > t[best].ipw) {
             best = i;
@@ -1009,6 +1042,16 @@ hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s)
     return t[idx].fn(p, s);
 }
 
+template <typename T>
+size_t ipm_scratch_elems(int idx, int B, int N)
+{
+    int n;
+    const IpmEntry<T> *t = table<T>(&n);
+    return t[idx].scratch(B, N);
+}
+
+template size_t ipm_scratch_elems<double>(int, int, int);
+template size_t ipm_scratch_elems<float>(int, int, int);
 template int ipm_find<double>(int, int, int, int *, int *, int *);
 template int ipm_find<float>(int, int, int, int *, int *, int *);
 template hipError_t ipm_launch<double>(int, const IpmParams<double> &, hipStream_t);

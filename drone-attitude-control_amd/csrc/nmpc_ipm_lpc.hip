@@ -1,0 +1,816 @@
+// nmpc_ipm_lpc.hip — batched box-constrained LQ-OCP solver, lane-per-component layout (gfx950).
+//
+// Same problem and algorithm as nmpc_ipm.hip and oracle/c/riccati_ipm.c (one
+// `AcadosOcpSolver.solve()` of src/force_model/controller.py:32 / src/jerk_model/controller.py:33:
+// SQP-GN on an LTI / LINEAR_LS / box-constrained OCP == one QP, solved by a Mehrotra
+// predictor-corrector interior-point method with a backward Riccati recursion per Newton
+// system), mapped differently onto the CDNA4 wavefront:
+//
+//   * a lane group of NZ = nx + nu lanes owns one instance, IPW = 64 / NZ instances per
+//     wavefront (quad13: 3 x 17 lanes); lane r owns component r of every stage z_k = [x_k; u_k]
+//     (x-lanes r < nx, u-lanes r >= nx). All per-element iterates (z, lambda, steps) and every
+//     per-stage record a lane reads back later were written by that same lane, so the HBM
+//     scratch needs no cross-lane hand-off and no fences;
+//   * the stage recursions keep their state in registers: x-lane i holds row i of P_{k+1}; the
+//     stage products use the model matrix [A B] as a wave-uniform SGPR operand (constant
+//     address space, s_load_dwordx16 streams), so the 13x17 products M = P [A B] (row i per
+//     x-lane) and F = [A B]' M + H (column r per lane) are v_fma_f64 chains with 17
+//     independent accumulators and no LDS operand traffic; M crosses lanes once through LDS
+//     (transposed), F_uu / h_u / L^{-1} F_ux cross once each;
+//   * the elementwise work of the IPM is fused into the four stage sweeps of an iteration:
+//       A  backward Riccati factorisation; applies the previous step lazily, forms Sigma,
+//          g = H z + G yref and the dynamics residual re of stage k on the fly;
+//       B  forward predictor; ratio test and centring sums on the fly;
+//       C  backward corrector vector; corrector right-hand side on the fly;
+//       D  forward corrector; step length and the new complementarity measure (closed form
+//          in alpha) on the fly;
+//   * group reductions (min/sum over the NZ lanes of an instance) run on ds_bpermute.
+//
+// The diagonal barrier term Sigma of P (x part) is carried separately from the row of P
+// (sdiag), so no lane ever indexes its registers with its own lane number.
+
+#include <hip/hip_runtime.h>
+
+#include "nmpc_internal.h"
+#include "nmpc_lpc_geom.h"
+
+namespace nmpc {
+namespace lpc {
+
+#define LPC_SYNC()                                               \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+        asm volatile("" ::: "memory");                           \
+    } while (0)
+
+template <typename T>
+using cptr = const T __attribute__((address_space(4))) *;
+
+__device__ __forceinline__ double frsq(double x)
+{
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = fma(y, fma(-h, y * y, 0.5), y);
+    y = fma(y, fma(-h, y * y, 0.5), y);
+    return y;
+}
+__device__ __forceinline__ float frsq(float x)
+{
+    float y = __builtin_amdgcn_rsqf(x);
+    return fmaf(y, fmaf(-0.5f * x, y * y, 0.5f), y);
+}
+__device__ __forceinline__ double frcp(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return r;
+}
+__device__ __forceinline__ float frcp(float x)
+{
+    float r = __builtin_amdgcn_rcpf(x);
+    return fmaf(fmaf(-x, r, 1.0f), r, r);
+}
+
+__host__ __device__ constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
+// x <- F_uu^{-1} x with the packed Cholesky factor (inverse diagonal)
+template <typename T, int NU>
+__device__ __forceinline__ void chol_solve(const T (&lf)[NU * (NU + 1) / 2], T (&x)[NU])
+{
+#pragma unroll
+    for (int i = 0; i < NU; i++) {
+        T s = x[i];
+#pragma unroll
+        for (int l = 0; l < i; l++) s = fma(-lf[tri(i, l)], x[l], s);
+        x[i] = s * lf[tri(i, i)];
+    }
+#pragma unroll
+    for (int i = NU - 1; i >= 0; i--) {
+        T s = x[i];
+#pragma unroll
+        for (int l = i + 1; l < NU; l++) s = fma(-lf[tri(l, i)], x[l], s);
+        x[i] = s * lf[tri(i, i)];
+    }
+}
+
+// reductions over the NZ lanes of each lane group (tree on ds_bpermute, result broadcast)
+template <int NZ, typename T, typename Op>
+__device__ __forceinline__ T gred(T v, int lane, int r, Op op)
+{
+#pragma unroll
+    for (int s = 1; s < NZ; s <<= 1) {
+        const T o = __shfl(v, lane + s < 64 ? lane + s : 63, 64);
+        if (r + s < NZ) v = op(v, o);
+    }
+    return __shfl(v, lane - r, 64);
+}
+
+// Stream the rows of a wave-uniform NR x NC matrix (constant address space) through SGPRs,
+// one row ahead of its use: body(l, row) consumes row l while row l+1 is in flight. The
+// scheduling barriers keep the compiler from hoisting every row's s_load at once (which
+// would exhaust the SGPR file and spill to VGPR lanes).
+template <int NR, int NC, typename T, typename Body>
+__device__ __forceinline__ void sgpr_rows(cptr<T> m, Body body)
+{
+    T cur[NC], nxt[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) cur[c] = m[c];
+#pragma unroll
+    for (int l = 0; l < NR; l++) {
+        if (l + 1 < NR) {
+#pragma unroll
+            for (int c = 0; c < NC; c++) nxt[c] = m[(l + 1) * NC + c];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        body(l, cur);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < NC; c++) cur[c] = nxt[c];
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ bool has_bound(T b)
+{
+    return fabs(b) < T(1e20);
+}
+
+template <typename T>
+struct Buf {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ T ld(unsigned uni, unsigned lane) const
+    {
+        if constexpr (sizeof(T) == 8)
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8u, uni * 8u, 0));
+        else
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, lane * 4u, uni * 4u, 0));
+    }
+    __device__ void st(unsigned uni, unsigned lane, T v) const
+    {
+        if constexpr (sizeof(T) == 8)
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r, lane * 8u, uni * 8u, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, lane * 4u, uni * 4u, 0);
+    }
+};
+
+template <typename T, int NX, int NU, int WPB, int MW>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8))) void ipm_lpc_kernel(IpmParams<T> p)
+{
+    using Gm = Geom<T, NX, NU, WPB>;
+    constexpr int NZ = Gm::NZ, IPW = Gm::IPW, VS = Gm::VS, LDZ = Gm::LDZ, LDX = Gm::LDX, LDU = Gm::LDU;
+    constexpr int NUT = NU * (NU + 1) / 2;
+    constexpr int XW = Gm::XW, XPR = Gm::XPR, XRE = Gm::XRE, UW = Gm::UW, UKFF = Gm::UKFF, UFI = Gm::UFI;
+
+    __shared__ __attribute__((aligned(16))) T lds[Gm::LDS_ELEMS];
+    T *abr = lds + Gm::C_ABR, *abt = lds + Gm::C_ABT, *hm = lds + Gm::C_H, *hem = lds + Gm::C_HE;
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int grp = lane / NZ, r = lane - grp * NZ;
+    const bool xl = r < NX, ul = !xl;
+    const int u = ul ? r - NX : 0;
+    const int N = p.N;
+    const unsigned wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const size_t wg = (size_t)blockIdx.x * WPB + wave_u;
+    const long long inst_raw = (long long)wg * IPW + grp;
+    const bool inst_ok = grp < IPW && inst_raw < p.B;
+    const int inst = inst_ok ? (int)inst_raw : 0;   // idle lanes read instance 0, never write outputs
+
+    // ---- model constants -> LDS (once per workgroup)
+    for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) {
+        const T v = p.AB[e];
+        abr[(e / NZ) * LDZ + e % NZ] = v;
+        abt[(e % NZ) * LDX + e / NZ] = v;
+    }
+    for (int e = threadIdx.x; e < NZ * NZ; e += 64 * WPB) hm[(e / NZ) * LDZ + e % NZ] = p.H[e];
+    for (int e = threadIdx.x; e < NX * NX; e += 64 * WPB) hem[(e / NX) * LDX + e % NX] = p.He[e];
+    for (int e = threadIdx.x; e < 3 * NZ; e += 64 * WPB) {
+        lds[Gm::C_LB + (e / NZ) * LDZ + e % NZ] = p.lbnd[e];
+        lds[Gm::C_UB + (e / NZ) * LDZ + e % NZ] = p.ubnd[e];
+    }
+    __syncthreads();
+    if (!__any(inst_ok)) return;
+
+    T *gb = lds + Gm::C_TOT + (wave * VS + grp) * Gm::G_TOT;
+    T *zb = gb + Gm::G_ZB, *rb = gb + Gm::G_RB, *vb = gb + Gm::G_VB, *hub = gb + Gm::G_HU, *fu = gb + Gm::G_FU;
+    T *mt = gb + Gm::G_MT, *ylds = gb + Gm::G_MT;
+
+    // per-lane constants: bounds of component r for stage types (0: k = 0, 1: 0 < k < N, 2: k = N)
+    const T c_r = xl ? p.c[r] : T(0);
+    const T *clb = lds + Gm::C_LB + r, *cub = lds + Gm::C_UB + r;
+    auto LB = [&](int k) { return clb[(k == 0 ? 0 : (k == N ? 2 : 1)) * LDZ]; };
+    auto UB = [&](int k) { return cub[(k == 0 ? 0 : (k == N ? 2 : 1)) * LDZ]; };
+
+    // ---- scratch: VS instance slots per wavefront, lane-owned elements
+    using L = Layout<NX, NU>;
+    const unsigned slot = (unsigned)L::slot(N);
+    Buf<T> S;
+    S.r = __builtin_amdgcn_make_buffer_rsrc(p.scratch + wg * VS * slot, 0, (int)(VS * slot * sizeof(T)), 0x00020000);
+    const unsigned lo_e = (unsigned)grp * slot + (unsigned)r;        // element (k, r) / x record of lane r
+    const unsigned lo_u = (unsigned)grp * slot + (unsigned)u;        // u record of lane r = nx + u
+    auto ldE = [&](int arr, int k) { return S.ld((unsigned)k * L::BLK, lo_e + arr); };
+    auto stE = [&](int arr, int k, T v) { S.st((unsigned)k * L::BLK, lo_e + arr, v); };
+    auto ldX = [&](int k, int w) { return S.ld((unsigned)k * L::BLK, lo_e + L::XREC + w * NX); };
+    auto stX = [&](int k, int w, T v) { S.st((unsigned)k * L::BLK, lo_e + L::XREC + w * NX, v); };
+    auto ldU = [&](int k, int w) { return S.ld((unsigned)k * L::BLK, lo_u + L::UREC + w * NU); };
+    auto stU = [&](int k, int w, T v) { S.st((unsigned)k * L::BLK, lo_u + L::UREC + w * NU, v); };
+
+    const T *yref = p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
+    const T *x0 = p.x0 + (size_t)inst * NX;
+    auto gmin = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return fmin(a, b); }); };
+    auto gmax = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return fmax(a, b); }); };
+    auto gsum = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return a + b; }); };
+
+    // ------------------------------------------------------------------ initial point
+    T r0 = 0, mu = 0, abz = 0;
+    for (int k = 0; k <= N; k++) {
+        const bool ex = k < N || xl;
+        const T *yk = yref + (size_t)k * p.ny;
+        T z = 0, lam_l = 0, lam_u = 0, gc = 0;
+        const T lb = LB(k), ub = UB(k);
+        if (ex) {
+            if (k < N) {
+                for (int j = 0; j < p.ny; j++) gc += p.G[r * p.ny + j] * yk[j];
+            } else {
+                for (int j = 0; j < p.ny_e; j++) gc += p.Ge[r * p.ny_e + j] * yk[j];
+            }
+            if (k == 0 && xl) {
+                z = x0[r];
+            } else {
+                z = p.yref_is_z ? yk[r] : T(0);
+                const bool hl = has_bound(lb), hu = has_bound(ub);
+                if (hl && hu) {
+                    const T d = T(0.01) * (ub - lb);
+                    z = fmin(fmax(z, lb + d), ub - d);
+                } else if (hl) {
+                    z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
+                } else if (hu) {
+                    z = fmin(z, ub - T(0.01) * fmax(fabs(ub), T(1)));
+                }
+                if (hl) lam_l = p.mu0 / (z - lb);
+                if (hu) lam_u = p.mu0 / (ub - z);
+            }
+        }
+        stE(L::Z, k, z);
+        stE(L::LL, k, lam_l);
+        stE(L::LU, k, lam_u);
+        stE(L::GC, k, gc);
+        zb[r] = z;
+        LPC_SYNC();
+        if (ex) {
+            T g = gc;
+            if (k < N) {
+#pragma unroll
+                for (int b = 0; b < NZ; b++) g = fma(hm[r * LDZ + b], zb[b], g);
+            } else {
+#pragma unroll
+                for (int b = 0; b < NX; b++) g = fma(hem[r * LDX + b], zb[b], g);
+            }
+            if (!(k == 0 && xl)) {
+                r0 = fmax(r0, fabs(g - lam_l + lam_u));
+                if (lam_l > T(0)) mu += lam_l * (z - lb);
+                if (lam_u > T(0)) mu += lam_u * (ub - z);
+            }
+            if (xl && k > 0) r0 = fmax(r0, fabs(abz - z));
+            if (xl && k < N) {
+                T s = c_r;
+#pragma unroll
+                for (int j = 0; j < NZ; j++) s = fma(abr[r * LDZ + j], zb[j], s);
+                abz = s;
+            }
+        }
+        LPC_SYNC();
+    }
+    r0 = gmax(r0);
+    mu = gsum(mu) * p.inv_m;
+
+    const T m_bounds = T(1) / p.inv_m;
+    T theta = 1;
+    bool active = inst_ok;
+    int status = 2, iters = 0;
+    bool fail = false, pending = false;
+    T alpha = 0, smu = 0;
+
+    // elementwise state of element (k, r) fetched one stage ahead in the sweeps
+    struct El {
+        T z, ll, lu, dz, dza, g;
+    };
+    // lazily apply the pending step of the previous iteration to element (k, r)
+    auto lazy = [&](int k, El &q) {
+        if (pending && (k < N || xl)) {
+            const T lb = LB(k), ub = UB(k);
+            if (q.ll > T(0)) {
+                const T t = q.z - lb, it_ = frcp(t), dla = -q.ll * (T(1) + q.dza * it_);
+                q.ll += alpha * ((smu - q.ll * t - dla * q.dza - q.ll * q.dz) * it_);
+            }
+            if (q.lu > T(0)) {
+                const T t = ub - q.z, it_ = frcp(t), dla = -q.lu * (T(1) - q.dza * it_);
+                q.lu += alpha * ((smu - q.lu * t + dla * q.dza + q.lu * q.dz) * it_);
+            }
+            q.z += alpha * q.dz;
+            stE(L::Z, k, q.z);
+            stE(L::LL, k, q.ll);
+            stE(L::LU, k, q.lu);
+        }
+    };
+    auto sigma = [&](int k, const El &q) {
+        T sg = 0;
+        if (q.ll > T(0)) sg += q.ll * frcp(q.z - LB(k));
+        if (q.lu > T(0)) sg += q.lu * frcp(UB(k) - q.z);
+        return sg;
+    };
+
+    // ---- forward recursion (B: predictor into dza with ratio test / centring sums;
+    //      D: corrector into dz with step length / new-mu sums):
+    //      dx_0 = 0, du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx_k; du_k] + re_k
+    auto forward = [&](bool corr, T &s_min, T &s_a, T &s_b, T &s_c) {
+        const T *arow = abr + (xl ? r : 0) * LDZ;   // row r of [A B] (LDS, read per stage)
+        s_min = 1;
+        s_a = s_b = s_c = 0;
+        auto stats = [&](int k, T dz, const El &q) {
+            const T lb = LB(k), ub = UB(k);
+            if (!corr) {
+                if (q.ll > T(0)) {
+                    const T t = q.z - lb, it_ = frcp(t);
+                    const T dl = -q.ll * (T(1) + dz * it_);
+                    if (dz < T(0)) s_min = fmin(s_min, -t * frcp(dz));
+                    if (dl < T(0)) s_min = fmin(s_min, -q.ll * frcp(dl));
+                    s_a += q.ll * t;
+                    s_b += q.ll * dz * (t + dz) * it_;
+                }
+                if (q.lu > T(0)) {
+                    const T t = ub - q.z, it_ = frcp(t);
+                    const T dl = -q.lu * (T(1) - dz * it_);
+                    if (dz > T(0)) s_min = fmin(s_min, t * frcp(dz));
+                    if (dl < T(0)) s_min = fmin(s_min, -q.lu * frcp(dl));
+                    s_a += q.lu * t;
+                    s_b += q.lu * dz * (dz - t) * it_;
+                }
+            } else {
+                const T dza = q.dza;
+                if (q.ll > T(0)) {
+                    const T t = q.z - lb, it_ = frcp(t);
+                    const T dla = -q.ll * (T(1) + dza * it_);
+                    const T dl = (smu - q.ll * t - dla * dza - q.ll * dz) * it_;
+                    if (dz < T(0)) s_min = fmin(s_min, -t * frcp(dz));
+                    if (dl < T(0)) s_min = fmin(s_min, -q.ll * frcp(dl));
+                    s_a += q.ll * t;
+                    s_b += dla * dza;
+                    s_c += dl * dz;
+                }
+                if (q.lu > T(0)) {
+                    const T t = ub - q.z, it_ = frcp(t);
+                    const T dla = -q.lu * (T(1) - dza * it_);
+                    const T dl = (smu - q.lu * t + dla * dza + q.lu * dz) * it_;
+                    if (dz > T(0)) s_min = fmin(s_min, t * frcp(dz));
+                    if (dl < T(0)) s_min = fmin(s_min, -q.lu * frcp(dl));
+                    s_a += q.lu * t;
+                    s_b -= dla * dza;
+                    s_c -= dl * dz;
+                }
+            }
+        };
+        struct Rec {
+            El e;
+            T c0, kq[NU];   // x-lane: re_k(r), K_k(:, r); u-lane: kff_k(u)
+        };
+        auto fetch = [&](int k, Rec &q) {
+            const int kk = k < N ? k : N - 1;
+            q.e.z = ldE(L::Z, k);
+            q.e.ll = ldE(L::LL, k);
+            q.e.lu = ldE(L::LU, k);
+            if (corr) q.e.dza = ldE(L::DZA, k);
+            if (xl) {
+                q.c0 = ldX(kk, XRE);
+#pragma unroll
+                for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
+            } else {
+                q.c0 = ldU(kk, UKFF);
+            }
+        };
+        const int dst = corr ? L::DZ : L::DZA;
+        T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
+        T dx = 0;
+        Rec q, qn;
+        fetch(0, qn);
+        for (int k = 0; k < N; k++) {
+            q = qn;
+            fetch(k + 1, qn);
+            if (xl) {
+#pragma unroll
+                for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
+                zb[r] = dx;
+            }
+            LPC_SYNC();
+            T du = 0;
+            if (ul) {
+                T s0 = q.c0, s1 = 0;
+#pragma unroll
+                for (int j = 0; j + 1 < NX; j += 2) {
+                    s0 += part[j * LDU + u];
+                    s1 += part[(j + 1) * LDU + u];
+                }
+                if (NX % 2) s0 += part[(NX - 1) * LDU + u];
+                du = s0 + s1;
+                zb[r] = du;
+            }
+            LPC_SYNC();
+            const T my = xl ? dx : du;
+            if (xl) {
+                T s0 = q.c0, s1 = 0;
+#pragma unroll
+                for (int j = 0; j + 1 < NZ; j += 2) {
+                    s0 = fma(arow[j], zb[j], s0);
+                    s1 = fma(arow[j + 1], zb[j + 1], s1);
+                }
+                if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
+                dx = s0 + s1;
+            }
+            stE(dst, k, my);
+            stats(k, my, q.e);
+            LPC_SYNC();
+        }
+        if (xl) {
+            stE(dst, N, dx);
+            stats(N, dx, qn.e);
+        }
+        s_min = gmin(s_min);
+        s_a = gsum(s_a);
+        s_b = gsum(s_b);
+        s_c = gsum(s_c);
+    };
+
+    cptr<T> abs_ = (cptr<T>)p.AB;   // [NX][NZ] row-major, wave-uniform SGPR operand
+
+    for (int it = 0;; it++) {
+        const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
+        const bool bad = !isfinite(mu) || !isfinite(theta) || fail;
+        if (active && (conv || bad)) {
+            active = false;
+            status = conv && !bad ? 0 : 4;
+            iters = it;
+        }
+        if (active && it >= p.max_iter) {
+            active = false;
+            status = 2;
+            iters = it;
+        }
+        if (!__any(active)) break;
+
+        // ============================ A: backward Riccati factorisation (+ lazy step, Sigma, g, re)
+        {
+            T prow[NX], sdiag, pv;
+            T znext;
+            El q, qn;
+            auto fetchA = [&](int k, El &e) {
+                e.z = ldE(L::Z, k);
+                e.ll = ldE(L::LL, k);
+                e.lu = ldE(L::LU, k);
+                e.g = ldE(L::GC, k);
+                if (pending) {
+                    e.dz = ldE(L::DZ, k);
+                    e.dza = ldE(L::DZA, k);
+                }
+            };
+            // terminal stage: P_N = He + Sigma_N, p_N = g_N
+            fetchA(N, q);
+            fetchA(N - 1, qn);
+            lazy(N, q);
+            {
+                const T sg = xl ? sigma(N, q) : T(0);
+                zb[r] = xl ? q.z : T(0);
+                LPC_SYNC();
+                T g = q.g;
+#pragma unroll
+                for (int b = 0; b < NX; b++) g = fma(hem[(xl ? r : 0) * LDX + b], zb[b], g);
+                if (xl) stE(L::GF, N, g);
+#pragma unroll
+                for (int i = 0; i < NX; i++) prow[i] = hem[(xl ? r : 0) * LDX + i];
+                sdiag = sg;
+                pv = g;
+                znext = q.z;
+                LPC_SYNC();
+            }
+            for (int k = N - 1; k >= 0; k--) {
+                q = qn;
+                if (k > 0) fetchA(k - 1, qn);
+                lazy(k, q);
+                const T sg = sigma(k, q);
+                zb[r] = q.z;
+                LPC_SYNC();
+                // g = H z + G yref, re = [A B] z_k + c - x_{k+1}
+                T g = q.g, re = 0;
+                {
+                    T g1 = 0;
+#pragma unroll
+                    for (int b = 0; b + 1 < NZ; b += 2) {
+                        g = fma(hm[r * LDZ + b], zb[b], g);
+                        g1 = fma(hm[r * LDZ + b + 1], zb[b + 1], g1);
+                    }
+                    if (NZ % 2) g = fma(hm[r * LDZ + NZ - 1], zb[NZ - 1], g);
+                    g += g1;
+                }
+                stE(L::GF, k, g);
+                if (xl) {
+                    T s0 = c_r - znext, s1 = 0;
+#pragma unroll
+                    for (int j = 0; j + 1 < NZ; j += 2) {
+                        s0 = fma(abr[r * LDZ + j], zb[j], s0);
+                        s1 = fma(abr[r * LDZ + j + 1], zb[j + 1], s1);
+                    }
+                    if (NZ % 2) s0 = fma(abr[r * LDZ + NZ - 1], zb[NZ - 1], s0);
+                    re = s0 + s1;
+                    rb[r] = re;
+                    stX(k, XRE, re);
+                }
+                znext = q.z;
+                LPC_SYNC();
+                // M = P [A B] (row r per x-lane; [A B] from SGPRs), Pr = P re, v = Pr + p
+                cptr<T> ab = abs_;
+                asm volatile("" : "+s"(ab));
+                if (xl) {
+                    T pr0 = sdiag * re, pr1 = 0;
+#pragma unroll
+                    for (int l = 0; l + 1 < NX; l += 2) {
+                        pr0 = fma(prow[l], rb[l], pr0);
+                        pr1 = fma(prow[l + 1], rb[l + 1], pr1);
+                    }
+                    if (NX % 2) pr0 = fma(prow[NX - 1], rb[NX - 1], pr0);
+                    const T pr = pr0 + pr1;
+                    stX(k, XPR, pr);
+                    vb[r] = pr + pv;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (xl) {
+                    T mrow[NZ];
+#pragma unroll
+                    for (int c = 0; c < NZ; c++) mrow[c] = sdiag * abr[r * LDZ + c];
+                    sgpr_rows<NX, NZ, T>(ab, [&](int l, const T (&row)[NZ]) {
+#pragma unroll
+                        for (int c = 0; c < NZ; c++) mrow[c] = fma(prow[l], row[c], mrow[c]);
+                    });
+#pragma unroll
+                    for (int c = 0; c < NZ; c++) mt[c * LDX + r] = mrow[c];
+                }
+                LPC_SYNC();
+                // F = [A B]' M + H (column r per lane; + Sigma on the diagonal, applied by the
+                // readers), h = [A B]' v + g
+                T fcol[NZ], h;
+                {
+                    T h0 = g, h1 = 0;
+#pragma unroll
+                    for (int i = 0; i + 1 < NX; i += 2) {
+                        h0 = fma(abt[r * LDX + i], vb[i], h0);
+                        h1 = fma(abt[r * LDX + i + 1], vb[i + 1], h1);
+                    }
+                    if (NX % 2) h0 = fma(abt[r * LDX + NX - 1], vb[NX - 1], h0);
+                    h = h0 + h1;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                {
+                    T mc[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; i++) mc[i] = mt[r * LDX + i];
+#pragma unroll
+                    for (int a = 0; a < NZ; a++) fcol[a] = hm[r * LDZ + a];
+                    asm volatile("" : "+s"(ab));
+                    sgpr_rows<NX, NZ, T>(ab, [&](int i, const T (&row)[NZ]) {
+#pragma unroll
+                        for (int a = 0; a < NZ; a++) fcol[a] = fma(row[a], mc[i], fcol[a]);
+                    });
+                    // materialise F here (IR sinking would otherwise defer the x part to the P
+                    // update and keep every streamed row of [A B] alive in SGPRs until then)
+#pragma unroll
+                    for (int a = 0; a < NZ; a++) asm volatile("" : "+v"(fcol[a]));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (ul) {
+                    T fd = fcol[NX];
+#pragma unroll
+                    for (int a = 0; a < NU; a++) {
+                        fu[a * NU + u] = fcol[NX + a];
+                        fd = (u == a) ? fcol[NX + a] : fd;
+                    }
+                    fu[u * NU + u] = fd + sg;
+                    hub[u] = h;
+                }
+                LPC_SYNC();
+                // F_uu = L L' (every lane), kff = -F_uu^{-1} h_u
+                T lf[NUT], hu[NU];
+#pragma unroll
+                for (int i = 0; i < NU; i++) hu[i] = hub[i];
+#pragma unroll
+                for (int i = 0; i < NU; i++)
+#pragma unroll
+                    for (int j = 0; j <= i; j++) {
+                        T s_ = fu[i * NU + j];
+#pragma unroll
+                        for (int l = 0; l < j; l++) s_ = fma(-lf[tri(i, l)], lf[tri(j, l)], s_);
+                        if (i == j) {
+                            const bool pd = s_ > T(0);
+                            fail |= active & !pd;
+                            lf[tri(i, i)] = frsq(pd ? s_ : T(1));
+                        } else {
+                            lf[tri(i, j)] = s_ * lf[tri(j, j)];
+                        }
+                    }
+                T y[NU], pnew = 0;
+#pragma unroll
+                for (int i = 0; i < NU; i++) y[i] = 0;
+                if (xl) {
+                    // Y(:, r) = L^{-1} F_ux(:, r), K(:, r) = -L^{-T} Y(:, r), p_r = h_r + K(:, r)' h_u
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        T s_ = fcol[NX + i];
+#pragma unroll
+                        for (int l = 0; l < i; l++) s_ = fma(-lf[tri(i, l)], y[l], s_);
+                        y[i] = s_ * lf[tri(i, i)];
+                    }
+                    T kc[NU];
+#pragma unroll
+                    for (int i = NU - 1; i >= 0; i--) {
+                        T s_ = y[i];
+#pragma unroll
+                        for (int l = i + 1; l < NU; l++) s_ = fma(lf[tri(l, i)], -kc[l], s_);
+                        kc[i] = -s_ * lf[tri(i, i)];
+                    }
+                    pnew = h;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        pnew = fma(kc[i], hu[i], pnew);
+                        ylds[r * LDU + i] = y[i];
+                        stX(k, i, kc[i]);
+                    }
+                } else {
+                    // row u of F_uu^{-1}, kff_u = -(F_uu^{-1} h_u)_u
+                    T e[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) e[i] = (u == i) ? T(1) : T(0);
+                    chol_solve<T, NU>(lf, e);
+                    T kf = 0;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        kf = fma(-e[i], hu[i], kf);
+                        stU(k, UFI + i, e[i]);
+                    }
+                    stU(k, UKFF, kf);
+                }
+                LPC_SYNC();
+                // P(r, :) = F(r, 0:nx) - Y(:, r)' Y  (+ Sigma_x of stage k on the diagonal); u-lanes
+                // compute a dummy row (keeps the loop-carried registers dead between stages)
+#pragma unroll
+                for (int i = 0; i < NX; i++) {
+                    T s_ = fcol[i];
+#pragma unroll
+                    for (int a = 0; a < NU; a++) s_ = fma(-ylds[i * LDU + a], y[a], s_);
+                    prow[i] = s_;
+                }
+                sdiag = sg;
+                pv = pnew;
+                LPC_SYNC();
+            }
+        }
+
+        pending = false;   // the previous step is applied (converged groups stay frozen from here)
+
+        // ============================ B: forward predictor + ratio test / centring sums
+        T a_aff, S0, S2, dummy;
+        forward(false, a_aff, S0, S2, dummy);
+        // mu_aff = [(1 - a) S0 - a^2 S2'] / m with S2' = sum lam dz (t + dz) / t (closed form)
+        const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
+        const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
+        smu = sgm * sgm * sgm * mu;
+
+        // ============================ C: backward corrector vector
+        {
+            auto ghat = [&](int k, const El &e) {
+                T g = e.g;
+                const T lb = LB(k), ub = UB(k);
+                if (e.ll > T(0)) {
+                    const T t = e.z - lb, it_ = frcp(t), dl = -e.ll * (T(1) + e.dza * it_);
+                    g += (dl * e.dza - smu) * it_;
+                }
+                if (e.lu > T(0)) {
+                    const T t = ub - e.z, it_ = frcp(t), dl = -e.lu * (T(1) - e.dza * it_);
+                    g += (dl * e.dza + smu) * it_;
+                }
+                return g;
+            };
+            struct RecC {
+                El e;
+                T pr, kq[NU];
+            };
+            auto fetchC = [&](int k, RecC &q) {
+                q.e.z = ldE(L::Z, k);
+                q.e.ll = ldE(L::LL, k);
+                q.e.lu = ldE(L::LU, k);
+                q.e.dza = ldE(L::DZA, k);
+                q.e.g = ldE(L::GF, k);
+                const int kk = k < N ? k : N - 1;
+                if (xl) {
+                    q.pr = ldX(kk, XPR);
+#pragma unroll
+                    for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < NU; i++) q.kq[i] = ldU(kk, UFI + i);
+                }
+            };
+            const T *acol = abt + r * LDX;   // column r of [A B] (LDS, read per stage)
+            RecC q, qn;
+            fetchC(N, q);
+            fetchC(N - 1, qn);
+            T pv = ghat(N, q.e);
+            for (int k = N - 1; k >= 0; k--) {
+                q = qn;
+                if (k > 0) fetchC(k - 1, qn);
+                const T gh = ghat(k, q.e);
+                if (xl) vb[r] = q.pr + pv;
+                LPC_SYNC();
+                T h0 = gh, h1 = 0;
+#pragma unroll
+                for (int i = 0; i + 1 < NX; i += 2) {
+                    h0 = fma(acol[i], vb[i], h0);
+                    h1 = fma(acol[i + 1], vb[i + 1], h1);
+                }
+                if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                const T h = h0 + h1;
+                if (ul) hub[u] = h;
+                LPC_SYNC();
+                T hu[NU];
+#pragma unroll
+                for (int i = 0; i < NU; i++) hu[i] = hub[i];
+                if (ul) {
+                    T kf = 0;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) kf = fma(-q.kq[i], hu[i], kf);
+                    stU(k, UKFF, kf);
+                } else {
+                    T s_ = h;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) s_ = fma(q.kq[i], hu[i], s_);
+                    pv = s_;
+                }
+                LPC_SYNC();
+            }
+        }
+
+        // ============================ D: forward corrector + step length / new mu
+        T amax, T0, C1, C2;
+        forward(true, amax, T0, C1, C2);
+        const T a = fmin(T(1), T(0.995) * amax);
+        if (active) {
+            // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
+            mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
+            theta *= (T(1) - a);
+            alpha = a;
+            pending = true;
+        }
+    }
+
+    // ------------------------------------------------------------------ apply pending step, outputs
+    if (!inst_ok) return;
+    T *xo = p.xout + (size_t)inst * (N + 1) * NX;
+    T *uo = p.uout + (size_t)inst * N * NU;
+    for (int k = 0; k <= N; k++) {
+        if (k == N && ul) continue;
+        T z = ldE(L::Z, k);
+        if (pending) z += alpha * ldE(L::DZ, k);
+        if (xl) xo[k * NX + r] = z;
+        else uo[k * NU + u] = z;
+    }
+    if (r == 0) {
+        p.status[inst] = status;
+        p.iters[inst] = iters;
+    }
+}
+
+}  // namespace lpc
+
+// ---------------------------------------------------------------------- launch glue
+template <typename T, int NX, int NU, int WPB, int MW>
+hipError_t launch_ipm_lpc(const IpmParams<T> &p, hipStream_t s)
+{
+    using Gm = lpc::Geom<T, NX, NU, WPB>;
+    const int waves = (p.B + Gm::IPW - 1) / Gm::IPW;
+    const int blocks = (waves + WPB - 1) / WPB;
+    hipLaunchKernelGGL((lpc::ipm_lpc_kernel<T, NX, NU, WPB, MW>), dim3(blocks), dim3(64 * WPB), 0, s, p);
+    return hipGetLastError();
+}
+
+// explicit instantiations (the dispatch table in nmpc_ipm.hip binds them)
+#define NMPC_LPC_INST(NX, NU, WPB, MW)                                                              \
+    template hipError_t launch_ipm_lpc<double, NX, NU, WPB, MW>(const IpmParams<double> &, hipStream_t); \
+    template hipError_t launch_ipm_lpc<float, NX, NU, WPB, MW>(const IpmParams<float> &, hipStream_t);
+NMPC_LPC_INST(13, 4, 4, 3)
+NMPC_LPC_INST(13, 4, 1, 3)
+NMPC_LPC_INST(13, 4, 2, 2)
+NMPC_LPC_INST(4, 2, 4, 2)
+NMPC_LPC_INST(6, 2, 4, 2)
+#undef NMPC_LPC_INST
+
+}  // namespace nmpc
