@@ -176,7 +176,7 @@ def main():
                        "global_batch": B * world, "parallelism": f"instance-sharded x{world}, RCCL stats reduce",
                        "instances_per_wave": cl.solver.launch_info()["instances_per_wave"]},
             "roofline": {"bound": "mfma", "pipe": "fp64 FMA on VALU" if args.precision == "fp64" else "fp32 FMA on VALU",
-                         "kernel": "ipm_kernel", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "kernel": cl.solver.launch_info()["kernel"], "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic,
                          "flops_per_launch": fl_launch, "kernel_ms": kernel_ms,
                          "n_ipm": n_ipm, "gpu_mean_qp_iter": st["mean_qp_iter"]},

@@ -406,9 +406,10 @@ class AcadosOcpSolver:
         return self._check(self.lib.nmpc_set_stream(self._h, ctypes.c_void_p(stream_ptr)), "set_stream")
 
     def launch_info(self):
-        out = (ctypes.c_int * 4)()
-        self._check(self.lib.nmpc_get_launch_info(self._h, out, 4), "launch_info")
-        return {"instances_per_wave": out[0], "workgroups": out[1], "threads": out[2], "lds_bytes": out[3]}
+        out = (ctypes.c_int * 5)()
+        self._check(self.lib.nmpc_get_launch_info(self._h, out, 5), "launch_info")
+        return {"instances_per_wave": out[0], "workgroups": out[1], "threads": out[2], "lds_bytes": out[3],
+                "kernel": "ipm_lpc_kernel" if out[4] == 1 else "ipm_kernel"}
 
     def discrete_model(self):
         A = np.zeros((self.nx, self.nx))

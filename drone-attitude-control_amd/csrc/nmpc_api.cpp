@@ -888,8 +888,9 @@ int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
 {
     if (!h || !out) return NMPC_EINVAL;
     const int waves = (h->batch + h->ipw - 1) / h->ipw;
-    const int v[4] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds};
-    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
+    const int kind = h->precision == NMPC_FP64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
+    const int v[5] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind};
+    for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
     return 0;
 }
 

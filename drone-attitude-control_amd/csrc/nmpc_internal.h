@@ -47,6 +47,9 @@ hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s);
 // scratch elements (of T) the kernel `idx` needs for a batch of B instances, horizon N
 template <typename T>
 size_t ipm_scratch_elems(int idx, int B, int N);
+// kernel family of entry `idx`: 0 wavefront per instance block, 1 lane per component
+template <typename T>
+int ipm_kind(int idx);
 
 // closed-loop step kernels (nmpc_closed_loop.hip)
 template <typename T>

@@ -987,13 +987,13 @@ static const IpmEntry<T> *table(int *n)
     return t;
 }
 
-// kernel family: NMPC_KERNEL=lpc selects the lane-per-component kernels, =wave the
-// wavefront-per-instance ones; default = wave
+// kernel family: lane-per-component (ipm_lpc_kernel) by default wherever one is compiled for
+// (nx, nu); NMPC_KERNEL=wave selects the wavefront-per-instance kernels (ipm_kernel)
 static int kernel_kind()
 {
     const char *k = getenv("NMPC_KERNEL");
-    if (k && (k[0] == 'l' || k[0] == 'L')) return 1;
-    return 0;
+    if (k && (k[0] == 'w' || k[0] == 'W')) return 0;
+    return 1;
 }
 
 template <typename T>
@@ -1017,9 +1017,12 @@ int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_o
             }
         }
     }
+    bool have = false;
+    for (int i = 0; i < n; i++) have |= t[i].nx == nx && t[i].nu == nu && t[i].kind == kind;
+    const int fam = have ? kind : 1 - kind;
     for (int i = 0; i < n; i++) {
-        if (t[i].nx != nx || t[i].nu != nu || t[i].kind != kind) continue;
-        if (kind == 1) {   // lane-per-component: instances per wave fixed by nx + nu, first listed
+        if (t[i].nx != nx || t[i].nu != nu || t[i].kind != fam) continue;
+        if (fam == 1) {   // lane-per-component: instances per wave fixed by nx + nu, first listed
             if (best < 0) best = i;
         } else if (ipw_req > 0) {
             if (t[i].ipw == ipw_req && best < 0) best = i;   // first listed = preferred variant
@@ -1050,6 +1053,16 @@ size_t ipm_scratch_elems(int idx, int B, int N)
     return t[idx].scratch(B, N);
 }
 
+template <typename T>
+int ipm_kind(int idx)
+{
+    int n;
+    const IpmEntry<T> *t = table<T>(&n);
+    return t[idx].kind;
+}
+
+template int ipm_kind<double>(int);
+template int ipm_kind<float>(int);
 template size_t ipm_scratch_elems<double>(int, int, int);
 template size_t ipm_scratch_elems<float>(int, int, int);
 template int ipm_find<double>(int, int, int, int *, int *, int *);

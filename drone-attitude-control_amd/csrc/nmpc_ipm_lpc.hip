@@ -34,6 +34,11 @@
 #include "nmpc_internal.h"
 #include "nmpc_lpc_geom.h"
 
+// stage records in flight ahead of the vector sweeps B, C, D
+#ifndef NMPC_LPC_PF
+#define NMPC_LPC_PF 1
+#endif
+
 namespace nmpc {
 namespace lpc {
 
@@ -138,23 +143,28 @@ __device__ __forceinline__ bool has_bound(T b)
     return fabs(b) < T(1e20);
 }
 
+// Scratch accessor: buffer resource in SGPRs, per-lane 32-bit byte offset (VGPR), stage
+// offset (wave-uniform). readfirstlane pins the stage offset to an SGPR: without it the
+// compiler may keep it in a VGPR and wrap every access in a waterfall loop.
 template <typename T>
 struct Buf {
     __amdgpu_buffer_rsrc_t r;
     __device__ T ld(unsigned uni, unsigned lane) const
     {
+        const unsigned so = __builtin_amdgcn_readfirstlane(uni * (unsigned)sizeof(T));
         if constexpr (sizeof(T) == 8)
-            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8u, uni * 8u, 0));
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8u, so, 0));
         else
-            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, lane * 4u, uni * 4u, 0));
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, lane * 4u, so, 0));
     }
     __device__ void st(unsigned uni, unsigned lane, T v) const
     {
+        const unsigned so = __builtin_amdgcn_readfirstlane(uni * (unsigned)sizeof(T));
         if constexpr (sizeof(T) == 8)
             __builtin_amdgcn_raw_buffer_store_b64(
-                __builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r, lane * 8u, uni * 8u, 0);
+                __builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r, lane * 8u, so, 0);
         else
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, lane * 4u, uni * 4u, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, lane * 4u, so, 0);
     }
 };
 
@@ -164,6 +174,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     using Gm = Geom<T, NX, NU, WPB>;
     constexpr int NZ = Gm::NZ, IPW = Gm::IPW, VS = Gm::VS, LDZ = Gm::LDZ, LDX = Gm::LDX, LDU = Gm::LDU;
     constexpr int NUT = NU * (NU + 1) / 2;
+    constexpr int PD = NMPC_LPC_PF;
     constexpr int XW = Gm::XW, XPR = Gm::XPR, XRE = Gm::XRE, UW = Gm::UW, UKFF = Gm::UKFF, UFI = Gm::UFI;
 
     __shared__ __attribute__((aligned(16))) T lds[Gm::LDS_ELEMS];
@@ -379,6 +390,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             T c0, kq[NU];   // x-lane: re_k(r), K_k(:, r); u-lane: kff_k(u)
         };
         auto fetch = [&](int k, Rec &q) {
+            k = k < N ? k : N;
             const int kk = k < N ? k : N - 1;
             q.e.z = ldE(L::Z, k);
             q.e.ll = ldE(L::LL, k);
@@ -395,48 +407,61 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         const int dst = corr ? L::DZ : L::DZA;
         T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
         T dx = 0;
-        Rec q, qn;
-        fetch(0, qn);
-        for (int k = 0; k < N; k++) {
-            q = qn;
-            fetch(k + 1, qn);
-            if (xl) {
+        // stage records in flight PD stages ahead (ring slot j holds stage k = j mod PD; the
+        // stage loop is unrolled by PD so every slot is a fixed register set)
+        Rec ring[PD];
 #pragma unroll
-                for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
-                zb[r] = dx;
-            }
-            LPC_SYNC();
-            T du = 0;
-            if (ul) {
-                T s0 = q.c0, s1 = 0;
+        for (int j = 0; j < PD; j++) fetch(j, ring[j]);
+        for (int kb = 0; kb < N; kb += PD) {
 #pragma unroll
-                for (int j = 0; j + 1 < NX; j += 2) {
-                    s0 += part[j * LDU + u];
-                    s1 += part[(j + 1) * LDU + u];
+            for (int j = 0; j < PD; j++) {
+                const int k = kb + j;
+                if (k >= N) break;
+                const Rec q = ring[j];
+                fetch(k + PD, ring[j]);
+                if (xl) {
+#pragma unroll
+                    for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
+                    zb[r] = dx;
                 }
-                if (NX % 2) s0 += part[(NX - 1) * LDU + u];
-                du = s0 + s1;
-                zb[r] = du;
-            }
-            LPC_SYNC();
-            const T my = xl ? dx : du;
-            if (xl) {
-                T s0 = q.c0, s1 = 0;
+                LPC_SYNC();
+                T du = 0;
+                if (ul) {
+                    T s0 = q.c0, s1 = 0;
 #pragma unroll
-                for (int j = 0; j + 1 < NZ; j += 2) {
-                    s0 = fma(arow[j], zb[j], s0);
-                    s1 = fma(arow[j + 1], zb[j + 1], s1);
+                    for (int jj = 0; jj + 1 < NX; jj += 2) {
+                        s0 += part[jj * LDU + u];
+                        s1 += part[(jj + 1) * LDU + u];
+                    }
+                    if (NX % 2) s0 += part[(NX - 1) * LDU + u];
+                    du = s0 + s1;
+                    zb[r] = du;
                 }
-                if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
-                dx = s0 + s1;
+                LPC_SYNC();
+                const T my = xl ? dx : du;
+                if (xl) {
+                    T s0 = q.c0, s1 = 0;
+#pragma unroll
+                    for (int jj = 0; jj + 1 < NZ; jj += 2) {
+                        s0 = fma(arow[jj], zb[jj], s0);
+                        s1 = fma(arow[jj + 1], zb[jj + 1], s1);
+                    }
+                    if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
+                    dx = s0 + s1;
+                }
+                stE(dst, k, my);
+                stats(k, my, q.e);
+                LPC_SYNC();
             }
-            stE(dst, k, my);
-            stats(k, my, q.e);
-            LPC_SYNC();
         }
         if (xl) {
+            El e;
+            e.z = ldE(L::Z, N);
+            e.ll = ldE(L::LL, N);
+            e.lu = ldE(L::LU, N);
+            if (corr) e.dza = ldE(L::DZA, N);
             stE(dst, N, dx);
-            stats(N, dx, qn.e);
+            stats(N, dx, e);
         }
         s_min = gmin(s_min);
         s_a = gsum(s_a);
@@ -445,6 +470,34 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     };
 
     cptr<T> abs_ = (cptr<T>)p.AB;   // [NX][NZ] row-major, wave-uniform SGPR operand
+
+#if defined(NMPC_PHASE_TIMING) && !defined(NMPC_SWEEP_TIMING)
+#define NMPC_SWEEP_TIMING 1
+#endif
+#ifdef NMPC_SWEEP_TIMING
+    // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per
+    // sweep, reported through the E_A/A/B/../D slots of nmpc_api.cpp (A -> 1, B -> 2, C -> 5, D -> 6)
+    const bool timed = p.cycles != nullptr;
+    unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = timed ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long tstart = tmark;
+    auto tick = [&](int slot) {
+        if (timed) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (slot >= 0) tcy[slot] += t - tmark;
+            tmark = t;
+        }
+    };
+#define LPC_TICK(slot) tick(slot)
+#else
+#define LPC_TICK(slot) ((void)0)
+#endif
+// NMPC_PHASE_TIMING: also split the Riccati stage into pre (lazy step, g, re) -> slot 0,
+// M -> 3, F -> 4, Cholesky / gains / P update -> 7
+#ifdef NMPC_PHASE_TIMING
+#define LPC_PTICK(slot) tick(slot)
+#else
+#define LPC_PTICK(slot) ((void)0)
+#endif
 
     for (int it = 0;; it++) {
         const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
@@ -460,6 +513,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             iters = it;
         }
         if (!__any(active)) break;
+        LPC_TICK(-1);
 
         // ============================ A: backward Riccati factorisation (+ lazy step, Sigma, g, re)
         {
@@ -496,6 +550,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_SYNC();
             }
             for (int k = N - 1; k >= 0; k--) {
+                LPC_PTICK(1);
                 q = qn;
                 if (k > 0) fetchA(k - 1, qn);
                 lazy(k, q);
@@ -529,6 +584,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 znext = q.z;
                 LPC_SYNC();
+                LPC_PTICK(0);
                 // M = P [A B] (row r per x-lane; [A B] from SGPRs), Pr = P re, v = Pr + p
                 cptr<T> ab = abs_;
                 asm volatile("" : "+s"(ab));
@@ -557,6 +613,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     for (int c = 0; c < NZ; c++) mt[c * LDX + r] = mrow[c];
                 }
                 LPC_SYNC();
+                LPC_PTICK(3);
                 // F = [A B]' M + H (column r per lane; + Sigma on the diagonal, applied by the
                 // readers), h = [A B]' v + g
                 T fcol[NZ], h;
@@ -599,6 +656,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     hub[u] = h;
                 }
                 LPC_SYNC();
+                LPC_PTICK(4);
                 // F_uu = L L' (every lane), kff = -F_uu^{-1} h_u
                 T lf[NUT], hu[NU];
 #pragma unroll
@@ -672,14 +730,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 sdiag = sg;
                 pv = pnew;
                 LPC_SYNC();
+                LPC_PTICK(7);
             }
         }
 
+        LPC_TICK(1);
         pending = false;   // the previous step is applied (converged groups stay frozen from here)
 
         // ============================ B: forward predictor + ratio test / centring sums
         T a_aff, S0, S2, dummy;
         forward(false, a_aff, S0, S2, dummy);
+        LPC_TICK(2);
         // mu_aff = [(1 - a) S0 - a^2 S2'] / m with S2' = sum lam dz (t + dz) / t (closed form)
         const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
         const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
@@ -705,6 +766,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 T pr, kq[NU];
             };
             auto fetchC = [&](int k, RecC &q) {
+                k = k < 0 ? 0 : k;
                 q.e.z = ldE(L::Z, k);
                 q.e.ll = ldE(L::LL, k);
                 q.e.lu = ldE(L::LU, k);
@@ -721,47 +783,56 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
             };
             const T *acol = abt + r * LDX;   // column r of [A B] (LDS, read per stage)
-            RecC q, qn;
-            fetchC(N, q);
-            fetchC(N - 1, qn);
-            T pv = ghat(N, q.e);
-            for (int k = N - 1; k >= 0; k--) {
-                q = qn;
-                if (k > 0) fetchC(k - 1, qn);
-                const T gh = ghat(k, q.e);
-                if (xl) vb[r] = q.pr + pv;
-                LPC_SYNC();
-                T h0 = gh, h1 = 0;
+            RecC qN;
+            fetchC(N, qN);
+            T pv = ghat(N, qN.e);
+            RecC ring[PD];
 #pragma unroll
-                for (int i = 0; i + 1 < NX; i += 2) {
-                    h0 = fma(acol[i], vb[i], h0);
-                    h1 = fma(acol[i + 1], vb[i + 1], h1);
+            for (int j = 0; j < PD; j++) fetchC(N - 1 - j, ring[j]);
+            for (int kb = 0; kb < N; kb += PD) {
+#pragma unroll
+                for (int j = 0; j < PD; j++) {
+                    const int k = N - 1 - kb - j;
+                    if (k < 0) break;
+                    const RecC q = ring[j];
+                    fetchC(k - PD, ring[j]);
+                    const T gh = ghat(k, q.e);
+                    if (xl) vb[r] = q.pr + pv;
+                    LPC_SYNC();
+                    T h0 = gh, h1 = 0;
+#pragma unroll
+                    for (int i = 0; i + 1 < NX; i += 2) {
+                        h0 = fma(acol[i], vb[i], h0);
+                        h1 = fma(acol[i + 1], vb[i + 1], h1);
+                    }
+                    if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                    const T h = h0 + h1;
+                    if (ul) hub[u] = h;
+                    LPC_SYNC();
+                    T hu[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) hu[i] = hub[i];
+                    if (ul) {
+                        T kf = 0;
+#pragma unroll
+                        for (int i = 0; i < NU; i++) kf = fma(-q.kq[i], hu[i], kf);
+                        stU(k, UKFF, kf);
+                    } else {
+                        T s_ = h;
+#pragma unroll
+                        for (int i = 0; i < NU; i++) s_ = fma(q.kq[i], hu[i], s_);
+                        pv = s_;
+                    }
+                    LPC_SYNC();
                 }
-                if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
-                const T h = h0 + h1;
-                if (ul) hub[u] = h;
-                LPC_SYNC();
-                T hu[NU];
-#pragma unroll
-                for (int i = 0; i < NU; i++) hu[i] = hub[i];
-                if (ul) {
-                    T kf = 0;
-#pragma unroll
-                    for (int i = 0; i < NU; i++) kf = fma(-q.kq[i], hu[i], kf);
-                    stU(k, UKFF, kf);
-                } else {
-                    T s_ = h;
-#pragma unroll
-                    for (int i = 0; i < NU; i++) s_ = fma(q.kq[i], hu[i], s_);
-                    pv = s_;
-                }
-                LPC_SYNC();
             }
         }
 
+        LPC_TICK(5);
         // ============================ D: forward corrector + step length / new mu
         T amax, T0, C1, C2;
         forward(true, amax, T0, C1, C2);
+        LPC_TICK(6);
         const T a = fmin(T(1), T(0.995) * amax);
         if (active) {
             // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
@@ -786,6 +857,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     if (r == 0) {
         p.status[inst] = status;
         p.iters[inst] = iters;
+#ifdef NMPC_SWEEP_TIMING
+        if (timed) {
+            unsigned long long *c = p.cycles + (size_t)inst * 9;
+            for (int j = 0; j < 8; j++) c[j] = tcy[j];
+            c[8] = __builtin_amdgcn_s_memtime() - tstart;
+        }
+#endif
     }
 }
 

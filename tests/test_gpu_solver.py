@@ -39,16 +39,21 @@ def rel_err(X, U, Xr, Ur):
     return err / scale
 
 
-def solve_batch(key, cases, precision="fp64", reps=1, ipw=None):
+def solve_batch(key, cases, precision="fp64", reps=1, ipw=None, kernel=None):
+    """kernel: None (default family: lane-per-component), "wave" (wavefront-per-instance,
+    with ipw instances per wavefront) or "lpc"."""
     name, N = split(key)
     x0 = np.tile(cases[key + "_x0"], (reps, 1))
     y = np.tile(cases[key + "_yref"], (reps, 1))
     if ipw:
         os.environ["NMPC_IPW"] = str(ipw)
+    if kernel:
+        os.environ["NMPC_KERNEL"] = kernel
     try:
         s = AcadosOcpSolver(OCPS[name](N), batch=x0.shape[0], precision=precision)
     finally:
         os.environ.pop("NMPC_IPW", None)
+        os.environ.pop("NMPC_KERNEL", None)
     s.set_batch("x0", x0)
     s.set_batch("yref", y)
     st = s.solve()
@@ -73,11 +78,28 @@ def test_batch_parity_fp64(key, cases):
 @pytest.mark.parametrize("key", ["force_N20", "jerk_N40"])
 @pytest.mark.parametrize("ipw", [1, 2, 4])
 def test_instance_packing_variants(key, ipw, cases):
-    """Every compiled lane-group width gives the same answer (tail groups included)."""
-    s, st = solve_batch(key, cases, reps=1, ipw=ipw)
+    """Every compiled lane-group width of the wavefront-per-instance family gives the same
+    answer (tail groups included)."""
+    s, st = solve_batch(key, cases, reps=1, ipw=ipw, kernel="wave")
+    assert s.launch_info()["instances_per_wave"] == ipw
     assert st == 0
     e = rel_err(s.get_batch("x"), s.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
     assert e.max() < TOL64
+
+
+@pytest.mark.parametrize("key", KEYS)
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_kernel_families_agree(key, precision, cases):
+    """Lane-per-component (default) and wavefront-per-instance kernels: same statuses, same
+    iterates to rounding, both within the oracle bar."""
+    a, sa = solve_batch(key, cases, precision=precision, kernel="lpc")
+    b, sb = solve_batch(key, cases, precision=precision, kernel="wave")
+    assert a.launch_info()["instances_per_wave"] == 64 // (a.nx + a.nu)
+    assert (a.get_batch_int("status") == b.get_batch_int("status")).all()
+    tol = TOL64 if precision == "fp64" else TOL32
+    ea = rel_err(a.get_batch("x"), a.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
+    eb = rel_err(b.get_batch("x"), b.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
+    assert ea.max() < tol and eb.max() < tol, (ea.max(), eb.max())
 
 
 def test_ragged_batch(cases):
