@@ -406,10 +406,11 @@ class AcadosOcpSolver:
         return self._check(self.lib.nmpc_set_stream(self._h, ctypes.c_void_p(stream_ptr)), "set_stream")
 
     def launch_info(self):
-        out = (ctypes.c_int * 5)()
-        self._check(self.lib.nmpc_get_launch_info(self._h, out, 5), "launch_info")
+        out = (ctypes.c_int * 6)()
+        self._check(self.lib.nmpc_get_launch_info(self._h, out, 6), "launch_info")
         return {"instances_per_wave": out[0], "workgroups": out[1], "threads": out[2], "lds_bytes": out[3],
-                "kernel": "ipm_lpc_kernel" if out[4] == 1 else "ipm_kernel"}
+                "kernel": "ipm_lpc_kernel" if out[4] == 1 else "ipm_kernel",
+                "structure": {0: "dense", 1: "force", 2: "jerk", 3: "quad13"}.get(out[5], str(out[5]))}
 
     def discrete_model(self):
         A = np.zeros((self.nx, self.nx))

@@ -580,6 +580,16 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
     const size_t model_bytes = off;
+    {
+        // structure-specialised kernel when the model fits one (exact zeros of [A B], diagonal costs)
+        std::vector<double> ABh((size_t)nx * nz);
+        for (int r = 0; r < nx; r++) {
+            for (int q = 0; q < nx; q++) ABh[r * nz + q] = h->A[r * nx + q];
+            for (int q = 0; q < nu; q++) ABh[r * nz + nx + q] = h->B[r * nu + q];
+        }
+        h->kidx = precision == NMPC_FP64 ? nmpc::ipm_refine<double>(h->kidx, ABh.data(), h->H.data(), h->He.data())
+                                         : nmpc::ipm_refine<float>(h->kidx, ABh.data(), h->H.data(), h->He.data());
+    }
     const size_t scratch_bytes = (precision == NMPC_FP64 ? nmpc::ipm_scratch_elems<double>(h->kidx, batch, N)
                                                          : nmpc::ipm_scratch_elems<float>(h->kidx, batch, N)) * es;
     bool ok = hipMalloc(&h->d_model, model_bytes) == hipSuccess &&
@@ -888,9 +898,11 @@ int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
 {
     if (!h || !out) return NMPC_EINVAL;
     const int waves = (h->batch + h->ipw - 1) / h->ipw;
-    const int kind = h->precision == NMPC_FP64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
-    const int v[5] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind};
-    for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
+    const bool f64 = h->precision == NMPC_FP64;
+    const int kind = f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
+    const int sid = f64 ? nmpc::ipm_structure<double>(h->kidx) : nmpc::ipm_structure<float>(h->kidx);
+    const int v[6] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid};
+    for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
     return 0;
 }
 

@@ -50,6 +50,12 @@ size_t ipm_scratch_elems(int idx, int B, int N);
 // kernel family of entry `idx`: 0 wavefront per instance block, 1 lane per component
 template <typename T>
 int ipm_kind(int idx);
+// structure-specialised twin of entry idx that the model (host [A B] row-major nx x (nx+nu),
+// H, He) fits, else idx; and the structure id of an entry (0 dense)
+template <typename T>
+int ipm_refine(int idx, const double *AB, const double *H, const double *He);
+template <typename T>
+int ipm_structure(int idx);
 
 // closed-loop step kernels (nmpc_closed_loop.hip)
 template <typename T>

@@ -944,6 +944,8 @@ struct IpmEntry {
     hipError_t (*fn)(const IpmParams<T> &, hipStream_t);
     int lds_bytes;
     size_t (*scratch)(int B, int N);
+    int sid;    // model structure the kernel is specialised for (0: dense, any model)
+    bool (*fits)(const double *AB, const double *H, const double *He);
 };
 
 template <typename T, int NX, int NU, int IPW, int WPB>
@@ -959,14 +961,15 @@ static constexpr IpmEntry<T> entry()
 {
     return IpmEntry<T>{0, NX, NU, IPW, WPB, MW, &launch_ipm<T, NX, NU, IPW, WPB, MW>,
                        (int)(sizeof(T) * Geometry<T, NX, NU, IPW, WPB>::LDS_ELEMS),
-                       &wave_scratch_elems<T, NX, NU, IPW, WPB>};
+                       &wave_scratch_elems<T, NX, NU, IPW, WPB>, 0, nullptr};
 }
 
-template <typename T, int NX, int NU, int WPB, int MW>
+template <typename T, int NX, int NU, int WPB, int MW, class SP = lpc::DenseStructure<NX, NU>>
 static constexpr IpmEntry<T> entry_lpc()
 {
-    return IpmEntry<T>{1, NX, NU, lpc::Geom<T, NX, NU, WPB>::IPW, WPB, MW, &launch_ipm_lpc<T, NX, NU, WPB, MW>,
-                       (int)(sizeof(T) * lpc::Geom<T, NX, NU, WPB>::LDS_ELEMS), &lpc::scratch_elems<T, NX, NU, WPB>};
+    return IpmEntry<T>{1, NX, NU, lpc::Geom<T, NX, NU, WPB>::IPW, WPB, MW, &launch_ipm_lpc<T, NX, NU, WPB, MW, SP>,
+                       (int)(sizeof(T) * lpc::Geom<T, NX, NU, WPB>::LDS_ELEMS), &lpc::scratch_elems<T, NX, NU, WPB>,
+                       SP::id, SP::id ? &lpc::structure_fits<SP, NX, NU> : nullptr};
 }
 
 template <typename T>
@@ -979,9 +982,14 @@ static const IpmEntry<T> *table(int *n)
         // selectable with NMPC_VARIANT for tuning runs
         entry<T, 13, 4, 1, 1, 3>(), entry<T, 13, 4, 1, 4>(), entry<T, 13, 4, 1, 1, 2>(),
         entry<T, 13, 4, 1, 4, 3>(), entry<T, 13, 4, 1, 2, 4>(),
-        // lane-per-component kernels (NMPC_KERNEL=lpc)
+        // lane-per-component kernels (the default family); the first listed per (nx, nu) is
+        // the default variant
         entry_lpc<T, 13, 4, 4, 3>(), entry_lpc<T, 13, 4, 1, 3>(), entry_lpc<T, 13, 4, 2, 2>(),
         entry_lpc<T, 4, 2, 4, 2>(), entry_lpc<T, 6, 2, 4, 2>(),
+        // their structure-specialised twins (chosen by ipm_refine when the model fits)
+        entry_lpc<T, 13, 4, 4, 3, lpc::Quad13Structure>(), entry_lpc<T, 13, 4, 1, 3, lpc::Quad13Structure>(),
+        entry_lpc<T, 13, 4, 2, 2, lpc::Quad13Structure>(), entry_lpc<T, 4, 2, 4, 2, lpc::ForceStructure>(),
+        entry_lpc<T, 6, 2, 4, 2, lpc::JerkStructure>(),
     };
     *n = (int)(sizeof(t) / sizeof(t[0]));
     return t;
@@ -1008,7 +1016,7 @@ int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_o
     if (var) {
         int want = atoi(var), seen = 0;
         for (int i = 0; i < n; i++) {
-            if (t[i].nx != nx || t[i].nu != nu || t[i].kind != kind) continue;
+            if (t[i].nx != nx || t[i].nu != nu || t[i].kind != kind || t[i].sid) continue;
             if (seen++ == want) {
                 *ipw_out = t[i].ipw;
                 *lds_out = t[i].lds_bytes;
@@ -1018,10 +1026,10 @@ int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_o
         }
     }
     bool have = false;
-    for (int i = 0; i < n; i++) have |= t[i].nx == nx && t[i].nu == nu && t[i].kind == kind;
+    for (int i = 0; i < n; i++) have |= t[i].nx == nx && t[i].nu == nu && t[i].kind == kind && !t[i].sid;
     const int fam = have ? kind : 1 - kind;
     for (int i = 0; i < n; i++) {
-        if (t[i].nx != nx || t[i].nu != nu || t[i].kind != fam) continue;
+        if (t[i].nx != nx || t[i].nu != nu || t[i].kind != fam || t[i].sid) continue;
         if (fam == 1) {   // lane-per-component: instances per wave fixed by nx + nu, first listed
             if (best < 0) best = i;
         } else if (ipw_req > 0) {
@@ -1052,6 +1060,38 @@ size_t ipm_scratch_elems(int idx, int B, int N)
     const IpmEntry<T> *t = table<T>(&n);
     return t[idx].scratch(B, N);
 }
+
+// the structure-specialised twin of dense entry `idx` (same family, shape, workgroup and
+// occupancy target) whose structure the model fits, else idx. NMPC_STRUCT=0 disables.
+template <typename T>
+int ipm_refine(int idx, const double *AB, const double *H, const double *He)
+{
+    int n;
+    const IpmEntry<T> *t = table<T>(&n);
+    const char *e = getenv("NMPC_STRUCT");
+    if (e && e[0] == '0') return idx;
+    const IpmEntry<T> &d = t[idx];
+    for (int i = 0; i < n; i++) {
+        const IpmEntry<T> &c = t[i];
+        if (c.sid && c.kind == d.kind && c.nx == d.nx && c.nu == d.nu && c.wpb == d.wpb && c.mw == d.mw &&
+            c.fits(AB, H, He))
+            return i;
+    }
+    return idx;
+}
+
+template <typename T>
+int ipm_structure(int idx)
+{
+    int n;
+    const IpmEntry<T> *t = table<T>(&n);
+    return t[idx].sid;
+}
+
+template int ipm_refine<double>(int, const double *, const double *, const double *);
+template int ipm_refine<float>(int, const double *, const double *, const double *);
+template int ipm_structure<double>(int);
+template int ipm_structure<float>(int);
 
 template <typename T>
 int ipm_kind(int idx)

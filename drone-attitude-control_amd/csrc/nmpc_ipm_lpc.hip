@@ -34,6 +34,8 @@
 #include "nmpc_internal.h"
 #include "nmpc_lpc_geom.h"
 
+#define NMPC_COMMA ,
+
 // stage records in flight ahead of the vector sweeps B, C, D
 #ifndef NMPC_LPC_PF
 #define NMPC_LPC_PF 1
@@ -113,27 +115,37 @@ __device__ __forceinline__ T gred(T v, int lane, int r, Op op)
     return __shfl(v, lane - r, 64);
 }
 
-// Stream the rows of a wave-uniform NR x NC matrix (constant address space) through SGPRs,
-// one row ahead of its use: body(l, row) consumes row l while row l+1 is in flight. The
-// scheduling barriers keep the compiler from hoisting every row's s_load at once (which
-// would exhaust the SGPR file and spill to VGPR lanes).
-template <int NR, int NC, typename T, typename Body>
+// Stream the rows of a wave-uniform NR x NC matrix (constant address space) through SGPRs in
+// chunks of RPC rows, one chunk ahead of its use: body(l, row) consumes row l while the next
+// chunk is in flight. Only entries the structure SP allows are loaded (the rest read as 0 and
+// the bodies skip them). The scheduling barriers keep the compiler from hoisting every
+// chunk's s_load at once (which would exhaust the SGPR file and spill to VGPR lanes).
+template <int NR, int NC, int RPC, class SP, typename T, typename Body>
 __device__ __forceinline__ void sgpr_rows(cptr<T> m, Body body)
 {
-    T cur[NC], nxt[NC];
+    constexpr int NCH = (NR + RPC - 1) / RPC;
+    T cur[RPC][NC], nxt[RPC][NC];
+    auto load = [&](int ch, T (&dst)[RPC][NC]) {
 #pragma unroll
-    for (int c = 0; c < NC; c++) cur[c] = m[c];
+        for (int rr = 0; rr < RPC; rr++) {
+            const int l = ch * RPC + rr;
 #pragma unroll
-    for (int l = 0; l < NR; l++) {
-        if (l + 1 < NR) {
-#pragma unroll
-            for (int c = 0; c < NC; c++) nxt[c] = m[(l + 1) * NC + c];
+            for (int c = 0; c < NC; c++) dst[rr][c] = (l < NR && SP::ab(l, c)) ? m[l * NC + c] : T(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        body(l, cur);
+    };
+    load(0, cur);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+        if (ch + 1 < NCH) load(ch + 1, nxt);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int c = 0; c < NC; c++) cur[c] = nxt[c];
+        for (int rr = 0; rr < RPC; rr++)
+            if (ch * RPC + rr < NR) body(ch * RPC + rr, cur[rr]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int rr = 0; rr < RPC; rr++)
+#pragma unroll
+            for (int c = 0; c < NC; c++) cur[rr][c] = nxt[rr][c];
     }
 }
 
@@ -168,9 +180,11 @@ struct Buf {
     }
 };
 
-template <typename T, int NX, int NU, int WPB, int MW>
+template <typename T, int NX, int NU, int WPB, int MW, class SP>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8))) void ipm_lpc_kernel(IpmParams<T> p)
 {
+    // rows of [A B] per SGPR chunk: ~16 loaded elements per chunk
+    constexpr int RPC = SP::max_row_nnz >= 16 ? 1 : (16 / SP::max_row_nnz < NX ? 16 / SP::max_row_nnz : NX);
     using Gm = Geom<T, NX, NU, WPB>;
     constexpr int NZ = Gm::NZ, IPW = Gm::IPW, VS = Gm::VS, LDZ = Gm::LDZ, LDX = Gm::LDX, LDU = Gm::LDU;
     constexpr int NUT = NU * (NU + 1) / 2;
@@ -539,12 +553,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 zb[r] = xl ? q.z : T(0);
                 LPC_SYNC();
                 T g = q.g;
+                const int rx = xl ? r : 0;
+                if (SP::hdiag) {
+                    g = fma(hem[rx * LDX + rx], q.z, g);
+                } else {
 #pragma unroll
-                for (int b = 0; b < NX; b++) g = fma(hem[(xl ? r : 0) * LDX + b], zb[b], g);
+                    for (int b = 0; b < NX; b++) g = fma(hem[rx * LDX + b], zb[b], g);
+                }
                 if (xl) stE(L::GF, N, g);
 #pragma unroll
-                for (int i = 0; i < NX; i++) prow[i] = hem[(xl ? r : 0) * LDX + i];
-                sdiag = sg;
+                for (int i = 0; i < NX; i++) prow[i] = SP::hdiag ? T(0) : hem[rx * LDX + i];
+                sdiag = sg + (SP::hdiag ? hem[rx * LDX + rx] : T(0));
                 pv = g;
                 znext = q.z;
                 LPC_SYNC();
@@ -559,7 +578,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_SYNC();
                 // g = H z + G yref, re = [A B] z_k + c - x_{k+1}
                 T g = q.g, re = 0;
-                {
+                if (SP::hdiag) {
+                    g = fma(hm[r * LDZ + r], q.z, g);
+                } else {
                     T g1 = 0;
 #pragma unroll
                     for (int b = 0; b + 1 < NZ; b += 2) {
@@ -605,9 +626,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     T mrow[NZ];
 #pragma unroll
                     for (int c = 0; c < NZ; c++) mrow[c] = sdiag * abr[r * LDZ + c];
-                    sgpr_rows<NX, NZ, T>(ab, [&](int l, const T (&row)[NZ]) {
+                    sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int l, const T (&row)[NZ]) {
 #pragma unroll
-                        for (int c = 0; c < NZ; c++) mrow[c] = fma(prow[l], row[c], mrow[c]);
+                        for (int c = 0; c < NZ; c++)
+                            if (SP::ab(l, c)) mrow[c] = fma(prow[l], row[c], mrow[c]);
                     });
 #pragma unroll
                     for (int c = 0; c < NZ; c++) mt[c * LDX + r] = mrow[c];
@@ -633,11 +655,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #pragma unroll
                     for (int i = 0; i < NX; i++) mc[i] = mt[r * LDX + i];
 #pragma unroll
-                    for (int a = 0; a < NZ; a++) fcol[a] = hm[r * LDZ + a];
+                    for (int a = 0; a < NZ; a++) fcol[a] = SP::hdiag ? T(0) : hm[r * LDZ + a];
                     asm volatile("" : "+s"(ab));
-                    sgpr_rows<NX, NZ, T>(ab, [&](int i, const T (&row)[NZ]) {
+                    sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int i, const T (&row)[NZ]) {
 #pragma unroll
-                        for (int a = 0; a < NZ; a++) fcol[a] = fma(row[a], mc[i], fcol[a]);
+                        for (int a = 0; a < NZ; a++)
+                            if (SP::ab(i, a)) fcol[a] = fma(row[a], mc[i], fcol[a]);
                     });
                     // materialise F here (IR sinking would otherwise defer the x part to the P
                     // update and keep every streamed row of [A B] alive in SGPRs until then)
@@ -652,7 +675,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         fu[a * NU + u] = fcol[NX + a];
                         fd = (u == a) ? fcol[NX + a] : fd;
                     }
-                    fu[u * NU + u] = fd + sg;
+                    fu[u * NU + u] = fd + sg + (SP::hdiag ? hm[r * LDZ + r] : T(0));
                     hub[u] = h;
                 }
                 LPC_SYNC();
@@ -727,7 +750,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     for (int a = 0; a < NU; a++) s_ = fma(-ylds[i * LDU + a], y[a], s_);
                     prow[i] = s_;
                 }
-                sdiag = sg;
+                sdiag = sg + (SP::hdiag ? hm[r * LDZ + r] : T(0));   // F(r, r) = F_col(r) + H_rr + Sigma
                 pv = pnew;
                 LPC_SYNC();
                 LPC_PTICK(7);
@@ -870,25 +893,30 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 }  // namespace lpc
 
 // ---------------------------------------------------------------------- launch glue
-template <typename T, int NX, int NU, int WPB, int MW>
+template <typename T, int NX, int NU, int WPB, int MW, class SP>
 hipError_t launch_ipm_lpc(const IpmParams<T> &p, hipStream_t s)
 {
     using Gm = lpc::Geom<T, NX, NU, WPB>;
     const int waves = (p.B + Gm::IPW - 1) / Gm::IPW;
     const int blocks = (waves + WPB - 1) / WPB;
-    hipLaunchKernelGGL((lpc::ipm_lpc_kernel<T, NX, NU, WPB, MW>), dim3(blocks), dim3(64 * WPB), 0, s, p);
+    hipLaunchKernelGGL((lpc::ipm_lpc_kernel<T, NX, NU, WPB, MW, SP>), dim3(blocks), dim3(64 * WPB), 0, s, p);
     return hipGetLastError();
 }
 
 // explicit instantiations (the dispatch table in nmpc_ipm.hip binds them)
-#define NMPC_LPC_INST(NX, NU, WPB, MW)                                                              \
-    template hipError_t launch_ipm_lpc<double, NX, NU, WPB, MW>(const IpmParams<double> &, hipStream_t); \
-    template hipError_t launch_ipm_lpc<float, NX, NU, WPB, MW>(const IpmParams<float> &, hipStream_t);
-NMPC_LPC_INST(13, 4, 4, 3)
-NMPC_LPC_INST(13, 4, 1, 3)
-NMPC_LPC_INST(13, 4, 2, 2)
-NMPC_LPC_INST(4, 2, 4, 2)
-NMPC_LPC_INST(6, 2, 4, 2)
+#define NMPC_LPC_INST(NX, NU, WPB, MW, SP)                                                              \
+    template hipError_t launch_ipm_lpc<double, NX, NU, WPB, MW, SP>(const IpmParams<double> &, hipStream_t); \
+    template hipError_t launch_ipm_lpc<float, NX, NU, WPB, MW, SP>(const IpmParams<float> &, hipStream_t);
+NMPC_LPC_INST(13, 4, 4, 3, lpc::DenseStructure<13 NMPC_COMMA 4>)
+NMPC_LPC_INST(13, 4, 1, 3, lpc::DenseStructure<13 NMPC_COMMA 4>)
+NMPC_LPC_INST(13, 4, 2, 2, lpc::DenseStructure<13 NMPC_COMMA 4>)
+NMPC_LPC_INST(4, 2, 4, 2, lpc::DenseStructure<4 NMPC_COMMA 2>)
+NMPC_LPC_INST(6, 2, 4, 2, lpc::DenseStructure<6 NMPC_COMMA 2>)
+NMPC_LPC_INST(13, 4, 4, 3, lpc::Quad13Structure)
+NMPC_LPC_INST(13, 4, 1, 3, lpc::Quad13Structure)
+NMPC_LPC_INST(13, 4, 2, 2, lpc::Quad13Structure)
+NMPC_LPC_INST(4, 2, 4, 2, lpc::ForceStructure)
+NMPC_LPC_INST(6, 2, 4, 2, lpc::JerkStructure)
 #undef NMPC_LPC_INST
 
 }  // namespace nmpc

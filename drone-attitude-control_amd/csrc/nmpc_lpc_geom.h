@@ -57,7 +57,84 @@ inline size_t scratch_elems(int B, int N)
 
 }  // namespace lpc
 
-template <typename T, int NX, int NU, int WPB, int MW>
+template <typename T, int NX, int NU, int WPB, int MW, class SP>
 hipError_t launch_ipm_lpc(const IpmParams<T> &p, hipStream_t s);
 
+}  // namespace nmpc
+
+namespace nmpc {
+namespace lpc {
+
+// ---------------------------------------------------------------------------------------
+// Compile-time model structure for the structure-specialised LPC kernels — the GPU analogue
+// of acados generating model-specific C code (force_model/ocp.py:95-96 builds one solver per
+// model). rows[l] has bit c set where [A B](l, c) may be nonzero: the structural closure of
+// the continuous model (any integrator's discrete map of an affine ODE stays inside it).
+// hdiag: H and He diagonal (LINEAR_LS with selection Vx/Vu and diagonal W, as every
+// reference model has). tests/test_structures.py recomputes the masks from models.py. The
+// host selects such a kernel only when the handle's discrete [A B] is exactly zero outside
+// the mask and H, He are diagonal (nmpc::ipm_refine); otherwise the dense kernel runs.
+template <int NX, int NU>
+struct DenseStructure {
+    static constexpr int id = 0;
+    static constexpr bool hdiag = false;
+    static constexpr bool ab(int, int) { return true; }
+    static constexpr int max_row_nnz = NX + NU;
+};
+
+// the mask rows are a template pack (not an array in memory) so that ab(l, c) folds to a
+// constant once the stage loops are unrolled
+template <int NX, int NU, int ID, unsigned... ROWS>
+struct MaskStructure {
+    static_assert(sizeof...(ROWS) == NX, "one mask row per state");
+    static constexpr int id = ID;
+    static constexpr bool hdiag = true;
+    static constexpr bool ab(int l, int c)
+    {
+        int i = 0;
+        bool res = false;
+        ((res = (i++ == l) ? ((ROWS >> c) & 1u) != 0 : res), ...);
+        return res;
+    }
+    static constexpr int max_nnz()
+    {
+        int m = 0;
+        for (int l = 0; l < NX; l++) {
+            int n = 0;
+            for (int c = 0; c < NX + NU; c++) n += ab(l, c) ? 1 : 0;
+            m = n > m ? n : m;
+        }
+        return m;
+    }
+    static constexpr int max_row_nnz = max_nnz();
+};
+
+// force_model (force_model/dynamics.py:32-37): x = [px, pz, vx, vz], u = [Fx, Fz]
+using ForceStructure = MaskStructure<4, 2, 1, 0x15u, 0x2au, 0x14u, 0x28u>;
+// jerk_model (jerk_model/dynamics.py:35-42): x = [px, pz, vx, vz, ax, az], u = [hx, hz]
+using JerkStructure = MaskStructure<6, 2, 2, 0x55u, 0xaau, 0x54u, 0xa8u, 0x50u, 0xa0u>;
+// quad13 (models.py quad13_model): x = [p, v, q, w], u = [aT, alpha]
+using Quad13Structure = MaskStructure<13, 4, 3, 0x8909u, 0x4492u, 0x2024u, 0x8908u, 0x4490u, 0x2020u, 0x40u, 0x4480u,
+                                      0x8900u, 0x11200u, 0x4400u, 0x8800u, 0x11000u>;
+
+// host check: the model fits structure SP (exact zeros outside the mask, diagonal costs)
+template <class SP, int NX, int NU>
+inline bool structure_fits(const double *AB, const double *H, const double *He)
+{
+    constexpr int NZ = NX + NU;
+    for (int l = 0; l < NX; l++)
+        for (int c = 0; c < NZ; c++)
+            if (!SP::ab(l, c) && AB[l * NZ + c] != 0.0) return false;
+    if (SP::hdiag) {
+        for (int i = 0; i < NZ; i++)
+            for (int j = 0; j < NZ; j++)
+                if (i != j && H[i * NZ + j] != 0.0) return false;
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j < NX; j++)
+                if (i != j && He[i * NX + j] != 0.0) return false;
+    }
+    return true;
+}
+
+}  // namespace lpc
 }  // namespace nmpc

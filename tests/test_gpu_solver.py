@@ -39,9 +39,10 @@ def rel_err(X, U, Xr, Ur):
     return err / scale
 
 
-def solve_batch(key, cases, precision="fp64", reps=1, ipw=None, kernel=None):
+def solve_batch(key, cases, precision="fp64", reps=1, ipw=None, kernel=None, structure=True):
     """kernel: None (default family: lane-per-component), "wave" (wavefront-per-instance,
-    with ipw instances per wavefront) or "lpc"."""
+    with ipw instances per wavefront) or "lpc"; structure=False forces the dense
+    lane-per-component kernel instead of the model-structure-specialised one."""
     name, N = split(key)
     x0 = np.tile(cases[key + "_x0"], (reps, 1))
     y = np.tile(cases[key + "_yref"], (reps, 1))
@@ -49,11 +50,14 @@ def solve_batch(key, cases, precision="fp64", reps=1, ipw=None, kernel=None):
         os.environ["NMPC_IPW"] = str(ipw)
     if kernel:
         os.environ["NMPC_KERNEL"] = kernel
+    if not structure:
+        os.environ["NMPC_STRUCT"] = "0"
     try:
         s = AcadosOcpSolver(OCPS[name](N), batch=x0.shape[0], precision=precision)
     finally:
         os.environ.pop("NMPC_IPW", None)
         os.environ.pop("NMPC_KERNEL", None)
+        os.environ.pop("NMPC_STRUCT", None)
     s.set_batch("x0", x0)
     s.set_batch("yref", y)
     st = s.solve()
@@ -100,6 +104,20 @@ def test_kernel_families_agree(key, precision, cases):
     ea = rel_err(a.get_batch("x"), a.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
     eb = rel_err(b.get_batch("x"), b.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
     assert ea.max() < tol and eb.max() < tol, (ea.max(), eb.max())
+
+
+@pytest.mark.parametrize("key", KEYS)
+def test_structure_specialised_matches_dense(key, cases):
+    """The model-structure-specialised kernel (chosen by default: every shipped model fits its
+    compiled [A B] mask and diagonal cost) and the dense one agree to rounding."""
+    a, sa = solve_batch(key, cases)
+    b, sb = solve_batch(key, cases, structure=False)
+    assert a.launch_info()["structure"] == split(key)[0]
+    assert b.launch_info()["structure"] == "dense"
+    assert sa == 0 and sb == 0
+    for f in ("x", "u"):
+        A, B = a.get_batch(f), b.get_batch(f)
+        assert np.abs(A - B).max() <= 1e-9 * max(1.0, np.abs(B).max())
 
 
 def test_ragged_batch(cases):
