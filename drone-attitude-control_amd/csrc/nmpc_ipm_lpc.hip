@@ -232,17 +232,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 
     // ---- scratch: VS instance slots per wavefront, lane-owned elements
     using L = Layout<NX, NU>;
-    const unsigned slot = (unsigned)L::slot(N);
     Buf<T> S;
-    S.r = __builtin_amdgcn_make_buffer_rsrc(p.scratch + wg * VS * slot, 0, (int)(VS * slot * sizeof(T)), 0x00020000);
-    const unsigned lo_e = (unsigned)grp * slot + (unsigned)r;        // element (k, r) / x record of lane r
-    const unsigned lo_u = (unsigned)grp * slot + (unsigned)u;        // u record of lane r = nx + u
-    auto ldE = [&](int arr, int k) { return S.ld((unsigned)k * L::BLK, lo_e + arr); };
-    auto stE = [&](int arr, int k, T v) { S.st((unsigned)k * L::BLK, lo_e + arr, v); };
-    auto ldX = [&](int k, int w) { return S.ld((unsigned)k * L::BLK, lo_e + L::XREC + w * NX); };
-    auto stX = [&](int k, int w, T v) { S.st((unsigned)k * L::BLK, lo_e + L::XREC + w * NX, v); };
-    auto ldU = [&](int k, int w) { return S.ld((unsigned)k * L::BLK, lo_u + L::UREC + w * NU); };
-    auto stU = [&](int k, int w, T v) { S.st((unsigned)k * L::BLK, lo_u + L::UREC + w * NU, v); };
+    S.r = __builtin_amdgcn_make_buffer_rsrc(p.scratch + wg * L::wave_elems(N), 0, (int)(L::wave_elems(N) * sizeof(T)),
+                                            0x00020000);
+    // lane-interleaved: every word is one run of L::LW lanes; idle lanes point past the buffer
+    const unsigned lo = lane < L::LW ? (unsigned)lane : 0x1000000u;
+    auto off = [&](int k, int w) { return ((unsigned)k * L::NW + (unsigned)w) * (unsigned)L::LW; };
+    auto ldE = [&](int arr, int k) { return S.ld(off(k, arr), lo); };
+    auto stE = [&](int arr, int k, T v) { S.st(off(k, arr), lo, v); };
+    auto ldX = [&](int k, int w) { return S.ld(off(k, L::REC + w), lo); };
+    auto stX = [&](int k, int w, T v) { S.st(off(k, L::REC + w), lo, v); };
+    auto ldU = [&](int k, int w) { return S.ld(off(k, L::REC + w), lo); };
+    auto stU = [&](int k, int w, T v) { S.st(off(k, L::REC + w), lo, v); };
 
     const T *yref = p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
     const T *x0 = p.x0 + (size_t)inst * NX;
@@ -352,6 +353,41 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // ---- forward recursion (B: predictor into dza with ratio test / centring sums;
     //      D: corrector into dz with step length / new-mu sums):
     //      dx_0 = 0, du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx_k; du_k] + re_k
+#if (defined(NMPC_PHASE_TIMING) || defined(NMPC_FWD_TIMING)) && !defined(NMPC_SWEEP_TIMING)
+#define NMPC_SWEEP_TIMING 1
+#endif
+#ifdef NMPC_SWEEP_TIMING
+    // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per
+    // sweep, reported through the E_A/A/B/../D slots of nmpc_api.cpp (A -> 1, B -> 2, C -> 5, D -> 6)
+    const bool timed = p.cycles != nullptr;
+    unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = timed ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long tstart = tmark;
+    auto tick = [&](int slot) {
+        if (timed) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (slot >= 0) tcy[slot] += t - tmark;
+            tmark = t;
+        }
+    };
+#define LPC_TICK(slot) tick(slot)
+#else
+#define LPC_TICK(slot) ((void)0)
+#endif
+// NMPC_PHASE_TIMING: also split the Riccati stage into pre (lazy step, g, re) -> slot 0,
+// M -> 3, F -> 4, Cholesky / gains / P update -> 7
+#ifdef NMPC_PHASE_TIMING
+#define LPC_PTICK(slot) tick(slot)
+#else
+#define LPC_PTICK(slot) ((void)0)
+#endif
+// NMPC_FWD_TIMING: split the predictor sweep B into x writes (slot 0), u sums (3), x update (4),
+// statistics / store (7); the sweep remainder stays in slot 2
+#ifdef NMPC_FWD_TIMING
+#define LPC_FTICK(slot) do { if (!corr) tick(slot); } while (0)
+#else
+#define LPC_FTICK(slot) ((void)0)
+#endif
+
     auto forward = [&](bool corr, T &s_min, T &s_a, T &s_b, T &s_c) {
         const T *arow = abr + (xl ? r : 0) * LDZ;   // row r of [A B] (LDS, read per stage)
         s_min = 1;
@@ -431,6 +467,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             for (int j = 0; j < PD; j++) {
                 const int k = kb + j;
                 if (k >= N) break;
+                LPC_FTICK(2);
                 const Rec q = ring[j];
                 fetch(k + PD, ring[j]);
                 if (xl) {
@@ -439,6 +476,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     zb[r] = dx;
                 }
                 LPC_SYNC();
+                LPC_FTICK(0);
                 T du = 0;
                 if (ul) {
                     T s0 = q.c0, s1 = 0;
@@ -452,6 +490,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     zb[r] = du;
                 }
                 LPC_SYNC();
+                LPC_FTICK(3);
                 const T my = xl ? dx : du;
                 if (xl) {
                     T s0 = q.c0, s1 = 0;
@@ -463,9 +502,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
                     dx = s0 + s1;
                 }
+                LPC_FTICK(4);
                 stE(dst, k, my);
                 stats(k, my, q.e);
                 LPC_SYNC();
+                LPC_FTICK(7);
             }
         }
         if (xl) {
@@ -485,33 +526,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 
     cptr<T> abs_ = (cptr<T>)p.AB;   // [NX][NZ] row-major, wave-uniform SGPR operand
 
-#if defined(NMPC_PHASE_TIMING) && !defined(NMPC_SWEEP_TIMING)
-#define NMPC_SWEEP_TIMING 1
-#endif
-#ifdef NMPC_SWEEP_TIMING
-    // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per
-    // sweep, reported through the E_A/A/B/../D slots of nmpc_api.cpp (A -> 1, B -> 2, C -> 5, D -> 6)
-    const bool timed = p.cycles != nullptr;
-    unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = timed ? __builtin_amdgcn_s_memtime() : 0ull;
-    const unsigned long long tstart = tmark;
-    auto tick = [&](int slot) {
-        if (timed) {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            if (slot >= 0) tcy[slot] += t - tmark;
-            tmark = t;
-        }
-    };
-#define LPC_TICK(slot) tick(slot)
-#else
-#define LPC_TICK(slot) ((void)0)
-#endif
-// NMPC_PHASE_TIMING: also split the Riccati stage into pre (lazy step, g, re) -> slot 0,
-// M -> 3, F -> 4, Cholesky / gains / P update -> 7
-#ifdef NMPC_PHASE_TIMING
-#define LPC_PTICK(slot) tick(slot)
-#else
-#define LPC_PTICK(slot) ((void)0)
-#endif
 
     for (int it = 0;; it++) {
         const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
@@ -560,7 +574,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #pragma unroll
                     for (int b = 0; b < NX; b++) g = fma(hem[rx * LDX + b], zb[b], g);
                 }
-                if (xl) stE(L::GF, N, g);
+                if (xl && !SP::hdiag) stE(L::GF, N, g);   // diagonal costs: C recomputes g
 #pragma unroll
                 for (int i = 0; i < NX; i++) prow[i] = SP::hdiag ? T(0) : hem[rx * LDX + i];
                 sdiag = sg + (SP::hdiag ? hem[rx * LDX + rx] : T(0));
@@ -590,7 +604,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if (NZ % 2) g = fma(hm[r * LDZ + NZ - 1], zb[NZ - 1], g);
                     g += g1;
                 }
-                stE(L::GF, k, g);
+                if (!SP::hdiag) stE(L::GF, k, g);
                 if (xl) {
                     T s0 = c_r - znext, s1 = 0;
 #pragma unroll
@@ -700,6 +714,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         }
                     }
                 T y[NU], pnew = 0;
+                // stage record words 0..NU: x-lane r: K(:, r) (Pr_r sits in word NU, stored above);
+                // u-lane u: kff_u, F_uu^{-1}(u, :). Stored after the branch with one store per
+                // word (stores in both arms would be merged with a divergent offset)
+                T rec[NU + 1];
 #pragma unroll
                 for (int i = 0; i < NU; i++) y[i] = 0;
                 if (xl) {
@@ -724,8 +742,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     for (int i = 0; i < NU; i++) {
                         pnew = fma(kc[i], hu[i], pnew);
                         ylds[r * LDU + i] = y[i];
-                        stX(k, i, kc[i]);
+                        rec[i] = kc[i];
                     }
+                    rec[NU] = 0;
                 } else {
                     // row u of F_uu^{-1}, kff_u = -(F_uu^{-1} h_u)_u
                     T e[NU];
@@ -736,10 +755,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
                         kf = fma(-e[i], hu[i], kf);
-                        stU(k, UFI + i, e[i]);
+                        rec[UFI + i] = e[i];
                     }
-                    stU(k, UKFF, kf);
+                    rec[UKFF] = kf;
                 }
+#pragma unroll
+                for (int i = 0; i < NU; i++) stX(k, i, rec[i]);
+                if (ul) stU(k, NU, rec[NU]);
                 LPC_SYNC();
                 // P(r, :) = F(r, 0:nx) - Y(:, r)' Y  (+ Sigma_x of stage k on the diagonal); u-lanes
                 // compute a dummy row (keeps the loop-carried registers dead between stages)
@@ -773,6 +795,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         {
             auto ghat = [&](int k, const El &e) {
                 T g = e.g;
+                if (SP::hdiag) g = fma(k < N ? hm[r * LDZ + r] : hem[(xl ? r : 0) * LDX + (xl ? r : 0)], e.z, g);
                 const T lb = LB(k), ub = UB(k);
                 if (e.ll > T(0)) {
                     const T t = e.z - lb, it_ = frcp(t), dl = -e.ll * (T(1) + e.dza * it_);
@@ -794,7 +817,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 q.e.ll = ldE(L::LL, k);
                 q.e.lu = ldE(L::LU, k);
                 q.e.dza = ldE(L::DZA, k);
-                q.e.g = ldE(L::GF, k);
+                q.e.g = ldE(SP::hdiag ? L::GC : L::GF, k);   // diagonal costs: g = G yref + H_rr z below
                 const int kk = k < N ? k : N - 1;
                 if (xl) {
                     q.pr = ldX(kk, XPR);

@@ -32,18 +32,21 @@ struct Geom {
     static_assert(IPW >= 1, "stage wider than a wavefront");
 };
 
-// per-instance scratch, stage-major: stage k owns one block of BLK elements holding, for every
-// lane r of the instance, the element arrays (z, lambda_l, lambda_u, dz_aff, dz, G yref, g) and
-// the x-lane / u-lane stage records; an access is (lane offset) + k BLK (one SGPR) + a
-// compile-time immediate
+// Scratch, wave-interleaved and stage-major: a wavefront owns (N+1) stage blocks of NW words
+// x LW lanes (LW = IPW * NZ, the lanes that carry an instance: 51 for quad13); word w of stage
+// k for lane l sits at (k NW + w) LW + l. Every access of a wavefront is one contiguous run of
+// LW elements (408 B for quad13 fp64) instead of one partial-line segment per instance, and
+// consecutive words share their boundary cache lines; the idle lanes of a wavefront address
+// beyond the buffer (no memory traffic). Words: the element arrays (z, lambda_l, lambda_u,
+// dz_aff, dz, G yref, g) of component r, then the stage record of the lane (x-lane r: K(:, r),
+// Pr_r, re_r; u-lane u: kff_u, F_uu^{-1}(u, :)).
 template <int NX, int NU>
 struct Layout {
-    static constexpr int NZ = NX + NU;
-    static constexpr int Z = 0, LL = NZ, LU = 2 * NZ, DZA = 3 * NZ, DZ = 4 * NZ, GC = 5 * NZ, GF = 6 * NZ;
-    static constexpr int XREC = 7 * NZ;                       // [XW][NX]
-    static constexpr int UREC = XREC + (NU + 2) * NX;         // [UW][NU]
-    static constexpr int BLK = UREC + (1 + NU) * NU;
-    __host__ __device__ static size_t slot(int N) { return ((size_t)(N + 1) * BLK + 31) & ~size_t(31); }
+    static constexpr int LW = (64 / (NX + NU)) * (NX + NU);
+    static constexpr int Z = 0, LL = 1, LU = 2, DZA = 3, DZ = 4, GC = 5, GF = 6, REC = 7;
+    static constexpr int RECW = (NU + 2) > (1 + NU) ? (NU + 2) : (1 + NU);
+    static constexpr int NW = REC + RECW;
+    __host__ __device__ static size_t wave_elems(int N) { return ((size_t)(N + 1) * NW * LW + 15) & ~size_t(15); }
 };
 
 template <typename T, int NX, int NU, int WPB>
@@ -52,7 +55,7 @@ inline size_t scratch_elems(int B, int N)
     using Gm = Geom<T, NX, NU, WPB>;
     const size_t waves = (size_t)(B + Gm::IPW - 1) / Gm::IPW;
     const size_t blocks = (waves + WPB - 1) / WPB;
-    return blocks * WPB * Gm::VS * Layout<NX, NU>::slot(N);
+    return blocks * WPB * Layout<NX, NU>::wave_elems(N);
 }
 
 }  // namespace lpc
