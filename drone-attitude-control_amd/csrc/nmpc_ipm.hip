@@ -968,7 +968,7 @@ template <typename T, int NX, int NU, int WPB, int MW, class SP = lpc::DenseStru
 static constexpr IpmEntry<T> entry_lpc()
 {
     return IpmEntry<T>{1, NX, NU, lpc::Geom<T, NX, NU, WPB>::IPW, WPB, MW, &launch_ipm_lpc<T, NX, NU, WPB, MW, SP>,
-                       (int)(sizeof(T) * lpc::Geom<T, NX, NU, WPB>::LDS_ELEMS), &lpc::scratch_elems<T, NX, NU, WPB>,
+                       (int)(sizeof(T) * lpc::Geom<T, NX, NU, WPB>::LDS_ELEMS), &lpc::scratch_elems<T, NX, NU, WPB, SP::hdiag>,
                        SP::id, SP::id ? &lpc::structure_fits<SP, NX, NU> : nullptr};
 }
 

@@ -189,7 +189,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     constexpr int NZ = Gm::NZ, IPW = Gm::IPW, VS = Gm::VS, LDZ = Gm::LDZ, LDX = Gm::LDX, LDU = Gm::LDU;
     constexpr int NUT = NU * (NU + 1) / 2;
     constexpr int PD = NMPC_LPC_PF;
-    constexpr int XW = Gm::XW, XPR = Gm::XPR, XRE = Gm::XRE, UW = Gm::UW, UKFF = Gm::UKFF, UFI = Gm::UFI;
+    constexpr int XPR = Gm::XPR, UKFF = Gm::UKFF, UFI = Gm::UFI;
 
     __shared__ __attribute__((aligned(16))) T lds[Gm::LDS_ELEMS];
     T *abr = lds + Gm::C_ABR, *abt = lds + Gm::C_ABT, *hm = lds + Gm::C_H, *hem = lds + Gm::C_HE;
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     auto UB = [&](int k) { return cub[(k == 0 ? 0 : (k == N ? 2 : 1)) * LDZ]; };
 
     // ---- scratch: VS instance slots per wavefront, lane-owned elements
-    using L = Layout<NX, NU>;
+    using L = Layout<NX, NU, SP::hdiag>;
     Buf<T> S;
     S.r = __builtin_amdgcn_make_buffer_rsrc(p.scratch + wg * L::wave_elems(N), 0, (int)(L::wave_elems(N) * sizeof(T)),
                                             0x00020000);
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         };
         struct Rec {
             El e;
-            T c0, kq[NU];   // x-lane: re_k(r), K_k(:, r); u-lane: kff_k(u)
+            T c0, kq[NU];   // x-lane: K_k(:, r); u-lane: kff_k(u)
         };
         auto fetch = [&](int k, Rec &q) {
             k = k < N ? k : N;
@@ -447,7 +447,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             q.e.lu = ldE(L::LU, k);
             if (corr) q.e.dza = ldE(L::DZA, k);
             if (xl) {
-                q.c0 = ldX(kk, XRE);
 #pragma unroll
                 for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
             } else {
@@ -456,7 +455,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         };
         const int dst = corr ? L::DZ : L::DZA;
         T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
-        T dx = 0;
+        // dx_{k+1}(r) = c_r + [A B](r, :) (z_k + dz_k) - z_{k+1}(r): the dynamics residual is
+        // folded in, so the sweep carries xt = dx_{k+1} + z_{k+1} and subtracts z_{k+1} when
+        // stage k+1's iterate has arrived
+        T xt = 0;
         // stage records in flight PD stages ahead (ring slot j holds stage k = j mod PD; the
         // stage loop is unrolled by PD so every slot is a fixed register set)
         Rec ring[PD];
@@ -470,10 +472,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_FTICK(2);
                 const Rec q = ring[j];
                 fetch(k + PD, ring[j]);
+                const T dx = k == 0 ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
                 if (xl) {
 #pragma unroll
                     for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
-                    zb[r] = dx;
+                    zb[r] = q.e.z + dx;
                 }
                 LPC_SYNC();
                 LPC_FTICK(0);
@@ -487,20 +490,20 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     }
                     if (NX % 2) s0 += part[(NX - 1) * LDU + u];
                     du = s0 + s1;
-                    zb[r] = du;
+                    zb[r] = q.e.z + du;
                 }
                 LPC_SYNC();
                 LPC_FTICK(3);
                 const T my = xl ? dx : du;
                 if (xl) {
-                    T s0 = q.c0, s1 = 0;
+                    T s0 = c_r, s1 = 0;
 #pragma unroll
                     for (int jj = 0; jj + 1 < NZ; jj += 2) {
                         s0 = fma(arow[jj], zb[jj], s0);
                         s1 = fma(arow[jj + 1], zb[jj + 1], s1);
                     }
                     if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
-                    dx = s0 + s1;
+                    xt = s0 + s1;
                 }
                 LPC_FTICK(4);
                 stE(dst, k, my);
@@ -515,6 +518,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             e.ll = ldE(L::LL, N);
             e.lu = ldE(L::LU, N);
             if (corr) e.dza = ldE(L::DZA, N);
+            const T dx = xt - e.z;
             stE(dst, N, dx);
             stats(N, dx, e);
         }
@@ -615,7 +619,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if (NZ % 2) s0 = fma(abr[r * LDZ + NZ - 1], zb[NZ - 1], s0);
                     re = s0 + s1;
                     rb[r] = re;
-                    stX(k, XRE, re);
                 }
                 znext = q.z;
                 LPC_SYNC();

@@ -26,9 +26,8 @@ struct Geom {
     static constexpr int G_ZB = 0, G_RB = G_ZB + LDZ, G_VB = G_RB + LDX, G_HU = G_VB + LDX, G_FU = G_HU + LDU,
                          G_MT = G_FU + rup(NU * NU), MTW = cmax(NZ * LDX, NX * LDU), G_TOT = G_MT + MTW;
     static constexpr int LDS_ELEMS = C_TOT + WPB * VS * G_TOT;
-    // per-instance scratch records: x-lane j: K(:, j), Pr_j, re_j; u-lane u: kff_u, F_uu^{-1}(u, :)
-    static constexpr int XW = NU + 2, XPR = NU, XRE = NU + 1;
-    static constexpr int UW = 1 + NU, UKFF = 0, UFI = 1;
+    static constexpr int XPR = NU;        // x record: K(:, r) in words 0..NU-1, Pr_r in word NU
+    static constexpr int UKFF = 0, UFI = 1;   // u record: kff_u, F_uu^{-1}(u, :) in words 1..NU
     static_assert(IPW >= 1, "stage wider than a wavefront");
 };
 
@@ -38,24 +37,25 @@ struct Geom {
 // LW elements (408 B for quad13 fp64) instead of one partial-line segment per instance, and
 // consecutive words share their boundary cache lines; the idle lanes of a wavefront address
 // beyond the buffer (no memory traffic). Words: the element arrays (z, lambda_l, lambda_u,
-// dz_aff, dz, G yref, g) of component r, then the stage record of the lane (x-lane r: K(:, r),
-// Pr_r, re_r; u-lane u: kff_u, F_uu^{-1}(u, :)).
-template <int NX, int NU>
+// dz_aff, dz, G yref and, for non-diagonal costs, g) of component r, then the stage record of
+// the lane (x-lane r: K(:, r), Pr_r; u-lane u: kff_u, F_uu^{-1}(u, :)). The dynamics residual
+// is recomputed by the forward sweeps from z (no record word).
+template <int NX, int NU, bool HDIAG = false>
 struct Layout {
     static constexpr int LW = (64 / (NX + NU)) * (NX + NU);
-    static constexpr int Z = 0, LL = 1, LU = 2, DZA = 3, DZ = 4, GC = 5, GF = 6, REC = 7;
-    static constexpr int RECW = (NU + 2) > (1 + NU) ? (NU + 2) : (1 + NU);
+    static constexpr int Z = 0, LL = 1, LU = 2, DZA = 3, DZ = 4, GC = 5, GF = HDIAG ? -1 : 6, REC = HDIAG ? 6 : 7;
+    static constexpr int RECW = NU + 1;
     static constexpr int NW = REC + RECW;
     __host__ __device__ static size_t wave_elems(int N) { return ((size_t)(N + 1) * NW * LW + 15) & ~size_t(15); }
 };
 
-template <typename T, int NX, int NU, int WPB>
+template <typename T, int NX, int NU, int WPB, bool HDIAG>
 inline size_t scratch_elems(int B, int N)
 {
     using Gm = Geom<T, NX, NU, WPB>;
     const size_t waves = (size_t)(B + Gm::IPW - 1) / Gm::IPW;
     const size_t blocks = (waves + WPB - 1) / WPB;
-    return blocks * WPB * Layout<NX, NU>::wave_elems(N);
+    return blocks * WPB * Layout<NX, NU, HDIAG>::wave_elems(N);
 }
 
 }  // namespace lpc
