@@ -118,8 +118,8 @@ __device__ __forceinline__ T gred(T v, int lane, int r, Op op)
 // Stream the rows of a wave-uniform NR x NC matrix (constant address space) through SGPRs in
 // chunks of RPC rows, one chunk ahead of its use: body(l, row) consumes row l while the next
 // chunk is in flight. Only entries the structure SP allows are loaded (the rest read as 0 and
-// the bodies skip them). The scheduling barriers keep the compiler from hoisting every
-// chunk's s_load at once (which would exhaust the SGPR file and spill to VGPR lanes).
+// the bodies skip them). The loads are inline-asm s_loads (not rematerialisable) followed by
+// one explicit lgkmcnt(0) wait per chunk; the scheduling barriers keep the chunks in order.
 template <int NR, int NC, int RPC, class SP, typename T, typename Body>
 __device__ __forceinline__ void sgpr_rows(cptr<T> m, Body body)
 {
@@ -130,10 +130,21 @@ __device__ __forceinline__ void sgpr_rows(cptr<T> m, Body body)
         for (int rr = 0; rr < RPC; rr++) {
             const int l = ch * RPC + rr;
 #pragma unroll
-            for (int c = 0; c < NC; c++) dst[rr][c] = (l < NR && SP::ab(l, c)) ? m[l * NC + c] : T(0);
+            for (int c = 0; c < NC; c++) {
+                if (l < NR && SP::ab(l, c)) {
+                    if constexpr (sizeof(T) == 8) {
+                        asm volatile("s_load_dwordx2 %0, %1, %2" : "=s"(dst[rr][c]) : "s"(m), "i"((l * NC + c) * 8));
+                    } else {
+                        asm volatile("s_load_dword %0, %1, %2" : "=s"(dst[rr][c]) : "s"(m), "i"((l * NC + c) * 4));
+                    }
+                } else {
+                    dst[rr][c] = T(0);
+                }
+            }
         }
     };
     load(0, cur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
         if (ch + 1 < NCH) load(ch + 1, nxt);
@@ -142,10 +153,13 @@ __device__ __forceinline__ void sgpr_rows(cptr<T> m, Body body)
         for (int rr = 0; rr < RPC; rr++)
             if (ch * RPC + rr < NR) body(ch * RPC + rr, cur[rr]);
         __builtin_amdgcn_sched_barrier(0);
+        if (ch + 1 < NCH) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int rr = 0; rr < RPC; rr++)
+            for (int rr = 0; rr < RPC; rr++)
 #pragma unroll
-            for (int c = 0; c < NC; c++) cur[rr][c] = nxt[rr][c];
+                for (int c = 0; c < NC; c++) cur[rr][c] = nxt[rr][c];
+        }
     }
 }
 
@@ -184,7 +198,14 @@ template <typename T, int NX, int NU, int WPB, int MW, class SP>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8))) void ipm_lpc_kernel(IpmParams<T> p)
 {
     // rows of [A B] per SGPR chunk: ~16 loaded elements per chunk
-    constexpr int RPC = SP::max_row_nnz >= 16 ? 1 : (16 / SP::max_row_nnz < NX ? 16 / SP::max_row_nnz : NX);
+#ifndef NMPC_LPC_RPC_SPARSE
+#define NMPC_LPC_RPC_SPARSE 16
+#endif
+    // structured kernels: ~NMPC_LPC_RPC_SPARSE nonzeros per chunk (all of [A B] in one chunk when it
+    // is that sparse); dense kernels: one 17-wide row per chunk
+    constexpr int RPC = SP::id == 0 ? 1
+                                    : (NMPC_LPC_RPC_SPARSE / SP::max_row_nnz < 1 ? 1
+                                       : (NMPC_LPC_RPC_SPARSE / SP::max_row_nnz < NX ? NMPC_LPC_RPC_SPARSE / SP::max_row_nnz : NX));
     using Gm = Geom<T, NX, NU, WPB>;
     constexpr int NZ = Gm::NZ, IPW = Gm::IPW, VS = Gm::VS, LDZ = Gm::LDZ, LDX = Gm::LDX, LDU = Gm::LDU;
     constexpr int NUT = NU * (NU + 1) / 2;
@@ -446,12 +467,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             q.e.ll = ldE(L::LL, k);
             q.e.lu = ldE(L::LU, k);
             if (corr) q.e.dza = ldE(L::DZA, k);
-            if (xl) {
+            // every lane loads the same record words (x: K(:, r); u: word 0 = kff) — loads in
+            // divergent arms get merged with a divergent offset (waterfall + private array)
 #pragma unroll
-                for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
-            } else {
-                q.c0 = ldU(kk, UKFF);
-            }
+            for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
+            q.c0 = q.kq[UKFF];
         };
         const int dst = corr ? L::DZ : L::DZA;
         T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
@@ -557,10 +577,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 e.ll = ldE(L::LL, k);
                 e.lu = ldE(L::LU, k);
                 e.g = ldE(L::GC, k);
-                if (pending) {
-                    e.dz = ldE(L::DZ, k);
-                    e.dza = ldE(L::DZA, k);
-                }
+                e.dz = ldE(L::DZ, k);     // unconditional: a divergent load arm costs more than
+                e.dza = ldE(L::DZA, k);   // the bytes (first iteration: unused stale words)
             };
             // terminal stage: P_N = He + Sigma_N, p_N = g_N
             fetchA(N, q);
@@ -822,14 +840,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 q.e.dza = ldE(L::DZA, k);
                 q.e.g = ldE(SP::hdiag ? L::GC : L::GF, k);   // diagonal costs: g = G yref + H_rr z below
                 const int kk = k < N ? k : N - 1;
-                if (xl) {
-                    q.pr = ldX(kk, XPR);
+                // same words for every lane (see fetch of the forward sweeps): x-lane K(:, r) and
+                // Pr_r in words 0..NU, u-lane F_uu^{-1}(u, :) in words 1..NU
+                T w[NU + 1];
 #pragma unroll
-                    for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
-                } else {
+                for (int i = 0; i <= NU; i++) w[i] = ldX(kk, i);
+                q.pr = w[XPR];
 #pragma unroll
-                    for (int i = 0; i < NU; i++) q.kq[i] = ldU(kk, UFI + i);
-                }
+                for (int i = 0; i < NU; i++) q.kq[i] = xl ? w[i] : w[UFI + i];
             };
             const T *acol = abt + r * LDX;   // column r of [A B] (LDS, read per stage)
             RecC qN;
