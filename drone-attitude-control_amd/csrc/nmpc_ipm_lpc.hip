@@ -38,7 +38,7 @@
 
 // stage records in flight ahead of the vector sweeps B, C, D
 #ifndef NMPC_LPC_PF
-#define NMPC_LPC_PF 1
+#define NMPC_LPC_PF 2
 #endif
 
 namespace nmpc {
@@ -490,8 +490,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 const int k = kb + j;
                 if (k >= N) break;
                 LPC_FTICK(2);
-                const Rec q = ring[j];
-                fetch(k + PD, ring[j]);
+                // the slot is read in place and refilled after its last use: copying it out
+                // first makes the compiler move the refill's registers at the loop back edge,
+                // which waits for those loads and exposes their whole latency
+                Rec &q = ring[j];
                 const T dx = k == 0 ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
                 if (xl) {
 #pragma unroll
@@ -528,6 +530,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_FTICK(4);
                 stE(dst, k, my);
                 stats(k, my, q.e);
+                fetch(k + PD, ring[j]);
                 LPC_SYNC();
                 LPC_FTICK(7);
             }
@@ -861,8 +864,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 for (int j = 0; j < PD; j++) {
                     const int k = N - 1 - kb - j;
                     if (k < 0) break;
-                    const RecC q = ring[j];
-                    fetchC(k - PD, ring[j]);
+                    RecC &q = ring[j];   // read in place, refilled after its last use (see forward)
                     const T gh = ghat(k, q.e);
                     if (xl) vb[r] = q.pr + pv;
                     LPC_SYNC();
@@ -890,6 +892,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         for (int i = 0; i < NU; i++) s_ = fma(q.kq[i], hu[i], s_);
                         pv = s_;
                     }
+                    fetchC(k - PD, ring[j]);
                     LPC_SYNC();
                 }
             }
