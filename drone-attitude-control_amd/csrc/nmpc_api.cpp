@@ -373,8 +373,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
 
     int ipw_req = 0;
     if (const char *e = std::getenv("NMPC_IPW")) ipw_req = std::atoi(e);
-    h->kidx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, -1, &h->ipw, &h->lds, &h->wpb)
-                                     : nmpc::ipm_find<float>(nx, nu, -1, &h->ipw, &h->lds, &h->wpb);
+    h->kidx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, -1, batch, &h->ipw, &h->lds, &h->wpb)
+                                     : nmpc::ipm_find<float>(nx, nu, -1, batch, &h->ipw, &h->lds, &h->wpb);
     if (h->kidx < 0) {
         std::string msg = "nmpc_create: no compiled kernel for nx=" + std::to_string(nx) + " nu=" + std::to_string(nu);
         delete h;
@@ -386,8 +386,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         int cand[4] = {8, 4, 2, 1}, chosen = -1;
         for (int ipw : cand) {
             int ip, ld;
-            const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw, &ip, &ld, nullptr)
-                                                   : nmpc::ipm_find<float>(nx, nu, ipw, &ip, &ld, nullptr);
+            const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw, batch, &ip, &ld, nullptr)
+                                                   : nmpc::ipm_find<float>(nx, nu, ipw, batch, &ip, &ld, nullptr);
             if (idx < 0) continue;
             if (chosen < 0) chosen = ipw;  // widest compiled
             if ((batch + ipw - 1) / ipw >= 2048) {
@@ -399,8 +399,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         ipw_req = chosen;
     }
     {
-        const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw_req, &h->ipw, &h->lds, &h->wpb)
-                                               : nmpc::ipm_find<float>(nx, nu, ipw_req, &h->ipw, &h->lds, &h->wpb);
+        const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw_req, batch, &h->ipw, &h->lds, &h->wpb)
+                                               : nmpc::ipm_find<float>(nx, nu, ipw_req, batch, &h->ipw, &h->lds, &h->wpb);
         if (idx >= 0) h->kidx = idx;
     }
 

@@ -41,7 +41,7 @@ size_t scratch_elems_per_instance(int N, int nx, int nu);
 // static LDS bytes per workgroup and the wavefronts per workgroup. ipw_req <= 0 picks the
 // widest packing compiled. Scratch must cover ceil(B / (ipw*wpb)) * ipw * wpb instances.
 template <typename T>
-int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_out);
+int ipm_find(int nx, int nu, int ipw_req, int batch, int *ipw_out, int *lds_out, int *wpb_out);
 template <typename T>
 hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s);
 // scratch elements (of T) the kernel `idx` needs for a batch of B instances, horizon N

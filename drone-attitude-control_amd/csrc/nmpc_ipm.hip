@@ -995,21 +995,28 @@ static const IpmEntry<T> *table(int *n)
     return t;
 }
 
-// kernel family: lane-per-component (ipm_lpc_kernel) by default wherever one is compiled for
-// (nx, nu); NMPC_KERNEL=wave selects the wavefront-per-instance kernels (ipm_kernel)
-static int kernel_kind()
+// kernel family: NMPC_KERNEL=lpc / =wave forces one; by default the lane-per-component
+// kernels (ipm_lpc_kernel) run when the stage is wide (nx + nu >= 12: quad13) or the batch fills
+// at least 768 wavefronts, else the wavefront-per-instance ones — for small models at small
+// batches their per-instance latency floor is lower (tools/family_sweep.sh: force N=20 B=1024
+// 0.97 vs 1.34 ms, jerk N=40 B=4096 1.17 vs 1.24 ms; force B=8192 fp32 1.24 vs 1.04 ms)
+static int kernel_kind(int nx, int nu, int batch)
 {
     const char *k = getenv("NMPC_KERNEL");
     if (k && (k[0] == 'w' || k[0] == 'W')) return 0;
-    return 1;
+    if (k && (k[0] == 'l' || k[0] == 'L')) return 1;
+    const int nz = nx + nu;
+    if (nz > 64) return 0;
+    const long waves = ((long)batch + 64 / nz - 1) / (64 / nz);
+    return (nz >= 12 || waves >= 768) ? 1 : 0;
 }
 
 template <typename T>
-int ipm_find(int nx, int nu, int ipw_req, int *ipw_out, int *lds_out, int *wpb_out)
+int ipm_find(int nx, int nu, int ipw_req, int batch, int *ipw_out, int *lds_out, int *wpb_out)
 {
     int n;
     const IpmEntry<T> *t = table<T>(&n);
-    const int kind = kernel_kind();
+    const int kind = kernel_kind(nx, nu, batch);
     int best = -1;
     // NMPC_VARIANT=k picks the k-th compiled kernel of this (nx, nu) and family (tuning runs)
     const char *var = getenv("NMPC_VARIANT");
@@ -1105,8 +1112,8 @@ template int ipm_kind<double>(int);
 template int ipm_kind<float>(int);
 template size_t ipm_scratch_elems<double>(int, int, int);
 template size_t ipm_scratch_elems<float>(int, int, int);
-template int ipm_find<double>(int, int, int, int *, int *, int *);
-template int ipm_find<float>(int, int, int, int *, int *, int *);
+template int ipm_find<double>(int, int, int, int, int *, int *, int *);
+template int ipm_find<float>(int, int, int, int, int *, int *, int *);
 template hipError_t ipm_launch<double>(int, const IpmParams<double> &, hipStream_t);
 template hipError_t ipm_launch<float>(int, const IpmParams<float> &, hipStream_t);
 

@@ -108,16 +108,29 @@ def test_kernel_families_agree(key, precision, cases):
 
 @pytest.mark.parametrize("key", KEYS)
 def test_structure_specialised_matches_dense(key, cases):
-    """The model-structure-specialised kernel (chosen by default: every shipped model fits its
-    compiled [A B] mask and diagonal cost) and the dense one agree to rounding."""
-    a, sa = solve_batch(key, cases)
-    b, sb = solve_batch(key, cases, structure=False)
+    """The model-structure-specialised lane-per-component kernel (chosen whenever that family
+    runs: every shipped model fits its compiled [A B] mask and diagonal cost) and the dense one
+    agree to rounding."""
+    a, sa = solve_batch(key, cases, kernel="lpc")
+    b, sb = solve_batch(key, cases, kernel="lpc", structure=False)
     assert a.launch_info()["structure"] == split(key)[0]
     assert b.launch_info()["structure"] == "dense"
     assert sa == 0 and sb == 0
     for f in ("x", "u"):
         A, B = a.get_batch(f), b.get_batch(f)
         assert np.abs(A - B).max() <= 1e-9 * max(1.0, np.abs(B).max())
+
+
+def test_default_family_is_batch_aware(cases):
+    """quad13 always runs lane-per-component; the small force model switches to it only when
+    the batch fills enough wavefronts (nmpc_ipm.hip kernel_kind)."""
+    key = "force_N20"
+    s, _ = solve_batch(key, cases)
+    assert s.launch_info()["kernel"] == "ipm_kernel"
+    s, _ = solve_batch(key, cases, reps=8192 // cases[key + "_x0"].shape[0] + 1)
+    assert s.launch_info()["kernel"] == "ipm_lpc_kernel"
+    s, _ = solve_batch("quad13_N20", cases)
+    assert s.launch_info()["kernel"] == "ipm_lpc_kernel"
 
 
 def test_ragged_batch(cases):
