@@ -81,6 +81,10 @@ __device__ __forceinline__ float frcp(float x)
     return fmaf(fmaf(-x, r, 1.0f), r, r);
 }
 
+// hardware reciprocal estimate without refinement (step-length heuristics only)
+__device__ __forceinline__ double rcp_raw(double x) { return __builtin_amdgcn_rcp(x); }
+__device__ __forceinline__ float rcp_raw(float x) { return __builtin_amdgcn_rcpf(x); }
+
 __host__ __device__ constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
 // x <- F_uu^{-1} x with the packed Cholesky factor (inverse diagonal)
@@ -347,28 +351,28 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         T z, ll, lu, dz, dza, g;
     };
     // lazily apply the pending step of the previous iteration to element (k, r)
+    // lazily apply the pending step of the previous iteration to element (k, r); the arithmetic
+    // is branch-free (selects), the write-back a write-only divergent block
     auto lazy = [&](int k, El &q) {
-        if (pending && (k < N || xl)) {
-            const T lb = LB(k), ub = UB(k);
-            if (q.ll > T(0)) {
-                const T t = q.z - lb, it_ = frcp(t), dla = -q.ll * (T(1) + q.dza * it_);
-                q.ll += alpha * ((smu - q.ll * t - dla * q.dza - q.ll * q.dz) * it_);
-            }
-            if (q.lu > T(0)) {
-                const T t = ub - q.z, it_ = frcp(t), dla = -q.lu * (T(1) - q.dza * it_);
-                q.lu += alpha * ((smu - q.lu * t + dla * q.dza + q.lu * q.dz) * it_);
-            }
-            q.z += alpha * q.dz;
+        const bool upd = pending && (k < N || xl);
+        const T lb = LB(k), ub = UB(k);
+        const bool vl = q.ll > T(0), vu = q.lu > T(0);
+        const T tl = q.z - lb, tu = ub - q.z, itl = frcp(tl), itu = frcp(tu);
+        const T dlal = -q.ll * (T(1) + q.dza * itl), dlau = -q.lu * (T(1) - q.dza * itu);
+        const T nl = q.ll + alpha * ((smu - q.ll * tl - dlal * q.dza - q.ll * q.dz) * itl);
+        const T nu_ = q.lu + alpha * ((smu - q.lu * tu + dlau * q.dza + q.lu * q.dz) * itu);
+        q.ll = (upd && vl) ? nl : q.ll;
+        q.lu = (upd && vu) ? nu_ : q.lu;
+        q.z = upd ? q.z + alpha * q.dz : q.z;
+        if (upd) {
             stE(L::Z, k, q.z);
             stE(L::LL, k, q.ll);
             stE(L::LU, k, q.lu);
         }
     };
     auto sigma = [&](int k, const El &q) {
-        T sg = 0;
-        if (q.ll > T(0)) sg += q.ll * frcp(q.z - LB(k));
-        if (q.lu > T(0)) sg += q.lu * frcp(UB(k) - q.z);
-        return sg;
+        const T sl = q.ll * frcp(q.z - LB(k)), su = q.lu * frcp(UB(k) - q.z);
+        return (q.ll > T(0) ? sl : T(0)) + (q.lu > T(0) ? su : T(0));
     };
 
     // ---- forward recursion (B: predictor into dza with ratio test / centring sums;
@@ -413,48 +417,40 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         const T *arow = abr + (xl ? r : 0) * LDZ;   // row r of [A B] (LDS, read per stage)
         s_min = 1;
         s_a = s_b = s_c = 0;
+        // ratio tests and closed-form mu sums of element (k, r), branch-free (selects instead of
+        // divergent arms). The predictor's quantities only steer the step length (safety factor
+        // 0.995) and sigma, so they use the raw hardware reciprocal; the corrector's dual step
+        // feeds mu_new (termination) and keeps the refined one.
         auto stats = [&](int k, T dz, const El &q) {
             const T lb = LB(k), ub = UB(k);
+            const bool vl = q.ll > T(0), vu = q.lu > T(0);
+            const T tl = q.z - lb, tu = ub - q.z;
+            const T rdz = rcp_raw(dz);
+            T c = 1;
             if (!corr) {
-                if (q.ll > T(0)) {
-                    const T t = q.z - lb, it_ = frcp(t);
-                    const T dl = -q.ll * (T(1) + dz * it_);
-                    if (dz < T(0)) s_min = fmin(s_min, -t * frcp(dz));
-                    if (dl < T(0)) s_min = fmin(s_min, -q.ll * frcp(dl));
-                    s_a += q.ll * t;
-                    s_b += q.ll * dz * (t + dz) * it_;
-                }
-                if (q.lu > T(0)) {
-                    const T t = ub - q.z, it_ = frcp(t);
-                    const T dl = -q.lu * (T(1) - dz * it_);
-                    if (dz > T(0)) s_min = fmin(s_min, t * frcp(dz));
-                    if (dl < T(0)) s_min = fmin(s_min, -q.lu * frcp(dl));
-                    s_a += q.lu * t;
-                    s_b += q.lu * dz * (dz - t) * it_;
-                }
+                const T itl = rcp_raw(tl), itu = rcp_raw(tu);
+                const T dll = -q.ll * (T(1) + dz * itl), dlu = -q.lu * (T(1) - dz * itu);
+                c = (vl && dz < T(0)) ? fmin(c, -tl * rdz) : c;
+                c = (vl && dll < T(0)) ? fmin(c, -q.ll * rcp_raw(dll)) : c;
+                c = (vu && dz > T(0)) ? fmin(c, tu * rdz) : c;
+                c = (vu && dlu < T(0)) ? fmin(c, -q.lu * rcp_raw(dlu)) : c;
+                s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
+                s_b += (vl ? q.ll * dz * (tl + dz) * itl : T(0)) + (vu ? q.lu * dz * (dz - tu) * itu : T(0));
             } else {
                 const T dza = q.dza;
-                if (q.ll > T(0)) {
-                    const T t = q.z - lb, it_ = frcp(t);
-                    const T dla = -q.ll * (T(1) + dza * it_);
-                    const T dl = (smu - q.ll * t - dla * dza - q.ll * dz) * it_;
-                    if (dz < T(0)) s_min = fmin(s_min, -t * frcp(dz));
-                    if (dl < T(0)) s_min = fmin(s_min, -q.ll * frcp(dl));
-                    s_a += q.ll * t;
-                    s_b += dla * dza;
-                    s_c += dl * dz;
-                }
-                if (q.lu > T(0)) {
-                    const T t = ub - q.z, it_ = frcp(t);
-                    const T dla = -q.lu * (T(1) - dza * it_);
-                    const T dl = (smu - q.lu * t + dla * dza + q.lu * dz) * it_;
-                    if (dz > T(0)) s_min = fmin(s_min, t * frcp(dz));
-                    if (dl < T(0)) s_min = fmin(s_min, -q.lu * frcp(dl));
-                    s_a += q.lu * t;
-                    s_b -= dla * dza;
-                    s_c -= dl * dz;
-                }
+                const T itl = frcp(tl), itu = frcp(tu);
+                const T dlal = -q.ll * (T(1) + dza * itl), dlau = -q.lu * (T(1) - dza * itu);
+                const T dll = (smu - q.ll * tl - dlal * dza - q.ll * dz) * itl;
+                const T dlu = (smu - q.lu * tu + dlau * dza + q.lu * dz) * itu;
+                c = (vl && dz < T(0)) ? fmin(c, -tl * rdz) : c;
+                c = (vl && dll < T(0)) ? fmin(c, -q.ll * rcp_raw(dll)) : c;
+                c = (vu && dz > T(0)) ? fmin(c, tu * rdz) : c;
+                c = (vu && dlu < T(0)) ? fmin(c, -q.lu * rcp_raw(dlu)) : c;
+                s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
+                s_b += (vl ? dlal * dza : T(0)) - (vu ? dlau * dza : T(0));
+                s_c += (vl ? dll * dz : T(0)) - (vu ? dlu * dz : T(0));
             }
+            s_min = fmin(s_min, c);
         };
         struct Rec {
             El e;
@@ -494,30 +490,33 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 // first makes the compiler move the refill's registers at the loop back edge,
                 // which waits for those loads and exposes their whole latency
                 Rec &q = ring[j];
-                const T dx = k == 0 ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
-                if (xl) {
+                const T dx = (k == 0 || !xl) ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
+                if (xl) {   // write-only divergent block
 #pragma unroll
                     for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
                     zb[r] = q.e.z + dx;
                 }
                 LPC_SYNC();
                 LPC_FTICK(0);
-                T du = 0;
-                if (ul) {
+                // u-lanes: du_u = kff_u + sum_j K(u, j) dx_j; every lane runs the same straight-line
+                // code (x-lanes sum column 0 and discard it)
+                T du;
+                {
+                    const int uu = ul ? u : 0;
                     T s0 = q.c0, s1 = 0;
 #pragma unroll
                     for (int jj = 0; jj + 1 < NX; jj += 2) {
-                        s0 += part[jj * LDU + u];
-                        s1 += part[(jj + 1) * LDU + u];
+                        s0 += part[jj * LDU + uu];
+                        s1 += part[(jj + 1) * LDU + uu];
                     }
-                    if (NX % 2) s0 += part[(NX - 1) * LDU + u];
-                    du = s0 + s1;
-                    zb[r] = q.e.z + du;
+                    if (NX % 2) s0 += part[(NX - 1) * LDU + uu];
+                    du = ul ? s0 + s1 : T(0);
                 }
+                if (ul) zb[r] = q.e.z + du;
                 LPC_SYNC();
                 LPC_FTICK(3);
                 const T my = xl ? dx : du;
-                if (xl) {
+                {
                     T s0 = c_r, s1 = 0;
 #pragma unroll
                     for (int jj = 0; jj + 1 < NZ; jj += 2) {
@@ -525,7 +524,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         s1 = fma(arow[jj + 1], zb[jj + 1], s1);
                     }
                     if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
-                    xt = s0 + s1;
+                    xt = xl ? s0 + s1 : xt;
                 }
                 LPC_FTICK(4);
                 stE(dst, k, my);
@@ -820,16 +819,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             auto ghat = [&](int k, const El &e) {
                 T g = e.g;
                 if (SP::hdiag) g = fma(k < N ? hm[r * LDZ + r] : hem[(xl ? r : 0) * LDX + (xl ? r : 0)], e.z, g);
-                const T lb = LB(k), ub = UB(k);
-                if (e.ll > T(0)) {
-                    const T t = e.z - lb, it_ = frcp(t), dl = -e.ll * (T(1) + e.dza * it_);
-                    g += (dl * e.dza - smu) * it_;
-                }
-                if (e.lu > T(0)) {
-                    const T t = ub - e.z, it_ = frcp(t), dl = -e.lu * (T(1) - e.dza * it_);
-                    g += (dl * e.dza + smu) * it_;
-                }
-                return g;
+                const T tl = e.z - LB(k), tu = UB(k) - e.z, itl = frcp(tl), itu = frcp(tu);
+                const T dll = -e.ll * (T(1) + e.dza * itl), dlu = -e.lu * (T(1) - e.dza * itu);
+                const T cl = (dll * e.dza - smu) * itl, cu = (dlu * e.dza + smu) * itu;
+                return g + (e.ll > T(0) ? cl : T(0)) + (e.lu > T(0) ? cu : T(0));
             };
             struct RecC {
                 El e;

@@ -116,9 +116,15 @@ def test_structure_specialised_matches_dense(key, cases):
     assert a.launch_info()["structure"] == split(key)[0]
     assert b.launch_info()["structure"] == "dense"
     assert sa == 0 and sb == 0
+    # both follow the same algorithm, but FMA order (sparse vs dense products) perturbs the
+    # step-length heuristics, so the iterate paths agree to the solver tolerance, not bitwise;
+    # 1e-7 is 10x inside the oracle bar each of them meets
     for f in ("x", "u"):
         A, B = a.get_batch(f), b.get_batch(f)
-        assert np.abs(A - B).max() <= 1e-9 * max(1.0, np.abs(B).max())
+        assert np.abs(A - B).max() <= 1e-7 * max(1.0, np.abs(B).max())
+    ea = rel_err(a.get_batch("x"), a.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
+    eb = rel_err(b.get_batch("x"), b.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
+    assert ea.max() < TOL64 and eb.max() < TOL64
 
 
 def test_default_family_is_batch_aware(cases):
