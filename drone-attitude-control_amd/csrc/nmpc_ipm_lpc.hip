@@ -736,55 +736,43 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             lf[tri(i, j)] = s_ * lf[tri(j, j)];
                         }
                     }
-                T y[NU], pnew = 0;
-                // stage record words 0..NU: x-lane r: K(:, r) (Pr_r sits in word NU, stored above);
-                // u-lane u: kff_u, F_uu^{-1}(u, :). Stored after the branch with one store per
-                // word (stores in both arms would be merged with a divergent offset)
-                T rec[NU + 1];
+                // x-lane r: Y(:, r) = L^{-1} F_ux(:, r), K(:, r) = -L^{-T} Y(:, r), p_r = h_r + K(:, r)' h_u;
+                // u-lane u: F_uu^{-1}(u, :) = L^{-T} L^{-1} e_u, kff_u = -F_uu^{-1}(u, :) h_u — the same
+                // two triangular solves on different right-hand sides, run by every lane at once
+                T y[NU], xs[NU], pnew;
+                {
+                    T f[NU];
 #pragma unroll
-                for (int i = 0; i < NU; i++) y[i] = 0;
-                if (xl) {
-                    // Y(:, r) = L^{-1} F_ux(:, r), K(:, r) = -L^{-T} Y(:, r), p_r = h_r + K(:, r)' h_u
+                    for (int i = 0; i < NU; i++) f[i] = xl ? fcol[NX + i] : ((u == i) ? T(1) : T(0));
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
-                        T s_ = fcol[NX + i];
+                        T s_ = f[i];
 #pragma unroll
                         for (int l = 0; l < i; l++) s_ = fma(-lf[tri(i, l)], y[l], s_);
                         y[i] = s_ * lf[tri(i, i)];
                     }
-                    T kc[NU];
 #pragma unroll
                     for (int i = NU - 1; i >= 0; i--) {
                         T s_ = y[i];
 #pragma unroll
-                        for (int l = i + 1; l < NU; l++) s_ = fma(lf[tri(l, i)], -kc[l], s_);
-                        kc[i] = -s_ * lf[tri(i, i)];
+                        for (int l = i + 1; l < NU; l++) s_ = fma(-lf[tri(l, i)], xs[l], s_);
+                        xs[i] = s_ * lf[tri(i, i)];
                     }
-                    pnew = h;
+                    T d = 0;
 #pragma unroll
-                    for (int i = 0; i < NU; i++) {
-                        pnew = fma(kc[i], hu[i], pnew);
-                        ylds[r * LDU + i] = y[i];
-                        rec[i] = kc[i];
-                    }
-                    rec[NU] = 0;
-                } else {
-                    // row u of F_uu^{-1}, kff_u = -(F_uu^{-1} h_u)_u
-                    T e[NU];
-#pragma unroll
-                    for (int i = 0; i < NU; i++) e[i] = (u == i) ? T(1) : T(0);
-                    chol_solve<T, NU>(lf, e);
-                    T kf = 0;
-#pragma unroll
-                    for (int i = 0; i < NU; i++) {
-                        kf = fma(-e[i], hu[i], kf);
-                        rec[UFI + i] = e[i];
-                    }
-                    rec[UKFF] = kf;
+                    for (int i = 0; i < NU; i++) d = fma(xs[i], hu[i], d);
+                    pnew = (xl ? h : T(0)) - d;   // x: p_r; u: kff_u
                 }
+                // stage record words 0..NU: x-lane r: K(:, r) = -xs (Pr_r sits in word NU, stored
+                // above); u-lane u: kff_u, F_uu^{-1}(u, :) = xs
+                if (xl) {   // write-only divergent block
 #pragma unroll
-                for (int i = 0; i < NU; i++) stX(k, i, rec[i]);
-                if (ul) stU(k, NU, rec[NU]);
+                    for (int i = 0; i < NU; i++) ylds[r * LDU + i] = y[i];
+                }
+                stX(k, 0, xl ? -xs[0] : pnew);
+#pragma unroll
+                for (int i = 1; i < NU; i++) stX(k, i, xl ? -xs[i] : xs[i - 1]);
+                if (ul) stU(k, NU, xs[NU - 1]);
                 LPC_SYNC();
                 // P(r, :) = F(r, 0:nx) - Y(:, r)' Y  (+ Sigma_x of stage k on the diagonal); u-lanes
                 // compute a dummy row (keeps the loop-carried registers dead between stages)

@@ -24,7 +24,12 @@ struct Geom {
     // per lane group: stage z / dx broadcast, re, v, h_u, F_uu, M^T (aliased by the rows of
     // Y = L^{-1} F_ux in the factorisation and by the partial products K(u, j) dx_j in the forward sweeps)
     static constexpr int G_ZB = 0, G_RB = G_ZB + LDZ, G_VB = G_RB + LDX, G_HU = G_VB + LDX, G_FU = G_HU + LDU,
-                         G_MT = G_FU + rup(NU * NU), MTW = cmax(NZ * LDX, NX * LDU), G_TOT = G_MT + MTW;
+                         G_MT = G_FU + rup(NU * NU), MTW = cmax(NZ * LDX, NX * LDU), G_RAW = G_MT + MTW;
+    // lane groups start 16 banks apart (mod 64 dword banks): with a 32-bank stride the first and
+    // third instance of a wavefront collided on every per-instance LDS access (PMC: bank
+    // conflicts were ~3/4 of LDS-active cycles)
+    static constexpr int DW = (int)sizeof(T) / 4, GSTEP = 64 / DW;
+    static constexpr int G_TOT = G_RAW + ((16 / DW - G_RAW % GSTEP) % GSTEP + GSTEP) % GSTEP;
     static constexpr int LDS_ELEMS = C_TOT + WPB * VS * G_TOT;
     static constexpr int XPR = NU;        // x record: K(:, r) in words 0..NU-1, Pr_r in word NU
     static constexpr int UKFF = 0, UFI = 1;   // u record: kff_u, F_uu^{-1}(u, :) in words 1..NU
