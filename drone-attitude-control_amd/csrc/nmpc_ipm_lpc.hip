@@ -559,7 +559,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         if (active && (conv || bad)) {
             active = false;
             status = conv && !bad ? 0 : 4;
-            iters = it;
+            iters = fail ? it - 1 : it;   // a failed factorisation ends the iteration it began
         }
         if (active && it >= p.max_iter) {
             active = false;
@@ -885,7 +885,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         forward(true, amax, T0, C1, C2);
         LPC_TICK(6);
         const T a = fmin(T(1), T(0.995) * amax);
-        if (active) {
+        // a failed factorisation (F_uu not positive definite) leaves the iterate as it stood at the
+        // start of this iteration, like the oracle's early exit (oracle/c/riccati_ipm.c:222)
+        if (active && !fail) {
             // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
             mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
             theta *= (T(1) - a);

@@ -256,3 +256,30 @@ def test_plant_simulator_matches_oracle():
             x = rng.normal(size=4)
             u = np.array([rng.normal(0, 0.5), abs(rng.normal(0.3, 0.1))])
             assert np.allclose(ss.simulate(x=x, u=u), ref(x, u, T), rtol=1e-13, atol=1e-15)
+
+
+@pytest.mark.parametrize("kernel", ["lpc", "wave"])
+def test_factorisation_failure_keeps_last_iterate(kernel, cases, golden_dir):
+    """A closed-loop jerk instance pushed past the position bound (tests/golden/qp_failure.npz,
+    make_failure_case.py): x_1 cannot be feasible, F_uu loses positive definiteness at the C
+    oracle's iteration 9 -> status 4 with the iterate from the start of that iteration, finite
+    (no NaN handed to the plant), and the other instances of the launch are unaffected."""
+    f = np.load(os.path.join(golden_dir, "qp_failure.npz"))
+    key = "jerk_N40"
+    x0 = np.vstack([f[key + "_x0"], cases[key + "_x0"][:3]])
+    y = np.vstack([f[key + "_yref"], cases[key + "_yref"][:3]])
+    os.environ["NMPC_KERNEL"] = kernel
+    try:
+        s = AcadosOcpSolver(OCPS["jerk"](40), batch=4)
+    finally:
+        os.environ.pop("NMPC_KERNEL", None)
+    s.set_batch("x0", x0)
+    s.set_batch("yref", y)
+    assert s.solve() == 4
+    status, it = s.get_batch_int("status"), s.get_batch_int("qp_iter")
+    assert list(status) == [4, 0, 0, 0]
+    assert it[0] == int(f[key + "_iters"][0])
+    X, U = s.get_batch("x"), s.get_batch("u")
+    assert np.isfinite(X).all() and np.isfinite(U).all()
+    assert rel_err(X[:1], U[:1], f[key + "_X"], f[key + "_U"]).max() < TOL64
+    assert rel_err(X[1:], U[1:], cases[key + "_X"][:3], cases[key + "_U"][:3]).max() < TOL64

@@ -171,3 +171,15 @@ def test_converters_and_plant():
     exact = np.concatenate([x[:2] + x[2:] * h + 0.5 * acc * h * h, x[2:] + acc * h])
     assert np.allclose(CL.rk4_step(x, uu, h), exact, atol=1e-14)
     assert CL.calc_aed(np.ones((3, 2)), np.zeros((3, 2))) == 1.0
+
+
+def test_factorisation_failure_fixture(golden_dir):
+    """tests/golden/qp_failure.npz: the C oracle still stops with status 4 after the recorded
+    number of iterations and returns the recorded (finite) iterate."""
+    from oracle import cref, models
+    f = np.load(os.path.join(golden_dir, "qp_failure.npz"))
+    R = cref.RiccatiIpmRef(models.MODELS["jerk"](40))
+    X, U, st, it = R.solve(f["jerk_N40_x0"], f["jerk_N40_yref"], nthreads=1)
+    assert st[0] == 4 and it[0] == f["jerk_N40_iters"][0]
+    assert np.isfinite(X).all() and np.isfinite(U).all()
+    assert np.array_equal(X, f["jerk_N40_X"]) and np.array_equal(U, f["jerk_N40_U"])
