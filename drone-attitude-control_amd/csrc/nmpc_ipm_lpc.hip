@@ -167,6 +167,35 @@ __device__ __forceinline__ void sgpr_rows(cptr<T> m, Body body)
     }
 }
 
+// compact row / column of [A B] (structured kernels): values and byte offsets, loaded ahead of
+// the LDS vector they are dotted with (s0 + sum_j v_j vec[o_j])
+template <typename T, int NL>
+struct SpL {
+    T v[NL];
+    int o[NL];
+};
+template <typename T, int NL>
+__device__ __forceinline__ void sp_load(SpL<T, NL> &q, const T *vals, const int *offs, int base)
+{
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        q.v[j] = vals[base + j];
+        q.o[j] = offs[base + j];
+    }
+}
+template <typename T, int NL>
+__device__ __forceinline__ T sp_dot(const SpL<T, NL> &q, const T *vec, T s0)
+{
+    T s1 = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        const T x = *(const T *)((const char *)vec + q.o[j]);
+        if (j & 1) s1 = fma(q.v[j], x, s1);
+        else s0 = fma(q.v[j], x, s0);
+    }
+    return s0 + s1;
+}
+
 template <typename T>
 __device__ __forceinline__ bool has_bound(T b)
 {
@@ -242,6 +271,49 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         lds[Gm::C_LB + (e / NZ) * LDZ + e % NZ] = p.lbnd[e];
         lds[Gm::C_UB + (e / NZ) * LDZ + e % NZ] = p.ubnd[e];
     }
+    // structured kernels: row l and column c of [A B] as compact (value, byte offset) lists for
+    // the per-lane dot products of the sweeps (dynamics residual / forward update: row r of the
+    // x-lane; h = [A B]' v: column r) — quad13: <= 5 / <= 4 terms instead of 17 / 13; padding
+    // entries are (0, 0)
+#ifdef NMPC_LPC_DENSE_SWEEPS
+    constexpr bool SPARSE = false;   // experiment builds: dense rows / columns in the sweeps
+#else
+    constexpr bool SPARSE = SP::id != 0;
+#endif
+    constexpr int RN = SPARSE ? SP::max_row_nnz : 1, CN = SPARSE ? SP::max_col_nnz : 1;
+    __shared__ __attribute__((aligned(16))) T slv[NX * RN + NZ * CN];
+    __shared__ __attribute__((aligned(16))) int sli[NX * RN + NZ * CN];
+    if constexpr (SPARSE) {
+        const int t = threadIdx.x;
+        if (t < NX) {
+            int n = 0;
+#pragma unroll
+            for (int c = 0; c < NZ; c++)
+                if (SP::ab(t, c)) {
+                    slv[t * RN + n] = p.AB[t * NZ + c];
+                    sli[t * RN + n] = c * (int)sizeof(T);
+                    n++;
+                }
+            for (; n < RN; n++) {
+                slv[t * RN + n] = T(0);
+                sli[t * RN + n] = 0;
+            }
+        } else if (t < NX + NZ) {
+            const int c = t - NX, base = NX * RN + c * CN;
+            int n = 0;
+#pragma unroll
+            for (int l = 0; l < NX; l++)
+                if (SP::ab(l, c)) {
+                    slv[base + n] = p.AB[l * NZ + c];
+                    sli[base + n] = l * (int)sizeof(T);
+                    n++;
+                }
+            for (; n < CN; n++) {
+                slv[base + n] = T(0);
+                sli[base + n] = 0;
+            }
+        }
+    }
     __syncthreads();
     if (!__any(inst_ok)) return;
 
@@ -275,6 +347,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     auto gmin = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return fmin(a, b); }); };
     auto gmax = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return fmax(a, b); }); };
     auto gsum = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return a + b; }); };
+
+    const int row_base = (xl ? r : 0) * RN, col_base = NX * RN + r * CN;
 
     // ------------------------------------------------------------------ initial point
     T r0 = 0, mu = 0, abz = 0;
@@ -480,6 +554,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         Rec ring[PD];
 #pragma unroll
         for (int j = 0; j < PD; j++) fetch(j, ring[j]);
+        SpL<T, RN> arl;
+        if constexpr (SPARSE) sp_load(arl, slv, sli, row_base);
         for (int kb = 0; kb < N; kb += PD) {
 #pragma unroll
             for (int j = 0; j < PD; j++) {
@@ -516,7 +592,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_SYNC();
                 LPC_FTICK(3);
                 const T my = xl ? dx : du;
-                {
+                if constexpr (SPARSE) {
+                    const T s = sp_dot(arl, zb, c_r);
+                    xt = xl ? s : xt;
+                } else {
                     T s0 = c_r, s1 = 0;
 #pragma unroll
                     for (int jj = 0; jj + 1 < NZ; jj += 2) {
@@ -610,6 +689,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_PTICK(1);
                 q = qn;
                 if (k > 0) fetchA(k - 1, qn);
+                SpL<T, RN> arl;
+                SpL<T, CN> acl;
+                if constexpr (SPARSE) {
+                    sp_load(arl, slv, sli, row_base);
+                    sp_load(acl, slv, sli, col_base);
+                }
                 lazy(k, q);
                 const T sg = sigma(k, q);
                 zb[r] = q.z;
@@ -629,7 +714,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     g += g1;
                 }
                 if (!SP::hdiag) stE(L::GF, k, g);
-                if (xl) {
+                if constexpr (SPARSE) {
+                    re = sp_dot(arl, zb, c_r - znext);
+                    if (xl) rb[r] = re;
+                } else if (xl) {
                     T s0 = c_r - znext, s1 = 0;
 #pragma unroll
                     for (int j = 0; j + 1 < NZ; j += 2) {
@@ -676,7 +764,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 // F = [A B]' M + H (column r per lane; + Sigma on the diagonal, applied by the
                 // readers), h = [A B]' v + g
                 T fcol[NZ], h;
-                {
+                if constexpr (SPARSE) {
+                    h = sp_dot(acl, vb, g);
+                } else {
                     T h0 = g, h1 = 0;
 #pragma unroll
                     for (int i = 0; i + 1 < NX; i += 2) {
@@ -840,6 +930,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             RecC ring[PD];
 #pragma unroll
             for (int j = 0; j < PD; j++) fetchC(N - 1 - j, ring[j]);
+            SpL<T, CN> acl;
+            if constexpr (SPARSE) sp_load(acl, slv, sli, col_base);
             for (int kb = 0; kb < N; kb += PD) {
 #pragma unroll
                 for (int j = 0; j < PD; j++) {
@@ -849,14 +941,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     const T gh = ghat(k, q.e);
                     if (xl) vb[r] = q.pr + pv;
                     LPC_SYNC();
-                    T h0 = gh, h1 = 0;
+                    T h;
+                    if constexpr (SPARSE) {
+                        h = sp_dot(acl, vb, gh);
+                    } else {
+                        T h0 = gh, h1 = 0;
 #pragma unroll
-                    for (int i = 0; i + 1 < NX; i += 2) {
-                        h0 = fma(acol[i], vb[i], h0);
-                        h1 = fma(acol[i + 1], vb[i + 1], h1);
+                        for (int i = 0; i + 1 < NX; i += 2) {
+                            h0 = fma(acol[i], vb[i], h0);
+                            h1 = fma(acol[i + 1], vb[i + 1], h1);
+                        }
+                        if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                        h = h0 + h1;
                     }
-                    if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
-                    const T h = h0 + h1;
                     if (ul) hub[u] = h;
                     LPC_SYNC();
                     T hu[NU];

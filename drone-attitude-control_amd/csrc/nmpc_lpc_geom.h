@@ -88,6 +88,7 @@ struct DenseStructure {
     static constexpr bool hdiag = false;
     static constexpr bool ab(int, int) { return true; }
     static constexpr int max_row_nnz = NX + NU;
+    static constexpr int max_col_nnz = NX;
 };
 
 // the mask rows are a template pack (not an array in memory) so that ab(l, c) folds to a
@@ -114,7 +115,18 @@ struct MaskStructure {
         }
         return m;
     }
+    static constexpr int max_col_nnz_()
+    {
+        int m = 0;
+        for (int c = 0; c < NX + NU; c++) {
+            int n = 0;
+            for (int l = 0; l < NX; l++) n += ab(l, c) ? 1 : 0;
+            m = n > m ? n : m;
+        }
+        return m;
+    }
     static constexpr int max_row_nnz = max_nnz();
+    static constexpr int max_col_nnz = max_col_nnz_();
 };
 
 // force_model (force_model/dynamics.py:32-37): x = [px, pz, vx, vz], u = [Fx, Fz]
