@@ -40,6 +40,10 @@
 #ifndef NMPC_LPC_PF
 #define NMPC_LPC_PF 2
 #endif
+// rows of Y = L^{-1} F_ux per LDS chunk in the P update of the Riccati stage
+#ifndef NMPC_LPC_PCH
+#define NMPC_LPC_PCH 2
+#endif
 
 namespace nmpc {
 namespace lpc {
@@ -866,6 +870,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_SYNC();
                 // P(r, :) = F(r, 0:nx) - Y(:, r)' Y  (+ Sigma_x of stage k on the diagonal); u-lanes
                 // compute a dummy row (keeps the loop-carried registers dead between stages)
+                // The rows of Y stream from LDS in chunks of PCH rows, one chunk in flight while
+                // the previous one is consumed: left to itself the scheduler reused one register
+                // quad for all 26 reads, i.e. 26 serialised LDS round trips per stage.
+#if NMPC_LPC_PCH == 0
 #pragma unroll
                 for (int i = 0; i < NX; i++) {
                     T s_ = fcol[i];
@@ -873,6 +881,37 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     for (int a = 0; a < NU; a++) s_ = fma(-ylds[i * LDU + a], y[a], s_);
                     prow[i] = s_;
                 }
+#else
+                {
+                    constexpr int PCH = NMPC_LPC_PCH, NPC = (NX + PCH - 1) / PCH;
+                    T yb[2][PCH][NU];
+                    auto yload = [&](int ch, T (&dst)[PCH][NU]) {
+#pragma unroll
+                        for (int ii = 0; ii < PCH; ii++) {
+                            const int i = ch * PCH + ii;
+#pragma unroll
+                            for (int a = 0; a < NU; a++) dst[ii][a] = i < NX ? ylds[i * LDU + a] : T(0);
+                        }
+                    };
+                    yload(0, yb[0]);
+#pragma unroll
+                    for (int ch = 0; ch < NPC; ch++) {
+                        if (ch + 1 < NPC) yload(ch + 1, yb[(ch + 1) & 1]);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int ii = 0; ii < PCH; ii++) {
+                            const int i = ch * PCH + ii;
+                            if (i < NX) {
+                                T s_ = fcol[i];
+#pragma unroll
+                                for (int a = 0; a < NU; a++) s_ = fma(-yb[ch & 1][ii][a], y[a], s_);
+                                prow[i] = s_;
+                            }
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+#endif
                 sdiag = sg + (SP::hdiag ? hm[r * LDZ + r] : T(0));   // F(r, r) = F_col(r) + H_rr + Sigma
                 pv = pnew;
                 LPC_SYNC();
