@@ -431,9 +431,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // lazily apply the pending step of the previous iteration to element (k, r)
     // lazily apply the pending step of the previous iteration to element (k, r); the arithmetic
     // is branch-free (selects), the write-back a write-only divergent block
-    auto lazy = [&](int k, El &q) {
+    // the bounds of element (k, r) are read once per stage, ahead of their use (B)
+    struct Bd {
+        T lb, ub;
+    };
+    auto bnd = [&](int k) { return Bd{LB(k), UB(k)}; };
+    auto lazy = [&](int k, El &q, const Bd &b) {
         const bool upd = pending && (k < N || xl);
-        const T lb = LB(k), ub = UB(k);
+        const T lb = b.lb, ub = b.ub;
         const bool vl = q.ll > T(0), vu = q.lu > T(0);
         const T tl = q.z - lb, tu = ub - q.z, itl = frcp(tl), itu = frcp(tu);
         const T dlal = -q.ll * (T(1) + q.dza * itl), dlau = -q.lu * (T(1) - q.dza * itu);
@@ -448,8 +453,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             stE(L::LU, k, q.lu);
         }
     };
-    auto sigma = [&](int k, const El &q) {
-        const T sl = q.ll * frcp(q.z - LB(k)), su = q.lu * frcp(UB(k) - q.z);
+    auto sigma = [&](const El &q, const Bd &b) {
+        const T sl = q.ll * frcp(q.z - b.lb), su = q.lu * frcp(b.ub - q.z);
         return (q.ll > T(0) ? sl : T(0)) + (q.lu > T(0) ? su : T(0));
     };
 
@@ -499,22 +504,23 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // divergent arms). The predictor's quantities only steer the step length (safety factor
         // 0.995) and sigma, so they use the raw hardware reciprocal; the corrector's dual step
         // feeds mu_new (termination) and keeps the refined one.
-        auto stats = [&](int k, T dz, const El &q) {
-            const T lb = LB(k), ub = UB(k);
+        auto stats = [&](T dz, const El &q, const Bd &b) {
+            const T lb = b.lb, ub = b.ub;
             const bool vl = q.ll > T(0), vu = q.lu > T(0);
             const T tl = q.z - lb, tu = ub - q.z;
-            const T rdz = rcp_raw(dz);
             T c = 1;
             if (!corr) {
+                // predictor: the largest inverse step ratio, division-free — primal -dz/t_l and
+                // dual -dlam_l/lam_l = 1 + dz/t_l (the affine dual step is -lam (1 + dz/t)), and
+                // the mirrored pair for the upper bound; alpha_aff = 1 / max(1, ...) per group
                 const T itl = rcp_raw(tl), itu = rcp_raw(tu);
-                const T dll = -q.ll * (T(1) + dz * itl), dlu = -q.lu * (T(1) - dz * itu);
-                c = (vl && dz < T(0)) ? fmin(c, -tl * rdz) : c;
-                c = (vl && dll < T(0)) ? fmin(c, -q.ll * rcp_raw(dll)) : c;
-                c = (vu && dz > T(0)) ? fmin(c, tu * rdz) : c;
-                c = (vu && dlu < T(0)) ? fmin(c, -q.lu * rcp_raw(dlu)) : c;
+                const T al = dz * itl, au = dz * itu;
+                c = vl ? fmax(c, fmax(-al, T(1) + al)) : c;
+                c = vu ? fmax(c, fmax(au, T(1) - au)) : c;
                 s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
                 s_b += (vl ? q.ll * dz * (tl + dz) * itl : T(0)) + (vu ? q.lu * dz * (dz - tu) * itu : T(0));
             } else {
+                const T rdz = rcp_raw(dz);
                 const T dza = q.dza;
                 const T itl = frcp(tl), itu = frcp(tu);
                 const T dlal = -q.ll * (T(1) + dza * itl), dlau = -q.lu * (T(1) - dza * itu);
@@ -528,7 +534,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 s_b += (vl ? dlal * dza : T(0)) - (vu ? dlau * dza : T(0));
                 s_c += (vl ? dll * dz : T(0)) - (vu ? dlu * dz : T(0));
             }
-            s_min = fmin(s_min, c);
+            s_min = corr ? fmin(s_min, c) : fmax(s_min, c);
         };
         struct Rec {
             El e;
@@ -560,6 +566,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         for (int j = 0; j < PD; j++) fetch(j, ring[j]);
         SpL<T, RN> arl;
         if constexpr (SPARSE) sp_load(arl, slv, sli, row_base);
+        const Bd b0 = bnd(0), bm = bnd(1);   // stage 0 and interior bounds (sweep constants)
         for (int kb = 0; kb < N; kb += PD) {
 #pragma unroll
             for (int j = 0; j < PD; j++) {
@@ -570,6 +577,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 // first makes the compiler move the refill's registers at the loop back edge,
                 // which waits for those loads and exposes their whole latency
                 Rec &q = ring[j];
+                const Bd bk = k == 0 ? b0 : bm;
                 const T dx = (k == 0 || !xl) ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
                 if (xl) {   // write-only divergent block
 #pragma unroll
@@ -611,7 +619,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 LPC_FTICK(4);
                 stE(dst, k, my);
-                stats(k, my, q.e);
+                stats(my, q.e, bk);
                 fetch(k + PD, ring[j]);
                 LPC_SYNC();
                 LPC_FTICK(7);
@@ -625,9 +633,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             if (corr) e.dza = ldE(L::DZA, N);
             const T dx = xt - e.z;
             stE(dst, N, dx);
-            stats(N, dx, e);
+            stats(dx, e, bnd(N));
         }
-        s_min = gmin(s_min);
+        s_min = corr ? gmin(s_min) : frcp(gmax(s_min));
         s_a = gsum(s_a);
         s_b = gsum(s_b);
         s_c = gsum(s_c);
@@ -668,9 +676,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // terminal stage: P_N = He + Sigma_N, p_N = g_N
             fetchA(N, q);
             fetchA(N - 1, qn);
-            lazy(N, q);
+            lazy(N, q, bnd(N));
             {
-                const T sg = xl ? sigma(N, q) : T(0);
+                const T sg = xl ? sigma(q, bnd(N)) : T(0);
                 zb[r] = xl ? q.z : T(0);
                 LPC_SYNC();
                 T g = q.g;
@@ -699,14 +707,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     sp_load(arl, slv, sli, row_base);
                     sp_load(acl, slv, sli, col_base);
                 }
-                lazy(k, q);
-                const T sg = sigma(k, q);
+                const Bd bk = bnd(k);
+                const T hrr = SP::hdiag ? hm[r * LDZ + r] : T(0);   // read once per stage
+                lazy(k, q, bk);
+                const T sg = sigma(q, bk);
                 zb[r] = q.z;
                 LPC_SYNC();
                 // g = H z + G yref, re = [A B] z_k + c - x_{k+1}
                 T g = q.g, re = 0;
                 if (SP::hdiag) {
-                    g = fma(hm[r * LDZ + r], q.z, g);
+                    g = fma(hrr, q.z, g);
                 } else {
                     T g1 = 0;
 #pragma unroll
@@ -806,7 +816,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         fu[a * NU + u] = fcol[NX + a];
                         fd = (u == a) ? fcol[NX + a] : fd;
                     }
-                    fu[u * NU + u] = fd + sg + (SP::hdiag ? hm[r * LDZ + r] : T(0));
+                    fu[u * NU + u] = fd + sg + hrr;
                     hub[u] = h;
                 }
                 LPC_SYNC();
@@ -912,7 +922,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     }
                 }
 #endif
-                sdiag = sg + (SP::hdiag ? hm[r * LDZ + r] : T(0));   // F(r, r) = F_col(r) + H_rr + Sigma
+                sdiag = sg + hrr;   // F(r, r) = F_col(r) + H_rr + Sigma
                 pv = pnew;
                 LPC_SYNC();
                 LPC_PTICK(7);
@@ -933,10 +943,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 
         // ============================ C: backward corrector vector
         {
+            // sweep constants: H_rr, interior and stage-0 bounds
+            const T hrr = SP::hdiag ? hm[r * LDZ + r] : T(0);
+            const Bd b0 = bnd(0), bm = bnd(1);
             auto ghat = [&](int k, const El &e) {
                 T g = e.g;
-                if (SP::hdiag) g = fma(k < N ? hm[r * LDZ + r] : hem[(xl ? r : 0) * LDX + (xl ? r : 0)], e.z, g);
-                const T tl = e.z - LB(k), tu = UB(k) - e.z, itl = frcp(tl), itu = frcp(tu);
+                if (SP::hdiag) g = fma(k < N ? hrr : hem[(xl ? r : 0) * LDX + (xl ? r : 0)], e.z, g);
+                const Bd b = k == N ? bnd(N) : (k == 0 ? b0 : bm);
+                const T tl = e.z - b.lb, tu = b.ub - e.z, itl = frcp(tl), itu = frcp(tu);
                 const T dll = -e.ll * (T(1) + e.dza * itl), dlu = -e.lu * (T(1) - e.dza * itu);
                 const T cl = (dll * e.dza - smu) * itl, cu = (dlu * e.dza + smu) * itu;
                 return g + (e.ll > T(0) ? cl : T(0)) + (e.lu > T(0) ? cu : T(0));
