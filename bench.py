@@ -57,11 +57,20 @@ def parse():
     return ap.parse_args()
 
 
+def ipm_tolerances(model, N):
+    """(tol_comp, tol_res) of the model's OCP solver options (library defaults when unset)."""
+    from drone_attitude_control_amd.models import OCPS
+    o = OCPS[model](N).solver_options
+    return float(o.qp_solver_tol_comp or 1e-15), float(o.qp_solver_tol_stat or 1e-12)
+
+
 def cpu_baseline(model, N, table, offsets, x_init, seconds):
-    """Time the C oracle (same Riccati IPM, fp64) on a bounded sample of the same instances."""
+    """Time the C oracle (same Riccati IPM, fp64, same tolerances) on a bounded sample of the
+    same instances."""
     from oracle import cref, models
     spec = models.MODELS[model](N)
-    R = cref.RiccatiIpmRef(spec)
+    tc, tr = ipm_tolerances(model, N)
+    R = cref.RiccatiIpmRef(spec, tol_comp=tc, tol_res=tr)
     ny, nye = spec.ny, spec.nx
     nsamp = min(len(offsets), 4096)
     Y = np.stack([np.concatenate([table[t:t + N, :ny].ravel(), table[t + N, :nye]]) for t in offsets[:nsamp]])
@@ -151,6 +160,7 @@ def main():
                                          device="cuda" if dist is not None and args.dist_backend == "nccl" else None)
 
     if rank == 0:
+        tols = ipm_tolerances(model, N)
         value = world * B * args.steps / elapsed
         n_ipm = n_ipm_cpu if n_ipm_cpu is not None else st["mean_qp_iter"]
         fl_launch = flops_per_iter(nx, nu, N) * n_ipm * B
@@ -171,7 +181,7 @@ def main():
             "dtype": "f64" if args.precision == "fp64" else "f32",
             "data": "synthetic (seeded closed-loop Monte-Carlo instances on the reference circle)",
             "config": {"workload": f"{model} closed-loop NMPC step: yref window + x0 pin + IPM solve "
-                                   f"(tol_comp 1e-15) + plant/noise advance",
+                                   f"(tol_comp {tols[0]:g}, tol_res {tols[1]:g}) + plant/noise advance",
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"instance-sharded x{world}, RCCL stats reduce",
                        "instances_per_wave": cl.solver.launch_info()["instances_per_wave"]},

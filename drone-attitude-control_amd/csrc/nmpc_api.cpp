@@ -526,8 +526,13 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     // ---- options
     const bool f64 = precision == NMPC_FP64;
     h->max_iter = d->qp_solver_iter_max > 0 ? d->qp_solver_iter_max : 50;
+    // fp32 handles never ask for more than single precision can reach (1e-7 / 1e-5)
     h->tol_comp = d->qp_solver_tol_comp > 0 ? d->qp_solver_tol_comp : (f64 ? 1e-15 : 1e-7);
     h->tol_res = d->qp_solver_tol_res > 0 ? d->qp_solver_tol_res : (f64 ? 1e-12 : 1e-5);
+    if (!f64) {
+        h->tol_comp = std::max(h->tol_comp, 1e-7);
+        h->tol_res = std::max(h->tol_res, 1e-5);
+    }
     h->mu0 = d->qp_solver_mu0 > 0 ? d->qp_solver_mu0 : 1e-2;
     // ---- host staging
     h->h_x0.assign((size_t)batch * nx, 0.0);

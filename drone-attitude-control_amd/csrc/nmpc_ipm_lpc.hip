@@ -40,6 +40,10 @@
 #ifndef NMPC_LPC_PF
 #define NMPC_LPC_PF 2
 #endif
+// forward sweeps: statistics of stage k-1 computed inside stage k's first LDS exchange
+#ifndef NMPC_LPC_DEFER
+#define NMPC_LPC_DEFER 1
+#endif
 // rows of Y = L^{-1} F_ux per LDS chunk in the P update of the Riccati stage
 #ifndef NMPC_LPC_PCH
 #define NMPC_LPC_PCH 2
@@ -567,6 +571,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         SpL<T, RN> arl;
         if constexpr (SPARSE) sp_load(arl, slv, sli, row_base);
         const Bd b0 = bnd(0), bm = bnd(1);   // stage 0 and interior bounds (sweep constants)
+#if NMPC_LPC_DEFER
+        // statistics pending from the previous stage (neutral before stage 0: no bound active)
+        T pm = 0;
+        El pe{};
+        Bd pb = b0;
+#endif
         for (int kb = 0; kb < N; kb += PD) {
 #pragma unroll
             for (int j = 0; j < PD; j++) {
@@ -579,6 +589,36 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 Rec &q = ring[j];
                 const Bd bk = k == 0 ? b0 : bm;
                 const T dx = (k == 0 || !xl) ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
+#if NMPC_LPC_DEFER
+                // branch-free stage (one scheduling region per LDS exchange): u-lanes write their
+                // partial-product row into the spare row NX, which nobody reads
+                {
+                    const int pr_ = xl ? r : NX;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) part[pr_ * LDU + i] = q.kq[i] * dx;
+                }
+                LPC_SYNC();
+                LPC_FTICK(0);
+                // the statistics of stage k-1 run here, between issuing the partial-sum reads
+                // and their first use, instead of at the end of stage k-1 on its critical path
+                stats(pm, pe, pb);
+                T du;
+                {
+                    const int uu = ul ? u : 0;
+                    T s0 = q.c0, s1 = 0;
+#pragma unroll
+                    for (int jj = 0; jj + 1 < NX; jj += 2) {
+                        s0 += part[jj * LDU + uu];
+                        s1 += part[(jj + 1) * LDU + uu];
+                    }
+                    if (NX % 2) s0 += part[(NX - 1) * LDU + uu];
+                    du = ul ? s0 + s1 : T(0);
+                }
+                const T my = xl ? dx : du;
+                zb[r] = q.e.z + my;
+                LPC_SYNC();
+                LPC_FTICK(3);
+#else
                 if (xl) {   // write-only divergent block
 #pragma unroll
                     for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
@@ -604,6 +644,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_SYNC();
                 LPC_FTICK(3);
                 const T my = xl ? dx : du;
+#endif
                 if constexpr (SPARSE) {
                     const T s = sp_dot(arl, zb, c_r);
                     xt = xl ? s : xt;
@@ -619,12 +660,21 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 LPC_FTICK(4);
                 stE(dst, k, my);
+#if NMPC_LPC_DEFER
+                pm = my;
+                pe = q.e;
+                pb = bk;
+#else
                 stats(my, q.e, bk);
+#endif
                 fetch(k + PD, ring[j]);
                 LPC_SYNC();
                 LPC_FTICK(7);
             }
         }
+#if NMPC_LPC_DEFER
+        stats(pm, pe, pb);
+#endif
         if (xl) {
             El e;
             e.z = ldE(L::Z, N);

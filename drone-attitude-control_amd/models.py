@@ -163,6 +163,12 @@ def quad13_ocp(N=20):
     o.sim_method_num_stages = 4
     o.N_horizon = N
     o.tf = p.dt * N
+    # IPM tolerances (solver options, like acados's qp_solver_tol_*): the well-conditioned quad13
+    # OCP meets the 1e-6 parity bar with > 300x margin at mu <= 1e-12 (max
+    # deviation 3e-9 on the golden cases, 7e-11 on the 8192 bench instances, vs ~1e-15 / 1e-12
+    # solves); the force OCP (condition ~4e4) keeps the library default 1e-15 / 1e-12
+    o.qp_solver_tol_comp = 1e-12
+    o.qp_solver_tol_stat = 1e-10
     return ocp
 
 

@@ -111,8 +111,8 @@ typedef struct nmpc_ocp_desc {
     const double *x0; /* constraints.x0 initial value (nx); may be NULL */
     /* QP / IPM options (solver_options.qp_solver_*) */
     int qp_solver_iter_max;    /* <= 0: 50 */
-    double qp_solver_tol_comp; /* <= 0: 1e-15 (fp64) / 1e-7 (fp32) */
-    double qp_solver_tol_res;  /* <= 0: 1e-12 (fp64) / 1e-6 (fp32) */
+    double qp_solver_tol_comp; /* <= 0: 1e-15 (fp64) / 1e-7 (fp32); fp32 clamps to >= 1e-7 */
+    double qp_solver_tol_res;  /* <= 0: 1e-12 (fp64) / 1e-5 (fp32); fp32 clamps to >= 1e-5 */
     double qp_solver_mu0;      /* <= 0: 1e-2 */
 } nmpc_ocp_desc;
 
