@@ -812,9 +812,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (xl) {
+                    // structured kernels: the diagonal part Sigma_x [A B](r, :) of M's row r
+                    // touches only the <= RN structural nonzeros of row r; it is added to M^T in
+                    // LDS (atomic adds after the plain stores, in order within the wavefront)
+                    // instead of scaling the dense LDS row of [A B] into all NZ accumulators
+                    SpL<T, RN> arm;
+                    if constexpr (SPARSE) sp_load(arm, slv, sli, row_base);
                     T mrow[NZ];
 #pragma unroll
-                    for (int c = 0; c < NZ; c++) mrow[c] = sdiag * abr[r * LDZ + c];
+                    for (int c = 0; c < NZ; c++) mrow[c] = SPARSE ? T(0) : sdiag * abr[r * LDZ + c];
                     sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int l, const T (&row)[NZ]) {
 #pragma unroll
                         for (int c = 0; c < NZ; c++)
@@ -822,6 +828,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     });
 #pragma unroll
                     for (int c = 0; c < NZ; c++) mt[c * LDX + r] = mrow[c];
+                    if constexpr (SPARSE) {
+#pragma unroll
+                        for (int j = 0; j < RN; j++)
+                            __hip_atomic_fetch_add((T *)((char *)mt + arm.o[j] * LDX) + r, sdiag * arm.v[j],
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    }
                 }
                 LPC_SYNC();
                 LPC_PTICK(3);
