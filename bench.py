@@ -87,10 +87,21 @@ def cpu_baseline(model, N, table, offsets, x_init, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    # single-core figure, on a smaller slice of the same inputs (~1/5 of the time)
+    n1 = max(1, min(nsamp, 256))
+    s1, t1 = 0, time.perf_counter()
+    while True:
+        R.solve(X0[:n1], Y[:n1], nthreads=1)
+        s1 += n1
+        e1 = time.perf_counter() - t1
+        if e1 >= seconds / 5:
+            break
     return {"value": solves / el, "unit": "NMPC steps/s", "cores": threads, "kind": "port",
             "sample": f"{solves} solves of the first closed-loop step of {nsamp} bench instances "
                       f"({model}, N={N}, fp64) in {el:.1f} s, OpenMP over instances; "
-                      f"oracle/c/riccati_ipm.c -O3 -march=x86-64-v3"}, n_ipm
+                      f"oracle/c/riccati_ipm.c -O3 -march=x86-64-v3",
+            "single_core": {"value": s1 / e1, "cores": 1,
+                            "sample": f"{s1} solves of {n1} of those instances in {e1:.1f} s"}}, n_ipm
 
 
 def load_traffic(model, N, batch, precision):
