@@ -194,7 +194,8 @@ def main():
             "config": {"workload": f"{model} closed-loop NMPC step: yref window + x0 pin + IPM solve "
                                    f"(tol_comp {tols[0]:g}, tol_res {tols[1]:g}) + plant/noise advance",
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,
-                       "global_batch": B * world, "parallelism": f"instance-sharded x{world}, RCCL stats reduce",
+                       "global_batch": B * world, "parallelism": f"instance-sharded x{world}, "
+                                                                    f"{'gloo' if args.dist_backend == 'gloo' else 'RCCL'} stats reduce",
                        "instances_per_wave": cl.solver.launch_info()["instances_per_wave"]},
             "roofline": {"bound": "mfma", "pipe": "fp64 FMA on VALU" if args.precision == "fp64" else "fp32 FMA on VALU",
                          "kernel": cl.solver.launch_info()["kernel"], "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
