@@ -63,12 +63,16 @@ namespace lpc {
 template <typename T>
 using cptr = const T __attribute__((address_space(4))) *;
 
+// Newton steps after the hardware fp64 rsq / rcp estimates (experiment builds may set 1)
+#ifndef NMPC_LPC_NEWTON
+#define NMPC_LPC_NEWTON 2
+#endif
 __device__ __forceinline__ double frsq(double x)
 {
     double y = __builtin_amdgcn_rsq(x);
     const double h = 0.5 * x;
     y = fma(y, fma(-h, y * y, 0.5), y);
-    y = fma(y, fma(-h, y * y, 0.5), y);
+    if (NMPC_LPC_NEWTON > 1) y = fma(y, fma(-h, y * y, 0.5), y);
     return y;
 }
 __device__ __forceinline__ float frsq(float x)
@@ -80,7 +84,7 @@ __device__ __forceinline__ double frcp(double x)
 {
     double r = __builtin_amdgcn_rcp(x);
     r = fma(fma(-x, r, 1.0), r, r);
-    r = fma(fma(-x, r, 1.0), r, r);
+    if (NMPC_LPC_NEWTON > 1) r = fma(fma(-x, r, 1.0), r, r);
     return r;
 }
 __device__ __forceinline__ float frcp(float x)
