@@ -40,6 +40,11 @@
 #ifndef NMPC_LPC_PF
 #define NMPC_LPC_PF 2
 #endif
+// Riccati / corrector-vector stages: the work the first LDS exchange does not need (dual part of
+// the lazy step, Sigma, the corrector right-hand side) runs after it, overlapping its latency
+#ifndef NMPC_LPC_EARLY_Z
+#define NMPC_LPC_EARLY_Z 1
+#endif
 // forward sweeps: statistics of stage k-1 computed inside stage k's first LDS exchange
 #ifndef NMPC_LPC_DEFER
 #define NMPC_LPC_DEFER 1
@@ -465,6 +470,27 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         const T sl = q.ll * frcp(q.z - b.lb), su = q.lu * frcp(b.ub - q.z);
         return (q.ll > T(0) ? sl : T(0)) + (q.lu > T(0) ? su : T(0));
     };
+    // the same lazy step split in two for the Riccati stages k < N: the primal update first (it
+    // is all the stage's first LDS exchange needs), the dual update after that exchange, where
+    // it fills the latency of the residual's LDS reads; the write-back is unconditional (a
+    // frozen group rewrites its unchanged words), so the stage stays one scheduling region
+    auto lazy_z = [&](El &q) {
+        const T zo = q.z;
+        q.z = pending ? q.z + alpha * q.dz : q.z;
+        return zo;
+    };
+    auto lazy_duals = [&](int k, El &q, T zo, const Bd &b) {
+        const bool vl = q.ll > T(0), vu = q.lu > T(0);
+        const T tl = zo - b.lb, tu = b.ub - zo, itl = frcp(tl), itu = frcp(tu);
+        const T dlal = -q.ll * (T(1) + q.dza * itl), dlau = -q.lu * (T(1) - q.dza * itu);
+        const T nl = q.ll + alpha * ((smu - q.ll * tl - dlal * q.dza - q.ll * q.dz) * itl);
+        const T nu_ = q.lu + alpha * ((smu - q.lu * tu + dlau * q.dza + q.lu * q.dz) * itu);
+        q.ll = (pending && vl) ? nl : q.ll;
+        q.lu = (pending && vu) ? nu_ : q.lu;
+        stE(L::Z, k, q.z);
+        stE(L::LL, k, q.ll);
+        stE(L::LU, k, q.lu);
+    };
 
     // ---- forward recursion (B: predictor into dza with ratio test / centring sums;
     //      D: corrector into dz with step length / new-mu sums):
@@ -763,10 +789,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 const Bd bk = bnd(k);
                 const T hrr = SP::hdiag ? hm[r * LDZ + r] : T(0);   // read once per stage
+#if NMPC_LPC_EARLY_Z
+                const T zo = lazy_z(q);
+                zb[r] = q.z;
+                LPC_SYNC();
+                lazy_duals(k, q, zo, bk);
+                const T sg = sigma(q, bk);
+#else
                 lazy(k, q, bk);
                 const T sg = sigma(q, bk);
                 zb[r] = q.z;
                 LPC_SYNC();
+#endif
                 // g = H z + G yref, re = [A B] z_k + c - x_{k+1}
                 T g = q.g, re = 0;
                 if (SP::hdiag) {
@@ -1057,9 +1091,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     const int k = N - 1 - kb - j;
                     if (k < 0) break;
                     RecC &q = ring[j];   // read in place, refilled after its last use (see forward)
+#if NMPC_LPC_EARLY_Z
+                    // v first: the corrector right-hand side is only needed after the exchange
+                    if (xl) vb[r] = q.pr + pv;
+                    LPC_SYNC();
+                    const T gh = ghat(k, q.e);
+#else
                     const T gh = ghat(k, q.e);
                     if (xl) vb[r] = q.pr + pv;
                     LPC_SYNC();
+#endif
                     T h;
                     if constexpr (SPARSE) {
                         h = sp_dot(acl, vb, gh);
