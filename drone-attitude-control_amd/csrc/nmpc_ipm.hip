@@ -999,9 +999,10 @@ static const IpmEntry<T> *table(int *n)
 
 // kernel family: NMPC_KERNEL=lpc / =wave forces one; by default the lane-per-component
 // kernels (ipm_lpc_kernel) run when the stage is wide (nx + nu >= 12: quad13) or the batch fills
-// at least 768 wavefronts, else the wavefront-per-instance ones — for small models at small
-// batches their per-instance latency floor is lower (tools/family_sweep.sh: force N=20 B=1024
-// 0.97 vs 1.34 ms, jerk N=40 B=4096 1.17 vs 1.24 ms; force B=8192 fp32 1.24 vs 1.04 ms)
+// at least 384 of their wavefronts, else the wavefront-per-instance ones — for small models at
+// small batches their per-instance latency floor is lower (tools/family_pairs.sh, fp64, lpc vs
+// wave: force N=20 B=1024 1.09 vs 0.98 ms, B=4096 1.19 vs 1.31, B=8192 1.29 vs 1.88; jerk N=40
+// B=2048 1.03 vs 0.91, B=4096 1.05 vs 1.16, B=8192 1.14 vs 1.79)
 static int kernel_kind(int nx, int nu, int batch)
 {
     const char *k = getenv("NMPC_KERNEL");
@@ -1010,7 +1011,7 @@ static int kernel_kind(int nx, int nu, int batch)
     const int nz = nx + nu;
     if (nz > 64) return 0;
     const long waves = ((long)batch + 64 / nz - 1) / (64 / nz);
-    return (nz >= 12 || waves >= 768) ? 1 : 0;
+    return (nz >= 12 || waves >= 384) ? 1 : 0;
 }
 
 template <typename T>
