@@ -45,6 +45,11 @@
 #ifndef NMPC_LPC_EARLY_Z
 #define NMPC_LPC_EARLY_Z 1
 #endif
+// structured Riccati stage: Sigma_x [A B](r, :) added to M^T by LDS atomics (1) or folded into
+// the M accumulators from the dense LDS row (0)
+#ifndef NMPC_LPC_ATOMIC_DIAG
+#define NMPC_LPC_ATOMIC_DIAG 0
+#endif
 // forward sweeps: statistics of stage k-1 computed inside stage k's first LDS exchange
 #ifndef NMPC_LPC_DEFER
 #define NMPC_LPC_DEFER 1
@@ -854,11 +859,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     // touches only the <= RN structural nonzeros of row r; it is added to M^T in
                     // LDS (atomic adds after the plain stores, in order within the wavefront)
                     // instead of scaling the dense LDS row of [A B] into all NZ accumulators
+                    constexpr bool ADIAG = SPARSE && NMPC_LPC_ATOMIC_DIAG;
                     SpL<T, RN> arm;
-                    if constexpr (SPARSE) sp_load(arm, slv, sli, row_base);
+                    if constexpr (ADIAG) sp_load(arm, slv, sli, row_base);
                     T mrow[NZ];
 #pragma unroll
-                    for (int c = 0; c < NZ; c++) mrow[c] = SPARSE ? T(0) : sdiag * abr[r * LDZ + c];
+                    for (int c = 0; c < NZ; c++) mrow[c] = ADIAG ? T(0) : sdiag * abr[r * LDZ + c];
                     sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int l, const T (&row)[NZ]) {
 #pragma unroll
                         for (int c = 0; c < NZ; c++)
@@ -866,7 +872,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     });
 #pragma unroll
                     for (int c = 0; c < NZ; c++) mt[c * LDX + r] = mrow[c];
-                    if constexpr (SPARSE) {
+                    if constexpr (ADIAG) {
 #pragma unroll
                         for (int j = 0; j < RN; j++)
                             __hip_atomic_fetch_add((T *)((char *)mt + arm.o[j] * LDX) + r, sdiag * arm.v[j],
