@@ -43,7 +43,7 @@
 // Riccati / corrector-vector stages: the work the first LDS exchange does not need (dual part of
 // the lazy step, Sigma, the corrector right-hand side) runs after it, overlapping its latency
 #ifndef NMPC_LPC_EARLY_Z
-#define NMPC_LPC_EARLY_Z 1
+#define NMPC_LPC_EARLY_Z 0
 #endif
 // structured Riccati stage: Sigma_x [A B](r, :) added to M^T by LDS atomics (1) or folded into
 // the M accumulators from the dense LDS row (0)
