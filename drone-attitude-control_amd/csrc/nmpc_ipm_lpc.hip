@@ -40,8 +40,9 @@
 #ifndef NMPC_LPC_PF
 #define NMPC_LPC_PF 2
 #endif
-// Riccati / corrector-vector stages: the work the first LDS exchange does not need (dual part of
-// the lazy step, Sigma, the corrector right-hand side) runs after it, overlapping its latency
+// Riccati / corrector-vector stages (experiment knob, off: measured 2-3 % slower on quad13): run
+// the work the first LDS exchange does not need (dual part of the lazy step, Sigma, the corrector
+// right-hand side) after that exchange instead of before it
 #ifndef NMPC_LPC_EARLY_Z
 #define NMPC_LPC_EARLY_Z 0
 #endif
