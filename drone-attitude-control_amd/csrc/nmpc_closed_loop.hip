@@ -158,6 +158,58 @@ __global__ __launch_bounds__(256) void cl_advance_kernel(ClParams<T> p)
     acc[3] += 1.0;
 }
 
+// The controller-model plant (plant == 0) at a compile-time size: the model matrices live in LDS
+// (one broadcast read per entry instead of a global load per thread and entry) and the state,
+// input and successor state in registers (the generic kernel's runtime-sized arrays spill to
+// scratch). Same arithmetic order as cl_advance_kernel.
+template <typename T, int NX, int NU>
+__global__ __launch_bounds__(256) void cl_model_advance_kernel(ClParams<T> p)
+{
+    __shared__ double sA[NX * NX], sB[NX * NU], sc[NX];
+    for (int e = threadIdx.x; e < NX * NX; e += blockDim.x) sA[e] = (double)p.A[e];
+    for (int e = threadIdx.x; e < NX * NU; e += blockDim.x) sB[e] = (double)p.Bm[e];
+    for (int e = threadIdx.x; e < NX; e += blockDim.x) sc[e] = (double)p.c[e];
+    __syncthreads();
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    const int t = (p.offset[b] + p.step) % p.period;
+    const T *xref = p.table + (size_t)t * p.table_cols;
+    T *st = p.state + (size_t)b * NX;
+    const T *xo = p.xout + ((size_t)b * (p.N + 1) + p.cost_stage) * NX;
+    const T *u0 = p.uout + (size_t)b * p.N * NU;
+    double x[NX], u[NU];
+#pragma unroll
+    for (int i = 0; i < NX; i++) x[i] = (double)st[i];
+#pragma unroll
+    for (int j = 0; j < NU; j++) u[j] = (double)u0[j];
+    double cost = 0.0, aed = 0.0;
+    for (int i = 0; i < p.ncl; i++) {
+        const double e = (double)xo[i] - (double)xref[i];
+        cost += (double)p.wcl[i] * e * e;
+    }
+    for (int i = 0; i < p.aed_dims; i++) aed += fabs((double)xref[i] - (double)st[i]);
+    double w = 0.0;
+    if (p.noise_table) {
+        if (p.step < p.noise_len) w = p.noise_table[(size_t)b * p.noise_len + p.step];
+    } else if (p.noise_std > 0) {
+        w = p.noise_std * philox_normal_dev(p.seed, (unsigned long long)(p.inst_base + b), (unsigned long long)p.step);
+    }
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        double s = sc[i];
+#pragma unroll
+        for (int j = 0; j < NX; j++) s += sA[i * NX + j] * x[j];
+#pragma unroll
+        for (int j = 0; j < NU; j++) s += sB[i * NU + j] * u[j];
+        st[i] = (T)(s + (i < p.noise_dims ? w : 0.0));
+    }
+    double *acc = p.acc + (size_t)b * 4;
+    acc[0] += cost;
+    acc[1] += aed;
+    acc[2] += p.status[b] != 0 ? 1.0 : 0.0;
+    acc[3] += 1.0;
+}
+
 template <typename T>
 hipError_t cl_prepare_launch(const ClParams<T> &p, hipStream_t s)
 {
@@ -170,6 +222,10 @@ hipError_t cl_prepare_launch(const ClParams<T> &p, hipStream_t s)
 template <typename T>
 hipError_t cl_advance_launch(const ClParams<T> &p, hipStream_t s)
 {
+    if (p.plant == 0 && p.nx == 13 && p.nu == 4) {   // quad13 (the headline model)
+        hipLaunchKernelGGL((cl_model_advance_kernel<T, 13, 4>), dim3((p.B + 255) / 256), dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(cl_advance_kernel<T>, dim3((p.B + 255) / 256), dim3(256), 0, s, p);
     return hipGetLastError();
 }
