@@ -49,7 +49,11 @@ def parse():
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--repeats", type=int, default=10,
+                    help="timed regions of --steps steps each; value = the median region (BASELINE.md: median of >= 10)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--python-loop-steps", type=int, default=100,
+                    help="steps of the B=1 Python drop-in loop timed for BASELINE config 1 (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the default); gloo only to rehearse several ranks "
@@ -57,19 +61,24 @@ def parse():
     return ap.parse_args()
 
 
-def ipm_tolerances(model, N):
-    """(tol_comp, tol_res) of the model's OCP solver options (library defaults when unset)."""
+def ipm_tolerances(model, N, precision="fp64"):
+    """(tol_comp, tol_res) the engine runs with: the model's OCP solver options (library
+    defaults 1e-15 / 1e-12 when unset), clamped to >= 1e-7 / 1e-5 for fp32 handles exactly as
+    nmpc_create does (nmpc_api.cpp)."""
     from drone_attitude_control_amd.models import OCPS
     o = OCPS[model](N).solver_options
-    return float(o.qp_solver_tol_comp or 1e-15), float(o.qp_solver_tol_stat or 1e-12)
+    tc, tr = float(o.qp_solver_tol_comp or 1e-15), float(o.qp_solver_tol_stat or 1e-12)
+    if precision == "fp32":
+        tc, tr = max(tc, 1e-7), max(tr, 1e-5)
+    return tc, tr
 
 
-def cpu_baseline(model, N, table, offsets, x_init, seconds):
-    """Time the C oracle (same Riccati IPM, fp64, same tolerances) on a bounded sample of the
-    same instances."""
+def cpu_baseline(model, N, table, offsets, x_init, seconds, precision):
+    """Time the C oracle (same Riccati IPM, fp64 arithmetic, the GPU run's tolerances) on a
+    bounded sample of the same instances."""
     from oracle import cref, models
     spec = models.MODELS[model](N)
-    tc, tr = ipm_tolerances(model, N)
+    tc, tr = ipm_tolerances(model, N, precision)
     R = cref.RiccatiIpmRef(spec, tol_comp=tc, tol_res=tr)
     ny, nye = spec.ny, spec.nx
     nsamp = min(len(offsets), 4096)
@@ -98,25 +107,43 @@ def cpu_baseline(model, N, table, offsets, x_init, seconds):
             break
     return {"value": solves / el, "unit": "NMPC steps/s", "cores": threads, "kind": "port",
             "sample": f"{solves} solves of the first closed-loop step of {nsamp} bench instances "
-                      f"({model}, N={N}, fp64) in {el:.1f} s, OpenMP over instances; "
-                      f"oracle/c/riccati_ipm.c -O3 -march=x86-64-v3",
+                      f"({model}, N={N}, fp64 arithmetic, tol_comp {tc:g} / tol_res {tr:g}) in {el:.1f} s, "
+                      f"OpenMP over instances; oracle/c/riccati_ipm.c -O3 -march=x86-64-v3",
             "single_core": {"value": s1 / e1, "cores": 1,
                             "sample": f"{s1} solves of {n1} of those instances in {e1:.1f} s"}}, n_ipm
 
 
-def load_traffic(model, N, batch, precision):
-    """HBM bytes per solve launch from the committed rocprofv3 PMC summary, if one matches."""
+def load_pmc(model, N, batch, precision, kernel):
+    """The committed rocprofv3 PMC summary entry (profiles/pmc_traffic.json) for this config and
+    solve kernel, if one matches: memory-side bytes per launch and MFMA instructions per launch."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return {}
     try:
         d = json.load(open(path))
         for e in d.get("entries", []):
-            if (e.get("model"), e.get("N"), e.get("batch"), e.get("precision")) == (model, N, batch, precision):
-                return e.get("hbm_bytes_per_launch")
+            if (e.get("model"), e.get("N"), e.get("batch"), e.get("precision")) == (model, N, batch, precision) \
+                    and e.get("kernel", kernel) == kernel:
+                return e
     except (ValueError, OSError):
-        return None
-    return None
+        return {}
+    return {}
+
+
+def python_loop_rate(N, steps):
+    """BASELINE config 1: the reference's single-trajectory closed loop (force_model/controller.py
+    :25-54) as the drop-in sees it — per step 31 yref set() calls, lbx/ubx, solve(), get(), the
+    converter and one plant step, each a Python -> C-ABI call (the QP and the plant on the GPU)."""
+    from drone_attitude_control_amd import controllers
+    from drone_attitude_control_amd.models import gen_circle_traj
+    ref = gen_circle_traj(500, N, 6, 2)
+    x0 = np.array([1.0, 0, 0, 0.62])
+    controllers.force_follow_trajectory(ref[:, :4], ref[:, 4:6], x0, False, verbose=False, N=N, n_steps=3)
+    t0 = time.perf_counter()
+    controllers.force_follow_trajectory(ref[:, :4], ref[:, 4:6], x0, False, verbose=False, N=N, n_steps=steps)
+    el = time.perf_counter() - t0
+    return {"value": steps / el, "unit": "NMPC steps/s", "batch": 1,
+            "sample": f"{steps} steps of controllers.force_follow_trajectory (force, N={N}, B=1, fp64) in {el:.2f} s"}
 
 
 def main():
@@ -148,38 +175,57 @@ def main():
                     table=table, offsets=offsets_r, x_init=x_r, instance_base=base, seed=args.seed)
     nx, nu = cl.solver.nx, cl.solver.nu
 
-    # CPU baseline first (rank 0, single-GPU runs only), on this rank's first-step inputs
-    cpu, n_ipm_cpu = None, None
+    # CPU baseline and the B=1 Python drop-in loop first (rank 0, single-GPU runs only)
+    cpu, n_ipm_cpu, pyloop = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, n_ipm_cpu = cpu_baseline(model, N, table, offsets_r, x_r, args.cpu_seconds)
+        cpu, n_ipm_cpu = cpu_baseline(model, N, table, offsets_r, x_r, args.cpu_seconds, args.precision)
+        if args.python_loop_steps > 0:
+            pyloop = python_loop_rate(20, args.python_loop_steps)
+            cpu["python_loop"] = pyloop
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     cl.run(args.warmup, sync=True)
-    barrier()
-    t0 = time.perf_counter()
-    cl.run(args.steps, sync=True)
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
+    regions, kernel_ms_r = [], []
+    for _ in range(max(1, args.repeats)):
+        barrier()
+        t0 = time.perf_counter()
+        cl.run(args.steps, sync=True)
+        t1 = time.perf_counter()
+        barrier()
+        regions.append(t1 - t0)
+        st = cl.stats()
+        kernel_ms_r.append(st["solve_kernel_ms"] / max(1, st["solve_launches"]))
+    regions = np.array(regions)
     st = cl.stats()
     red = np.array([st["cost_sum"], st["aed_sum"], st["failed"], st["instance_steps"]])
-    # one SUM of the statistics and one MAX of the timings over RCCL, after the timed region
-    red, elapsed, kernel_ms = reduce_run(dist, red, elapsed, st["solve_kernel_ms"] / max(1, st["solve_launches"]),
-                                         device="cuda" if dist is not None and args.dist_backend == "nccl" else None)
+    # one SUM of the statistics and one MAX of the timings over RCCL, after the timed regions
+    red, regions, kernel_ms_r = reduce_run(dist, red, regions, np.array(kernel_ms_r),
+                                           device="cuda" if dist is not None and args.dist_backend == "nccl" else None)
+    regions = np.atleast_1d(regions)
+    kernel_ms_r = np.atleast_1d(kernel_ms_r)
+    med = int(np.argsort(regions)[len(regions) // 2])
+    elapsed = float(regions[med])
+    kernel_ms = float(np.median(kernel_ms_r))
 
     if rank == 0:
-        tols = ipm_tolerances(model, N)
+        tols = ipm_tolerances(model, N, args.precision)
         value = world * B * args.steps / elapsed
-        n_ipm = n_ipm_cpu if n_ipm_cpu is not None else st["mean_qp_iter"]
+        # credited IPM iterations: the CPU baseline's on the same inputs at the same tolerances,
+        # never more than the GPU's own mean (extra iterations on either side earn nothing)
+        n_ipm = st["mean_qp_iter"] if n_ipm_cpu is None else min(n_ipm_cpu, st["mean_qp_iter"])
         fl_launch = flops_per_iter(nx, nu, N) * n_ipm * B
         achieved = fl_launch / (kernel_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.precision]
-        traffic = load_traffic(model, N, B, args.precision)
+        info = cl.solver.launch_info()
+        pmc = load_pmc(model, N, B, args.precision, info["kernel"])
+        headline = model == "quad13" and N == 20
+        metric = ("NMPC steps/sec (batched trajectories), N=20 nx=13 nu=4, 1/2/4/8 MI355X" if headline else
+                  f"NMPC steps/sec (batched trajectories), N={N} nx={nx} nu={nu} ({model}), 1/2/4/8 MI355X")
         line = {
-            "metric": "NMPC steps/sec (batched trajectories), N=20 nx=13 nu=4, 1/2/4/8 MI355X",
+            "metric": metric,
             "value": value,
             "unit": "NMPC steps/s",
             "n_gpus": world,
@@ -196,14 +242,25 @@ def main():
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"instance-sharded x{world}, "
                                                                     f"{'gloo' if args.dist_backend == 'gloo' else 'RCCL'} stats reduce",
-                       "instances_per_wave": cl.solver.launch_info()["instances_per_wave"]},
-            "roofline": {"bound": "mfma", "pipe": "fp64 FMA on VALU" if args.precision == "fp64" else "fp32 FMA on VALU",
-                         "kernel": cl.solver.launch_info()["kernel"], "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic,
+                       "instances_per_wave": info["instances_per_wave"]},
+            "timing": {"regions": len(regions), "steps_per_region": args.steps, "value_from": "median region",
+                       "region_ms": [round(float(r) * 1e3, 4) for r in regions],
+                       "spread": float((regions.max() - regions.min()) / elapsed)},
+            "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32",
+                         "pipe": ("FP64 FMA on the VALU" if args.precision == "fp64" else "FP32 FMA on the VALU")
+                         + " (MI355X: FP64 matrix peak = FP64 vector peak; FP32 matrix peak = FP32 vector peak)",
+                         "kernel": info["kernel"], "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": pmc.get("hbm_bytes_per_launch"),
+                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per launch from the committed rocprofv3 PMC pass "
+                                         f"({pmc.get('source', 'none for this config')}); no x2 FETCH_SIZE "
+                                         "correction: the kernel's loads are 4/8-B per lane, the guide's x2 is "
+                                         "calibrated for 16-B streams; includes Infinity-Cache hits",
+                         "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
                          "flops_per_launch": fl_launch, "kernel_ms": kernel_ms,
-                         "n_ipm": n_ipm, "gpu_mean_qp_iter": st["mean_qp_iter"]},
+                         "n_ipm": n_ipm, "n_ipm_cpu": n_ipm_cpu, "gpu_mean_qp_iter": st["mean_qp_iter"]},
             "solve_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "QP solves/s",
-                           "note": "ipm_kernel alone (mean launch duration from HIP events), all ranks"},
+                           "note": "solve kernel alone (median of the regions' mean launch durations, HIP events), "
+                                   "all ranks"},
             "cpu_baseline": cpu,
             "closed_loop": {"mean_cost_per_step": red[0] / max(1.0, red[3]),
                             "aed": red[1] / max(1.0, red[3]) / (2 if model != "quad13" else 3),

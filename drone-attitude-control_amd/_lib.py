@@ -90,6 +90,7 @@ SIGNATURES = {
     "nmpc_closed_loop_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ClosedLoopDesc)]),
     "nmpc_closed_loop_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "nmpc_closed_loop_stats": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_int]),
+    "nmpc_closed_loop_instance_stats": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_size_t]),
     "nmpc_closed_loop_get_state": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_size_t]),
     "nmpc_sim_plant": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                       ctypes.c_double, _dp, _dp, _dp]),

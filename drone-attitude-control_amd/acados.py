@@ -222,8 +222,9 @@ def describe_ocp(ocp):
         lbu=lbu, ubu=ubu, idxbu=idxbu, lbx=lbx, ubx=ubx, idxbx=idxbx,
         lbx_e=lbx_e, ubx_e=ubx_e, idxbx_e=idxbx_e, x0=_arr(cons.x0, nx),
         qp_solver_iter_max=int(opts.qp_solver_iter_max or 0),
+        # acados's qp_tol sets every QP tolerance (stat/eq/ineq/comp) unless one is given
         qp_solver_tol_comp=float(opts.qp_solver_tol_comp or (opts.qp_tol or 0.0) or 0.0),
-        qp_solver_tol_res=float(opts.qp_solver_tol_stat or 0.0),
+        qp_solver_tol_res=float(opts.qp_solver_tol_stat or (opts.qp_tol or 0.0) or 0.0),
         qp_solver_mu0=float(opts.qp_solver_mu0 or 0.0))
 
 

@@ -68,6 +68,20 @@ def workload(model, N, batch_global, seed=42, main_like_first=True):
     return table, offsets, x
 
 
+NY = {"force": (6, 4), "jerk": (8, 6), "quad13": (17, 13)}
+
+
+def first_step_qps(model, N, table, offsets, x_init):
+    """The QPs the closed loop solves at step 0 (what cl_prepare_kernel builds on the device):
+    x0 = x_init, yref_k = table[t + k, :ny] (k < N), yref_N = table[t + N, :ny_e], t = offset.
+    Returns (x0 [B, nx], yref [B, N*ny + ny_e])."""
+    ny, nye = NY[model]
+    offsets = np.asarray(offsets)
+    rows = offsets[:, None] + np.arange(N)[None, :]
+    Y = np.concatenate([table[rows, :ny].reshape(len(offsets), -1), table[offsets + N, :nye]], axis=1)
+    return np.asarray(x_init, dtype=np.float64), Y
+
+
 class ClosedLoop:
     """Device closed loop of `batch` instances of `model` on one GPU."""
 
@@ -128,6 +142,14 @@ class ClosedLoop:
             raise NmpcError(f"nmpc_closed_loop_stats: {self.lib.nmpc_last_error(self.solver._h).decode()}")
         return {"cost_sum": out[0], "aed_sum": out[1], "failed": out[2], "instance_steps": out[3],
                 "solve_kernel_ms": out[4], "solve_launches": int(out[5]), "mean_qp_iter": out[6]}
+
+    def instance_stats(self):
+        """Per-instance [cost sum, AED numerator, failed solves, steps] (batch x 4)."""
+        out = np.zeros((self.batch, 4))
+        rc = self.lib.nmpc_closed_loop_instance_stats(self.solver._h, _lib.dptr(out), out.size)
+        if rc != 0:
+            raise NmpcError(f"nmpc_closed_loop_instance_stats: {self.lib.nmpc_last_error(self.solver._h).decode()}")
+        return out
 
     def state(self):
         out = np.zeros((self.batch, self.solver.nx))

@@ -1095,6 +1095,8 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
         if (r < 0) return r;
     }
     h->cl_last_launches = steps;
+    // the loop rewrote the device x0 / yref: the next nmpc_solve re-uploads the host-staged inputs
+    h->x0_dirty = h->yref_dirty = true;
     if (sync) {
         hipError_t e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_run");
@@ -1127,6 +1129,19 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
     for (int b = 0; b < h->batch; b++) mean += it[b];
     v[6] = mean / h->batch;
     for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+    return 0;
+}
+
+int nmpc_closed_loop_instance_stats(nmpc_solver *h, double *out, size_t count)
+{
+    if (!h || !out) return NMPC_EINVAL;
+    if (!h->cl_ready) return h->fail(NMPC_ESTATE, "nmpc_closed_loop_instance_stats: closed loop not initialised");
+    if (count != (size_t)h->batch * 4)
+        return h->fail(NMPC_EINVAL, "nmpc_closed_loop_instance_stats: needs batch*4 values");
+    hipSetDevice(h->device);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, h->d_acc, count * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_instance_stats");
     return 0;
 }
 

@@ -25,16 +25,24 @@ def rank_workload(model, N, per_rank, world, rank, seed=42):
 
 
 def reduce_run(dist, stats, elapsed, kernel_ms, device=None):
-    """SUM-reduce `stats` (1-D float array) and MAX-reduce (elapsed, kernel_ms) over ranks.
+    """SUM-reduce `stats` (1-D float array) and MAX-reduce `elapsed` and `kernel_ms` (scalars, or
+    equal-length arrays: one entry per timed region, reduced elementwise) over ranks.
     `dist` is torch.distributed (initialised) or None for a single process; `device` is the
     tensor device the backend needs ("cuda" for RCCL/nccl, None/"cpu" for gloo)."""
     stats = np.asarray(stats, dtype=np.float64)
+    el = np.atleast_1d(np.asarray(elapsed, dtype=np.float64))
+    km = np.atleast_1d(np.asarray(kernel_ms, dtype=np.float64))
+    scalar = np.ndim(elapsed) == 0
+
+    def out(e, k):
+        return (float(e[0]), float(k[0])) if scalar else (e, k)
+
     if dist is None:
-        return stats, float(elapsed), float(kernel_ms)
+        return (stats,) + out(el, km)
     import torch
     t = torch.tensor(stats, dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    m = torch.tensor([float(elapsed), float(kernel_ms)], dtype=torch.float64, device=device)
+    m = torch.tensor(np.concatenate([el, km]), dtype=torch.float64, device=device)
     dist.all_reduce(m, op=dist.ReduceOp.MAX)
     m = m.cpu().numpy()
-    return t.cpu().numpy(), float(m[0]), float(m[1])
+    return (t.cpu().numpy(),) + out(m[:el.size], m[el.size:])

@@ -219,6 +219,9 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync);
  * out[4] total device ms of the solve kernel over the last run (HIP events around each launch),
  * out[5] solve launches in the last run, out[6] mean qp_iter of the last step */
 int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n);
+/* per-instance accumulators, batch*4: [cost sum, AED numerator, failed solves, steps] of each
+ * instance (the Monte-Carlo distribution behind nmpc_closed_loop_stats' sums) */
+int nmpc_closed_loop_instance_stats(nmpc_solver *h, double *out, size_t count);
 /* current closed-loop states, batch*nx */
 int nmpc_closed_loop_get_state(nmpc_solver *h, double *out, size_t count);
 

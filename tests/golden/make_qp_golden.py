@@ -7,8 +7,10 @@ Inputs are seeded synthetic instances built on the reference's own circle table
 the seed-42 noise stream (main.py:44). Expected outputs are the oracle's KKT-certified
 exact QP solutions (oracle/qp.py) and its closed-loop restatement (oracle/closed_loop.py).
 These fixtures pin the HIP engine to the oracle; the oracle itself is pinned to the
-reference through the fixtures of make_golden.py (acados is absent: QP parity vs acados
-is unpinned).
+reference through the fixtures of make_golden.py and to acados's own recorded run through
+tests/golden/reference_plots.npz (extract_reference_plots.py).
+
+    python tests/golden/make_qp_golden.py [qp] [closed_loop]
 """
 import os
 import sys
@@ -56,7 +58,7 @@ def perturbed_x0(name, xr, t, rng):
     return x0
 
 
-def main():
+def qp_cases():
     out = {}
     rng = np.random.default_rng(20251121)
     for name, N in CASES:
@@ -83,25 +85,41 @@ def main():
         out[key + "_cost"] = np.array(COST)
         print(key, "done")
     np.savez_compressed(os.path.join(HERE, "qp_cases.npz"), **out)
+    print("wrote qp_cases.npz")
 
-    # closed loops of main.py (seed 42 noise stream, x0 = [1, 0, 0, 0.62]), first 60 steps
+
+def closed_loops():
+    """The whole seed-42 main.py run (main.py:43-46): force for all 500 steps
+    (params.py:119), then jerk continuing the same noise stream, x0 = [1, 0, 0, 0.62], at the
+    reference default N_horizon = 30 (params.py:121) and at the BASELINE N = 20. Stored per
+    run: Xsim (501 x 4), the controller inputs U, the plant inputs (theta, F_d), a, the
+    closed-loop cost (controller.py:40-41,54) and the AED (store_results.py:233-236, as
+    main.py:23 computes it from ref[:N_sim] and Xsim[:N_sim])."""
     noise = np.load(os.path.join(HERE, "noise_seed42.npy"))
+    refs = np.load(os.path.join(HERE, "circle_ref.npz"))
     cl = {}
     for N in (20, 30):
-        refs = np.load(os.path.join(HERE, "circle_ref.npz"))
         ref = refs[f"nh{N}_nx6"]
         x0 = np.array([1.0, 0, 0, 0.62])
         ns = CL.NoiseStream(noise)
-        c, X, a, Up, Uc = CL.force_follow_trajectory(models.force_model(N), ref[:, :4], ref[:, 4:6], x0, ns,
-                                                     n_steps=60)
-        cl[f"force_N{N}_X"], cl[f"force_N{N}_U"], cl[f"force_N{N}_Uplant"], cl[f"force_N{N}_cost"] = X, Uc, Up, c
-        c, X, a, Up, Uc = CL.jerk_follow_trajectory(models.jerk_model(N), ref[:, :6], ref[:, 6:], x0, ns,
-                                                    n_steps=60)
-        cl[f"jerk_N{N}_X"], cl[f"jerk_N{N}_U"], cl[f"jerk_N{N}_Uplant"], cl[f"jerk_N{N}_cost"] = X, Uc, Up, c
-        cl[f"jerk_N{N}_a"] = a
+        for name, run, xr, ur in (("force", CL.force_follow_trajectory, ref[:, :4], ref[:, 4:6]),
+                                  ("jerk", CL.jerk_follow_trajectory, ref[:, :6], ref[:, 6:])):
+            c, X, a, Up, Uc = run(models.MODELS[name](N), xr, ur, x0, ns)
+            k = f"{name}_N{N}"
+            cl[k + "_X"], cl[k + "_U"], cl[k + "_Uplant"], cl[k + "_a"], cl[k + "_cost"] = X, Uc, Up, a, c
+            cl[k + "_aed"] = CL.calc_aed(ref[:500, :2], X[:500, :2])
         cl[f"noise_used_N{N}"] = np.array(ns.i)
+        print("closed loops N", N, "done")
     np.savez_compressed(os.path.join(HERE, "closed_loop.npz"), **cl)
-    print("wrote qp_cases.npz, closed_loop.npz")
+    print("wrote closed_loop.npz")
+
+
+def main():
+    what = sys.argv[1:] or ["qp", "closed_loop"]
+    if "qp" in what:
+        qp_cases()
+    if "closed_loop" in what:
+        closed_loops()
 
 
 if __name__ == "__main__":

@@ -38,7 +38,7 @@ def test_value_matches_step_time(line):
 
 def test_roofline_fraction(line):
     r = line["roofline"]
-    assert r["unit"] in ("GB/s", "TFLOP/s") and r["bound"] in ("hbm", "mfma")
+    assert r["unit"] in ("GB/s", "TFLOP/s") and r["bound"] in ("hbm", "mfma", "valu_fp64", "valu_fp32")
     assert math.isclose(r["frac"], r["achieved"] / r["peak"], rel_tol=1e-9)
     # achieved = algorithmic flops per launch / kernel duration
     assert math.isclose(r["achieved"], r["flops_per_launch"] / (r["kernel_ms"] * 1e-3) / 1e12, rel_tol=1e-6)

@@ -1,6 +1,12 @@
-"""GPU closed-loop parity: the reference's follow_trajectory loops (force/jerk) driven through
-the façade (every QP solve and plant step on the GPU) against the oracle's restatement
-(tests/golden/closed_loop.npz: first 60 steps of main.py, seed-42 noise, x0=[1,0,0,0.62])."""
+"""GPU closed-loop parity: the reference's follow_trajectory loops (force/jerk) with every QP
+solve and plant step on the GPU, over the whole seed-42 main.py run (500 steps, force then
+jerk on one noise stream, x0 = [1, 0, 0, 0.62], main.py:43-46), against
+  * the oracle's restatement (tests/golden/closed_loop.npz, make_qp_golden.py closed_loop), and
+  * for jerk at the reference default N = 30, acados's own recorded run
+    (tests/golden/reference_plots.npz, extracted from experiment_data/img/*.pdf).
+Bars: states 1e-6 absolute (the solve bar, BASELINE north_star), closed-loop cost and AED 1e-6
+relative (f4: controller.py:40-41,54, store_results.py:233-236).
+"""
 import os
 
 import numpy as np
@@ -9,6 +15,8 @@ import pytest
 from drone_attitude_control_amd import controllers
 
 pytestmark = pytest.mark.gpu
+
+STEPS = 500
 
 
 @pytest.fixture(scope="module")
@@ -25,48 +33,89 @@ def stream(noise):
 
 @pytest.mark.parametrize("N", [20, 30])
 def test_force_and_jerk_closed_loop(data, N):
+    """The façade loop (nmpc_set / nmpc_solve / nmpc_get per step, nmpc_sim_plant per plant step)."""
     cl, noise, refs = data
     ref = refs[f"nh{N}_nx6"]
     draw = stream(noise)
     x0 = np.array([1.0, 0, 0, 0.62])
     c, X, a, Up = controllers.force_follow_trajectory(ref[:, :4], ref[:, 4:6], x0, draw, verbose=False,
-                                                      N=N, n_steps=60)
+                                                      N=N, n_steps=STEPS)
     assert np.abs(X - cl[f"force_N{N}_X"]).max() < 1e-6
     assert np.abs(Up - cl[f"force_N{N}_Uplant"]).max() < 1e-6
     assert c == pytest.approx(float(cl[f"force_N{N}_cost"]), rel=1e-6)
+    assert controllers.calc_aed(ref[:STEPS, :2], X[:STEPS, :2]) == pytest.approx(float(cl[f"force_N{N}_aed"]),
+                                                                                 rel=1e-6)
     c, X, a, Up = controllers.jerk_follow_trajectory(ref[:, :6], ref[:, 6:], x0, draw, verbose=False,
-                                                     N=N, n_steps=60)
+                                                     N=N, n_steps=STEPS)
     assert np.abs(X - cl[f"jerk_N{N}_X"]).max() < 1e-6
     assert np.abs(a - cl[f"jerk_N{N}_a"]).max() < 1e-6
     assert c == pytest.approx(float(cl[f"jerk_N{N}_cost"]), rel=1e-6)
+    assert controllers.calc_aed(ref[:STEPS, :2], X[:STEPS, :2]) == pytest.approx(float(cl[f"jerk_N{N}_aed"]),
+                                                                                 rel=1e-6)
+
+
+def _device_loop(model, N, refs_noise, B=5):
+    """nmpc_closed_loop_* (prepare -> solve -> advance, all on the device) for a batch whose
+    instance 0 is main.py's run with the seed-42 noise stream injected (force draws 0..499,
+    jerk 500..999); the other instances start elsewhere on the circle."""
+    from drone_attitude_control_amd.batched import ClosedLoop, reference_table
+    noise = refs_noise
+    table = reference_table(model, N)
+    offsets = np.array([0, 10, 100, 250, 400][:B], dtype=np.int32)
+    x = table[offsets, :4].copy()
+    x[0] = [1.0, 0, 0, 0.62]
+    if model == "jerk":
+        x = np.hstack([x, np.tile([0.0, 9.81], (B, 1))])
+    nt = np.zeros((B, STEPS))
+    nt[0] = noise[:STEPS] if model == "force" else noise[STEPS:2 * STEPS]
+    return ClosedLoop(model, B, N=N, table=table, offsets=offsets, x_init=x, noise_table=nt)
 
 
 @pytest.mark.parametrize("N", [20, 30])
-def test_device_closed_loop_matches_oracle(data, N):
-    """nmpc_closed_loop_* (prepare -> solve -> advance, all on the device) for a batch whose
-    instance 0 is main.py's run with the seed-42 noise stream injected; other instances get
-    the same inputs shifted in start row. Instance 0 must match the oracle's closed loop."""
-    from drone_attitude_control_amd.batched import ClosedLoop, reference_table
+@pytest.mark.parametrize("model", ["force", "jerk"])
+def test_device_closed_loop_matches_oracle(data, N, model):
+    """All 500 steps on the device; instance 0's states after every step and its accumulated
+    closed-loop cost / AED numerator (f4) against the oracle."""
     cl_gold, noise, refs = data
-    for model, nz in (("force", slice(0, 60)), ("jerk", slice(60, 120))):
-        table = reference_table(model, N)
-        B = 5
-        offsets = np.array([0, 10, 100, 250, 400], dtype=np.int32)
-        x = table[offsets, :4].copy()
-        x[0] = [1.0, 0, 0, 0.62]
-        if model == "jerk":
-            x = np.hstack([x, np.tile([0.0, 9.81], (B, 1))])
-        nt = np.zeros((B, 60))
-        nt[0] = noise[nz]
-        loop = ClosedLoop(model, B, N=N, table=table, offsets=offsets, x_init=x, noise_table=nt)
-        states = []
-        for _ in range(60):
-            loop.run(1)
-            states.append(loop.state()[0, :4].copy())
-        X = np.array(states)
-        assert np.abs(X - cl_gold[f"{model}_N{N}_X"][1:61]).max() < 1e-6
-        st = loop.stats()
-        assert st["failed"] == 0 and st["instance_steps"] == B * 60
+    loop = _device_loop(model, N, noise)
+    states = []
+    for _ in range(STEPS):
+        loop.run(1)
+        states.append(loop.state()[0, :4].copy())
+    X = np.array(states)
+    Xg = cl_gold[f"{model}_N{N}_X"]
+    assert np.abs(X - Xg[1:STEPS + 1]).max() < 1e-6
+    st = loop.stats()
+    assert st["failed"] == 0 and st["instance_steps"] == 5 * STEPS
+    per = loop.instance_stats()
+    assert per[0, 0] == pytest.approx(float(cl_gold[f"{model}_N{N}_cost"]), rel=1e-6)
+    assert per[0, 1] / (STEPS * 2) == pytest.approx(float(cl_gold[f"{model}_N{N}_aed"]), rel=1e-6)
+    assert per[0, 3] == STEPS
+    assert st["cost_sum"] == pytest.approx(per[:, 0].sum(), rel=1e-12)
+
+
+def test_device_jerk_loop_matches_acados_run(data, golden_dir):
+    """Instance 0 of the device jerk loop (N = 30, the reference default) against the plotted
+    acados run itself: positions, velocities and accelerations at every plotted sample."""
+    _, noise, _ = data
+    plots = np.load(os.path.join(golden_dir, "reference_plots.npz"))
+    loop = _device_loop("jerk", 30, noise, B=1)
+    states = [loop.state()[0].copy()]
+    for _ in range(STEPS - 1):
+        loop.run(1)
+        states.append(loop.state()[0].copy())
+    S = np.array(states)          # S[t] = Xsim[t] (+ a before step t)
+    fig = "example_jerk_trajectory_component"
+    for j, col, tol in ((0, 0, 1e-6), (1, 1, 1e-6), (4, 2, 1e-6), (5, 3, 1e-6)):
+        p = plots[f"{fig}__p{j}"]
+        i = np.round(p[:, 0] / 0.02).astype(int)
+        assert np.abs(S[i, col] - p[:, 1]).max() < tol, j
+    # a[t] is the acceleration after step t = the state's a-part before step t + 1
+    for j, col in ((10, 4), (11, 5)):
+        p = plots[f"{fig}__p{j}"]
+        i = np.round(p[:, 0] / 0.02).astype(int)
+        ok = i < STEPS - 1
+        assert np.abs(S[i[ok] + 1, col] - p[ok, 1]).max() < 1e-5
 
 
 @pytest.mark.parametrize("model", ["force", "quad13"])
@@ -101,3 +150,24 @@ def test_batched_closed_loop_survives_infeasible_steps():
     assert st["failed"] >= 1
     assert np.isfinite(st["cost_sum"]) and np.isfinite(st["aed_sum"])
     assert np.isfinite(loop.state()).all()
+
+
+def test_solve_after_closed_loop_uses_host_inputs(data):
+    """After a device closed loop rewrote the engine's x0 / yref buffers, a plain nmpc_solve
+    with no new set() calls solves the host-staged problem again, not the loop's last window."""
+    from oracle import models, qp
+    cl_gold, noise, refs = data
+    loop = _device_loop("force", 20, noise, B=1)
+    s = loop.solver
+    ref = refs["nh20_nx6"]
+    yref, ye = qp.yref_window(ref[:, :4], ref[:, 4:6], 7, 20)
+    x0 = ref[7, :4] + 0.01
+    s.set_batch("x0", x0[None])
+    s.set_batch("yref", np.concatenate([yref.ravel(), ye])[None])
+    assert s.solve() == 0
+    u1 = s.get_batch("u").copy()
+    loop.run(3)
+    assert s.solve() == 0
+    assert np.array_equal(s.get_batch("u"), u1)
+    o = qp.solve_ocp(models.force_model(20), x0, yref, ye)
+    assert np.abs(u1[0] - o["U"]).max() < 1e-6

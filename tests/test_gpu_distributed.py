@@ -1,0 +1,52 @@
+"""BASELINE config 4 in miniature on the one-GPU box: the force model's closed loop sharded over
+two ranks (torch.distributed.run, gloo backend — RCCL needs one GPU per rank, and the 8-GPU
+run is the driver's), each rank running the device closed loop (batched.ClosedLoop) on its
+slice of the global batch, then bench.py's end-of-run reduction. The reduced statistics must
+equal a single-process run over the same global batch: instances are keyed by their global id
+(sharding.rank_workload, Philox noise by global instance), so sharding changes nothing but the
+summation order."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(args, world):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
+    if world > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
+               *args, "--dist-backend", "gloo"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+
+
+@pytest.mark.timeout(300)
+def test_force_two_ranks_reduce_equals_one_process():
+    common = ["--model", "force", "--steps", "4", "--warmup", "2", "--repeats", "2", "--no-cpu-baseline"]
+    two = _bench(common + ["--gpus", "2", "--batch", "2048"], 2)
+    one = _bench(common + ["--gpus", "1", "--batch", "4096"], 1)
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == one["config"]["global_batch"] == 4096
+    a, b = two["closed_loop"], one["closed_loop"]
+    assert a["instance_steps"] == b["instance_steps"] == 4096 * (2 + 2 * 4)
+    assert a["failed_solves"] == b["failed_solves"]
+    assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=1e-10)
+    assert a["aed"] == pytest.approx(b["aed"], rel=1e-10)
+    assert two["value"] > 0 and len(two["timing"]["region_ms"]) == 2

@@ -163,13 +163,20 @@ def test_c_riccati_threads_deterministic(golden_dir):
 
 
 def test_closed_loop_oracle_matches_golden(golden_dir):
+    """The oracle reproduces the committed 500-step main.py goldens (force then jerk on one
+    noise stream, N = 20)."""
     d = np.load(os.path.join(golden_dir, "closed_loop.npz"))
     noise = np.load(os.path.join(golden_dir, "noise_seed42.npy"))
     ref = trajectory.gen_circle_traj(500, 20, 6, 2)
     ns = CL.NoiseStream(noise)
-    c, X, a, Up, Uc = CL.force_follow_trajectory(models.force_model(20), ref[:, :4], ref[:, 4:6],
-                                                 np.array([1.0, 0, 0, 0.62]), ns, n_steps=60)
+    x0 = np.array([1.0, 0, 0, 0.62])
+    c, X, a, Up, Uc = CL.force_follow_trajectory(models.force_model(20), ref[:, :4], ref[:, 4:6], x0, ns)
+    assert X.shape == (501, 4) and ns.i == 500
     assert np.allclose(X, d["force_N20_X"], atol=1e-9) and c == pytest.approx(float(d["force_N20_cost"]), rel=1e-9)
+    assert CL.calc_aed(ref[:500, :2], X[:500, :2]) == pytest.approx(float(d["force_N20_aed"]), rel=1e-9)
+    c, X, a, Up, Uc = CL.jerk_follow_trajectory(models.jerk_model(20), ref[:, :6], ref[:, 6:], x0, ns)
+    assert ns.i == 1000 and int(d["noise_used_N20"]) == 1000
+    assert np.allclose(X, d["jerk_N20_X"], atol=1e-9) and c == pytest.approx(float(d["jerk_N20_cost"]), rel=1e-9)
 
 
 def test_converters_and_plant():

@@ -42,6 +42,10 @@ def _worker(rank, world, port, out):
         for model, N in MODELS:
             table, offsets, x, base = rank_workload(model, N, PER_RANK, world, rank)
             red, el, km = reduce_run(dist, host_stats(table, offsets, x), elapsed=1.0 + rank, kernel_ms=2.0 * (rank + 1))
+            # per-region timings (bench.py --repeats): elementwise MAX over ranks
+            _, el_r, km_r = reduce_run(dist, np.zeros(1), np.array([1.0 + rank, 5.0 - rank]),
+                                       np.array([0.5 * rank, 1.0]))
+            assert np.array_equal(el_r, [1.0 + world - 1, 5.0]) and np.array_equal(km_r, [0.5 * (world - 1), 1.0])
             res[model] = (red, el, km, base, offsets, x)
         out[rank] = res
     finally:
@@ -62,6 +66,8 @@ def test_single_process_reduce_is_identity():
     s = np.array([1.0, 2.0, 3.0, 4.0])
     red, el, km = reduce_run(None, s, 1.5, 0.5)
     assert np.array_equal(red, s) and el == 1.5 and km == 0.5
+    red, el, km = reduce_run(None, s, np.array([1.0, 2.0]), np.array([3.0, 4.0]))
+    assert np.array_equal(el, [1.0, 2.0]) and np.array_equal(km, [3.0, 4.0])
 
 
 @pytest.mark.timeout(300)
