@@ -222,6 +222,15 @@ struct nmpc_solver {
     std::vector<hipEvent_t> cl_events;
     double cl_last_ms = 0.0;
     double cost_s = 1.0;  // stage cost factor (time step or 1)
+    // condensed family (nmpc_cond.hip): states eliminated on the host, MFMA Hessian GEMMs
+    bool cond = false;
+    int cond_wpb = 1;
+    size_t cond_lds = 0;
+    nmpc::CondHost ch;
+    void *d_cond = nullptr;   // typed blob: Gx, H0, H0t, Fx, Fy, fc, Phx, dx, lox, hix, lou, hiu, Gall, Phall, dall
+    int *d_cond_i = nullptr;  // xcols, rstart, ks
+    size_t co[15] = {0};
+    size_t ci[3] = {0};
 
     size_t ystride() const { return (size_t)N * ny + ny_e; }
     size_t esz() const { return precision == NMPC_FP64 ? sizeof(double) : sizeof(float); }
@@ -245,7 +254,7 @@ void free_all(nmpc_solver *h)
     hipSetDevice(h->device);
     for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
-                    (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles})
+                    (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -254,8 +263,51 @@ void free_all(nmpc_solver *h)
 }
 
 template <typename T>
+int launch_cond(nmpc_solver *h, hipEvent_t e0, hipEvent_t e1)
+{
+    nmpc::CondParams<T> p{};
+    const nmpc::CondHost &c = h->ch;
+    p.B = h->batch;
+    p.N = h->N;
+    p.nx = h->nx;
+    p.nu = h->nu;
+    p.n = c.n;
+    p.nb = c.nb;
+    p.mx = c.mx;
+    p.ldg = c.ldg;
+    p.nY = c.nY;
+    p.ny = h->ny;
+    p.yref_is_z = h->yref_is_z;
+    p.max_iter = h->max_iter;
+    p.wave_elems = (int)nmpc::cond_wave_elems<T>(c.nb, c.ldg);
+    p.tol_comp = (T)h->tol_comp;
+    p.tol_res = (T)h->tol_res;
+    p.mu0 = (T)h->mu0;
+    p.inv_m = (T)h->inv_m;
+    const T *b = (const T *)h->d_cond;
+    const T **f[15] = {&p.Gx, &p.H0, &p.H0t, &p.Fx, &p.Fy, &p.fc, &p.Phx, &p.dx, &p.lox, &p.hix,
+                       &p.lou, &p.hiu, &p.Gall, &p.Phall, &p.dall};
+    for (int i = 0; i < 15; i++) *f[i] = b + h->co[i];
+    p.xcols = h->d_cond_i + h->ci[0];
+    p.rstart = h->d_cond_i + h->ci[1];
+    p.ks = h->d_cond_i + h->ci[2];
+    p.x0 = (const T *)h->d_x0;
+    p.yref = (const T *)h->d_yref;
+    p.xout = (T *)h->d_x;
+    p.uout = (T *)h->d_u;
+    p.status = h->d_status;
+    p.iters = h->d_iters;
+    hipEventRecord(e0 ? e0 : h->ev0, h->stream);
+    hipError_t e = nmpc::cond_launch<T>(p, h->cond_wpb, h->cond_lds, h->stream);
+    hipEventRecord(e1 ? e1 : h->ev1, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "condensed ipm kernel launch");
+    return 0;
+}
+
+template <typename T>
 int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
+    if (h->cond) return launch_cond<T>(h, e0, e1);
     nmpc::IpmParams<T> p;
     p.B = h->batch;
     p.N = h->N;
@@ -375,14 +427,14 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     if (const char *e = std::getenv("NMPC_IPW")) ipw_req = std::atoi(e);
     h->kidx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, -1, batch, &h->ipw, &h->lds, &h->wpb)
                                      : nmpc::ipm_find<float>(nx, nu, -1, batch, &h->ipw, &h->lds, &h->wpb);
-    if (h->kidx < 0) {
-        std::string msg = "nmpc_create: no compiled kernel for nx=" + std::to_string(nx) + " nu=" + std::to_string(nu);
-        delete h;
-        g_err = msg;
-        return NMPC_EUNSUPPORTED;
+    {
+        // kernel family: NMPC_KERNEL=cond forces the condensed MFMA kernels; they also take any
+        // (nx, nu) without a compiled stage-wise kernel (dimension-generic at run time)
+        const char *kf = std::getenv("NMPC_KERNEL");
+        h->cond = (kf && (kf[0] == 'c' || kf[0] == 'C')) || h->kidx < 0;
     }
     // packing heuristic: keep >= 2 wavefronts per SIMD (1024 SIMDs on MI355X) if possible
-    if (ipw_req <= 0) {
+    if (ipw_req <= 0 && !h->cond) {
         int cand[4] = {8, 4, 2, 1}, chosen = -1;
         for (int ipw : cand) {
             int ip, ld;
@@ -398,7 +450,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         }
         ipw_req = chosen;
     }
-    {
+    if (!h->cond) {
         const int idx = precision == NMPC_FP64 ? nmpc::ipm_find<double>(nx, nu, ipw_req, batch, &h->ipw, &h->lds, &h->wpb)
                                                : nmpc::ipm_find<float>(nx, nu, ipw_req, batch, &h->ipw, &h->lds, &h->wpb);
         if (idx >= 0) h->kidx = idx;
@@ -585,7 +637,30 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
     const size_t model_bytes = off;
-    {
+    if (h->cond) {
+        if (!nmpc::cond_build(nx, nu, N, ny, ny_e, h->A, h->B, h->c, h->H, h->G, h->He, h->Ge, h->lbnd, h->ubnd, h->ch)) {
+            delete h;
+            g_err = "nmpc_create: no compiled kernel for nx=" + std::to_string(nx) + " nu=" + std::to_string(nu) +
+                    " and the condensed kernels need N*nu <= 128 and N*nu + bounded x rows <= 512";
+            return NMPC_EUNSUPPORTED;
+        }
+        // workgroup: the most wavefronts (<= 4) whose LDS (shared Gx + per-wave tiles/vectors) fits
+        const size_t we = precision == NMPC_FP64 ? nmpc::cond_wave_elems<double>(h->ch.nb, h->ch.ldg)
+                                                 : nmpc::cond_wave_elems<float>(h->ch.nb, h->ch.ldg);
+        const size_t gx = (size_t)16 * h->ch.nb * h->ch.ldg;
+        h->cond_wpb = 0;
+        for (int w = 4; w >= 1 && !h->cond_wpb; w--)
+            if ((gx + w * we) * es <= 160 * 1024) h->cond_wpb = w;
+        if (!h->cond_wpb) {
+            delete h;
+            g_err = "nmpc_create: the condensed kernel's LDS need exceeds 160 KB for this OCP";
+            return NMPC_EUNSUPPORTED;
+        }
+        h->cond_lds = (gx + h->cond_wpb * we) * es;
+        h->ipw = 1;
+        h->wpb = h->cond_wpb;
+        h->lds = (int)h->cond_lds;
+    } else {
         // structure-specialised kernel when the model fits one (exact zeros of [A B], diagonal costs)
         std::vector<double> ABh((size_t)nx * nz);
         for (int r = 0; r < nx; r++) {
@@ -595,8 +670,9 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         h->kidx = precision == NMPC_FP64 ? nmpc::ipm_refine<double>(h->kidx, ABh.data(), h->H.data(), h->He.data())
                                          : nmpc::ipm_refine<float>(h->kidx, ABh.data(), h->H.data(), h->He.data());
     }
-    const size_t scratch_bytes = (precision == NMPC_FP64 ? nmpc::ipm_scratch_elems<double>(h->kidx, batch, N)
-                                                         : nmpc::ipm_scratch_elems<float>(h->kidx, batch, N)) * es;
+    const size_t scratch_bytes = h->cond ? 256
+                                         : (precision == NMPC_FP64 ? nmpc::ipm_scratch_elems<double>(h->kidx, batch, N)
+                                                                   : nmpc::ipm_scratch_elems<float>(h->kidx, batch, N)) * es;
     bool ok = hipMalloc(&h->d_model, model_bytes) == hipSuccess &&
               hipMalloc(&h->d_x0, (size_t)batch * nx * es) == hipSuccess &&
               hipMalloc(&h->d_yref, (size_t)batch * h->ystride() * es) == hipSuccess &&
@@ -621,14 +697,15 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     for (int r = 0; r < nx; r++)
         for (int q = 0; q < nz; q++) ABt[q * nx + r] = AB[r * nz + q];
     char *dm = (char *)h->d_model;
-    auto put = [&](size_t o, const std::vector<double> &v) {
+    auto put_at = [&](char *base, size_t o, const std::vector<double> &v) {
         if (f64) {
-            hipMemcpy(dm + o, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice);
+            hipMemcpy(base + o, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice);
         } else {
             std::vector<float> t(v.begin(), v.end());
-            hipMemcpy(dm + o, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice);
+            hipMemcpy(base + o, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice);
         }
     };
+    auto put = [&](size_t o, const std::vector<double> &v) { put_at(dm, o, v); };
     put(h->off_AB, AB);
     put(h->off_ABt, ABt);
     put(h->off_c, h->c);
@@ -638,6 +715,32 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     put(h->off_Ge, h->Ge);
     put(h->off_lb, h->lbnd);
     put(h->off_ub, h->ubnd);
+    if (h->cond) {
+        const nmpc::CondHost &c = h->ch;
+        const std::vector<double> *parts[15] = {&c.Gx, &c.H0, &c.H0t, &c.Fx, &c.Fy, &c.fc, &c.Phx, &c.dx, &c.lox,
+                                                &c.hix, &c.lou, &c.hiu, &c.Gall, &c.Phall, &c.dall};
+        size_t tot = 0;
+        for (int i = 0; i < 15; i++) {
+            h->co[i] = tot;
+            tot += (parts[i]->size() + 63) & ~(size_t)63;
+        }
+        const std::vector<int> *iparts[3] = {&c.xcols, &c.rstart, &c.ks};
+        size_t itot = 0;
+        for (int i = 0; i < 3; i++) {
+            h->ci[i] = itot;
+            itot += (iparts[i]->size() + 63) & ~(size_t)63;
+        }
+        if (hipMalloc(&h->d_cond, tot * es) != hipSuccess || hipMalloc((void **)&h->d_cond_i, itot * sizeof(int)) != hipSuccess) {
+            h->fail(NMPC_ENOMEM, "nmpc_create: device allocation failed (condensed data)");
+            free_all(h);
+            delete h;
+            return NMPC_ENOMEM;
+        }
+        char *cb = (char *)h->d_cond;
+        for (int i = 0; i < 15; i++) put_at(cb, h->co[i] * es, *parts[i]);
+        for (int i = 0; i < 3; i++)
+            hipMemcpy(h->d_cond_i + h->ci[i], iparts[i]->data(), iparts[i]->size() * sizeof(int), hipMemcpyHostToDevice);
+    }
     if ((e = hipDeviceSynchronize()) != hipSuccess) {
         int r = hip_fail(h, e, "model upload");
         free_all(h);
@@ -904,8 +1007,8 @@ int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
     if (!h || !out) return NMPC_EINVAL;
     const int waves = (h->batch + h->ipw - 1) / h->ipw;
     const bool f64 = h->precision == NMPC_FP64;
-    const int kind = f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
-    const int sid = f64 ? nmpc::ipm_structure<double>(h->kidx) : nmpc::ipm_structure<float>(h->kidx);
+    const int kind = h->cond ? 2 : f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
+    const int sid = h->cond ? 0 : f64 ? nmpc::ipm_structure<double>(h->kidx) : nmpc::ipm_structure<float>(h->kidx);
     const int v[6] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid};
     for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
     return 0;

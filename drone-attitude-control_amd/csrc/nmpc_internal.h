@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include <vector>
+
 namespace nmpc {
 
 // Kernel parameters of the batched IPM solve (nmpc_ipm.hip). All pointers are device
@@ -56,6 +58,51 @@ template <typename T>
 int ipm_refine(int idx, const double *AB, const double *H, const double *He);
 template <typename T>
 int ipm_structure(int idx);
+
+// Condensed IPM (nmpc_cond.hip): one wavefront per instance, states eliminated on the host
+// (nmpc_cond_host.cpp). Matrices are shared by every instance; layouts noted per field.
+template <typename T>
+struct CondParams {
+    int B, N, nx, nu, n, nb, mx, ldg, nY, ny, yref_is_z, max_iter;
+    int wave_elems;    // LDS elements per wavefront (cond_wave_elems)
+    T tol_comp, tol_res, mu0, inv_m;
+    const T *Gx;       // [16 nb][ldg] Gamma_x column-major (rows = bounded x rows), zero padded
+    const T *H0;       // [n][n] condensed Hessian, column-major
+    const T *H0t;      // lower 16x16 tiles of H0 (tile I(I+1)/2 + J, column-major within the tile)
+    const T *Fx;       // [nx][n]  f = fc + Fx x0 + Fy yref (column-major)
+    const T *Fy;       // [nY][n]
+    const T *fc;       // [n]
+    const T *Phx;      // [nx][mx] x-row offsets xf = dx + Phx x0 (column-major)
+    const T *dx;       // [mx]
+    const T *lox, *hix;   // [mx] x-row bounds (|b| >= 1e20: none)
+    const T *lou, *hiu;   // [n] input bounds
+    const int *xcols;  // [mx] nonzero columns of each x row (k nu)
+    const int *rstart; // [n] first x row with a nonzero in column i
+    const int *ks;     // [nb] first 4-row step of Gx with a nonzero in tile column block I
+    const T *Gall;     // [n][(N+1) nx] outputs X = Phall x0 + dall + Gall U (column-major)
+    const T *Phall;    // [nx][(N+1) nx]
+    const T *dall;     // [(N+1) nx]
+    const T *x0;       // [B][nx]
+    const T *yref;     // [B][nY]
+    T *xout, *uout;
+    int *status, *iters;
+};
+template <typename T>
+hipError_t cond_launch(const CondParams<T> &p, int wpb, size_t lds_bytes, hipStream_t s);
+template <typename T>
+size_t cond_wave_elems(int nb, int ldg);
+
+// host condensing of the stage-wise QP data (double); returns false if the dims are outside
+// what the condensed kernels are compiled for (n <= 128, n + mx <= 512)
+struct CondHost {
+    int n = 0, nb = 0, mx = 0, ldg = 0, nY = 0;
+    std::vector<double> Gx, H0, H0t, Fx, Fy, fc, Phx, dx, lox, hix, lou, hiu, Gall, Phall, dall;
+    std::vector<int> xcols, rstart, ks;
+};
+bool cond_build(int nx, int nu, int N, int ny, int ny_e, const std::vector<double> &A, const std::vector<double> &Bm,
+                const std::vector<double> &c, const std::vector<double> &H, const std::vector<double> &G,
+                const std::vector<double> &He, const std::vector<double> &Ge, const std::vector<double> &lbnd,
+                const std::vector<double> &ubnd, CondHost &out);
 
 // closed-loop step kernels (nmpc_closed_loop.hip)
 template <typename T>
