@@ -26,10 +26,11 @@
 // (lower triangle, 16x16 column-major tiles of pitch 17) and a few broadcast vectors in LDS, and
 // its constraint rows (64 per register chunk: slacks, multipliers, steps) and the n-vectors
 // (lanes = rows) in registers. Reductions over the wavefront are DPP row rotations + 4
-// readlanes. Termination, status codes and the failure semantics follow the Riccati kernels:
-// mu <= tol_comp and theta r0 <= tol_res (theta = prod(1 - alpha): the linear residuals
-// contract exactly by 1 - alpha), status 2 after max_iter, 4 on a non-positive pivot (the
-// iterate of the start of that iteration is returned) or a non-finite mu.
+// readlanes. Primal and dual steps have separate lengths. Termination: mu <= tol_comp and
+// max |residual| <= tol_res (dual rd = H0 U + f - C' lambda, primal CU - lo - t_l, hi - CU - t_u,
+// evaluated at every iterate); status codes and failure semantics follow the Riccati kernels:
+// status 2 after max_iter, 4 on a non-positive pivot (the iterate of the start of that
+// iteration is returned) or a non-finite mu.
 
 #include <hip/hip_runtime.h>
 
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
     T invd[UC];
 #pragma unroll
     for (int c = 0; c < UC; c++) invd[c] = 0;
-    T theta = 1, r0 = 0;
+    T rres = 0;   // max |residual| (dual rd, primal rpl / rpu) at the current iterate
     int status = 2, iters = 0;
     const int ksteps = mxp >> 2;
 
@@ -391,16 +392,19 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
             dlu[c] = hu[c] ? (-rcu[c] - lu[c] * dtu[c]) / tu[c] : T(0);
         }
     };
-    auto max_step = [&](const T (&dtl)[RC], const T (&dtu)[RC], const T (&dll)[RC], const T (&dlu)[RC]) {
-        T a = 1;
+    // largest primal (slacks) and dual (multipliers) steps that keep them non-negative
+    auto max_step = [&](const T (&dtl)[RC], const T (&dtu)[RC], const T (&dll)[RC], const T (&dlu)[RC], T &ap, T &ad) {
+        ap = 1;
+        ad = 1;
 #pragma unroll
         for (int c = 0; c < RC; c++) {
-            if (hl[c] && dtl[c] < T(0)) a = fmin(a, -tl[c] / dtl[c]);
-            if (hl[c] && dll[c] < T(0)) a = fmin(a, -ll[c] / dll[c]);
-            if (hu[c] && dtu[c] < T(0)) a = fmin(a, -tu[c] / dtu[c]);
-            if (hu[c] && dlu[c] < T(0)) a = fmin(a, -lu[c] / dlu[c]);
+            if (hl[c] && dtl[c] < T(0)) ap = fmin(ap, -tl[c] / dtl[c]);
+            if (hu[c] && dtu[c] < T(0)) ap = fmin(ap, -tu[c] / dtu[c]);
+            if (hl[c] && dll[c] < T(0)) ad = fmin(ad, -ll[c] / dll[c]);
+            if (hu[c] && dlu[c] < T(0)) ad = fmin(ad, -lu[c] / dlu[c]);
         }
-        return wred(a, vmin);
+        ap = wred(ap, vmin);
+        ad = wred(ad, vmin);
     };
 
     for (int it = 0;; it++) {
@@ -430,17 +434,15 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
                 rpl[c] = hl[c] ? cu[c] - lo[c] - tl[c] : T(0);
                 rpu[c] = hu[c] ? hi[c] - cu[c] - tu[c] : T(0);
             }
-            if (it == 0) {
-                T m = 0;
+            T m = 0;
 #pragma unroll
-                for (int c = 0; c < UC; c++) m = fmax(m, fabs(rd[c]));
+            for (int c = 0; c < UC; c++) m = fmax(m, fabs(rd[c]));
 #pragma unroll
-                for (int c = 0; c < RC; c++) m = fmax(m, fmax(fabs(rpl[c]), fabs(rpu[c])));
-                r0 = wred(m, vmax);
-            }
+            for (int c = 0; c < RC; c++) m = fmax(m, fmax(fabs(rpl[c]), fabs(rpu[c])));
+            rres = wred(m, vmax);
         }
-        const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
-        if (conv || !isfinite(mu) || !isfinite(theta)) {
+        const bool conv = mu <= p.tol_comp && rres <= p.tol_res;
+        if (conv || !isfinite(mu) || !isfinite(rres)) {
             status = conv ? 0 : 4;
             iters = it;
             break;
@@ -551,13 +553,14 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
             rcu[c] = lu[c] * tu[c];
         }
         solve(rcl, rcu, cd, atl, atu, all_, alu);
-        const T a_aff = max_step(atl, atu, all_, alu);
+        T ap, ad;
+        max_step(atl, atu, all_, alu, ap, ad);
         T mu_aff;
         {
             T s = 0;
 #pragma unroll
             for (int c = 0; c < RC; c++)
-                s += (tl[c] + a_aff * atl[c]) * (ll[c] + a_aff * all_[c]) + (tu[c] + a_aff * atu[c]) * (lu[c] + a_aff * alu[c]);
+                s += (tl[c] + ap * atl[c]) * (ll[c] + ad * all_[c]) + (tu[c] + ap * atu[c]) * (lu[c] + ad * alu[c]);
             mu_aff = wred(s, sum) * p.inv_m;
         }
         const T sg = mu > T(0) ? fmax(mu_aff, T(0)) / mu : T(0);
@@ -570,25 +573,27 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
         }
         T dtl[RC], dtu[RC], dll[RC], dlu[RC];
         solve(rcl, rcu, cd, dtl, dtu, dll, dlu);
-        const T a = fmin(T(1), T(0.995) * max_step(dtl, dtu, dll, dlu));
-        // ---- step
+        max_step(dtl, dtu, dll, dlu, ap, ad);
+        ap = fmin(T(1), T(0.995) * ap);
+        ad = fmin(T(1), T(0.995) * ad);
+        // ---- step: separate primal and dual lengths (one common length stalls on some
+        //      instances: mu cycles while the primal residual converges)
 #pragma unroll
         for (int c = 0; c < UC; c++) {
             const int i = lane + 64 * c;
-            if (i < n) Uv[i] = fma(a, Sv[i], Uv[i]);
+            if (i < n) Uv[i] = fma(ap, Sv[i], Uv[i]);
         }
         T s = 0;
 #pragma unroll
         for (int c = 0; c < RC; c++) {
-            cu[c] = fma(a, cd[c], cu[c]);
-            tl[c] = hl[c] ? fma(a, dtl[c], tl[c]) : T(1);
-            tu[c] = hu[c] ? fma(a, dtu[c], tu[c]) : T(1);
-            ll[c] = hl[c] ? fma(a, dll[c], ll[c]) : T(0);
-            lu[c] = hu[c] ? fma(a, dlu[c], lu[c]) : T(0);
+            cu[c] = fma(ap, cd[c], cu[c]);
+            tl[c] = hl[c] ? fma(ap, dtl[c], tl[c]) : T(1);
+            tu[c] = hu[c] ? fma(ap, dtu[c], tu[c]) : T(1);
+            ll[c] = hl[c] ? fma(ad, dll[c], ll[c]) : T(0);
+            lu[c] = hu[c] ? fma(ad, dlu[c], lu[c]) : T(0);
             s += ll[c] * tl[c] + lu[c] * tu[c];
         }
         mu = wred(s, sum) * p.inv_m;
-        theta *= T(1) - a;
         CSYNC();
     }
 
