@@ -410,7 +410,7 @@ class AcadosOcpSolver:
         out = (ctypes.c_int * 6)()
         self._check(self.lib.nmpc_get_launch_info(self._h, out, 6), "launch_info")
         return {"instances_per_wave": out[0], "workgroups": out[1], "threads": out[2], "lds_bytes": out[3],
-                "kernel": {0: "ipm_kernel", 1: "ipm_lpc_kernel", 2: "cond_ipm_kernel"}.get(out[4], str(out[4])),
+                "kernel": {0: "ipm_kernel", 1: "ipm_lpc_kernel", 2: "cond_ipm_kernel", 3: "ipm_lpi_kernel"}.get(out[4], str(out[4])),
                 "structure": {0: "dense", 1: "force", 2: "jerk", 3: "quad13"}.get(out[5], str(out[5]))}
 
     def discrete_model(self):

@@ -11,7 +11,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "lib", "libnmpc_hip.so")
-SOURCES = ["nmpc_ipm.hip", "nmpc_ipm_lpc.hip", "nmpc_cond.hip", "nmpc_plant.hip", "nmpc_closed_loop.hip",
+SOURCES = ["nmpc_ipm.hip", "nmpc_ipm_lpc.hip", "nmpc_ipm_lpi.hip", "nmpc_cond.hip", "nmpc_plant.hip", "nmpc_closed_loop.hip",
            "nmpc_api.cpp", "nmpc_cond_host.cpp"]
 HEADERS = ["nmpc_internal.h", "nmpc_lpc_geom.h", os.path.join("..", "..", "include", "nmpc.h")]
 ARCH = os.environ.get("NMPC_OFFLOAD_ARCH", "gfx950")

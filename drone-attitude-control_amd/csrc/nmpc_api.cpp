@@ -297,10 +297,28 @@ int launch_cond(nmpc_solver *h, hipEvent_t e0, hipEvent_t e1)
     p.uout = (T *)h->d_u;
     p.status = h->d_status;
     p.iters = h->d_iters;
+    p.cycles = nullptr;
+    static const bool cycles = std::getenv("NMPC_SWEEP_CYCLES") != nullptr;
+    if (cycles) {
+        if (!h->d_cycles && hipMalloc(&h->d_cycles, (size_t)h->batch * 9 * sizeof(unsigned long long)) != hipSuccess)
+            h->d_cycles = nullptr;
+        p.cycles = h->d_cycles;
+    }
     hipEventRecord(e0 ? e0 : h->ev0, h->stream);
     hipError_t e = nmpc::cond_launch<T>(p, h->cond_wpb, h->cond_lds, h->stream);
     hipEventRecord(e1 ? e1 : h->ev1, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "condensed ipm kernel launch");
+    if (cycles && h->d_cycles) {
+        // tuning aid (NMPC_COND_TIMING builds): mean cycles per instance in each phase
+        std::vector<unsigned long long> cy((size_t)h->batch * 9);
+        hipStreamSynchronize(h->stream);
+        hipMemcpy(cy.data(), h->d_cycles, cy.size() * sizeof(cy[0]), hipMemcpyDeviceToHost);
+        double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int b = 0; b < h->batch; b++)
+            for (int j = 0; j < 8; j++) m[j] += (double)cy[(size_t)b * 9 + j] / h->batch;
+        std::fprintf(stderr, "[nmpc cond cycles] B=%d per instance: setup %.0f resid %.0f syrk %.0f chol %.0f pred %.0f"
+                     " corr %.0f step %.0f out %.0f\n", h->batch, m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]);
+    }
     return 0;
 }
 
@@ -336,6 +354,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
     p.status = h->d_status;
     p.iters = h->d_iters;
     p.scratch = (T *)h->d_scratch;
+    p.ipw = h->ipw;
+    p.lpi_stride = ((long long)h->batch + h->ipw - 1) / h->ipw * h->ipw;
     p.cycles = nullptr;
     static const bool sweep_cycles = std::getenv("NMPC_SWEEP_CYCLES") != nullptr;
     if (sweep_cycles) {
@@ -647,7 +667,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         // workgroup: the most wavefronts (<= 4) whose LDS (shared Gx + per-wave tiles/vectors) fits
         const size_t we = precision == NMPC_FP64 ? nmpc::cond_wave_elems<double>(h->ch.nb, h->ch.ldg)
                                                  : nmpc::cond_wave_elems<float>(h->ch.nb, h->ch.ldg);
-        const size_t gx = (size_t)16 * h->ch.nb * h->ch.ldg;
+        const size_t gx = (size_t)16 * h->ch.nb * h->ch.ldg + (((size_t)h->ch.n * h->ch.n + 3) & ~(size_t)3);
         h->cond_wpb = 0;
         for (int w = 4; w >= 1 && !h->cond_wpb; w--)
             if ((gx + w * we) * es <= 160 * 1024) h->cond_wpb = w;

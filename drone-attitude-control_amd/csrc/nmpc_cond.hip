@@ -127,6 +127,20 @@ __device__ __forceinline__ T wred(T v, Op op)
     return op(op(rl(v, 15), rl(v, 31)), op(rl(v, 47), rl(v, 63)));
 }
 
+// NMPC_COND_TIMING builds (tools): s_memtime per phase, accumulated per instance into p.cycles
+#ifdef NMPC_COND_TIMING
+#define CT_DECL unsigned long long ct_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ct_last = __builtin_amdgcn_s_memtime();
+#define CT(slot)                                                    \
+    do {                                                            \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ct_acc[slot] += t_ - ct_last;                               \
+        ct_last = t_;                                               \
+    } while (0)
+#else
+#define CT_DECL
+#define CT(slot) ((void)0)
+#endif
+
 template <typename T>
 __device__ __forceinline__ bool has(T b)
 {
@@ -146,26 +160,26 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
     const int mxp = (mx + 3) & ~3;
     const int q = lane >> 4, c16 = lane & 15;
 
-    // ---- shared: Gx column-major [np][ldg] (zero padded), once per workgroup
+    // ---- shared: Gx column-major [np][ldg] (zero padded) and H0 column-major [n][n], once per
+    //      workgroup
+    CT_DECL
     T *G = sh;
+    T *H0 = sh + (size_t)np * ldg;
     for (int e = threadIdx.x; e < np * ldg; e += blockDim.x) G[e] = p.Gx[e];
+    for (int e = threadIdx.x; e < n * n; e += blockDim.x) H0[e] = p.H0[e];
     __syncthreads();
     const long long inst_l = (long long)blockIdx.x * (blockDim.x >> 6) + wave;
     if (inst_l >= p.B) return;
     const int inst = (int)inst_l;
 
     // ---- per-wavefront LDS
-    T *Kt = sh + (size_t)np * ldg + (size_t)wave * p.wave_elems;
+    T *Kt = H0 + (((size_t)n * n + 3) & ~(size_t)3) + (size_t)wave * p.wave_elems;
     const int ntiles = nb * (nb + 1) / 2;
     T *Uv = Kt + ntiles * TS;   // [np] iterate U (broadcast reads)
     T *Sv = Uv + np;            // [np] Newton step dU
     T *DU = Sv + np;            // [np] barrier Hessian of the u rows
     T *WX = DU + np;            // [ldg] weights of the x rows (C' w)
     T *DX = WX + ldg;           // [ldg] barrier Hessian of the x rows
-    auto K = [&](int i, int j) -> T & {   // lower triangle, i >= j
-        const int I = i >> 4, J = j >> 4;
-        return Kt[(I * (I + 1) / 2 + J) * TS + (j & 15) * TP + (i & 15)];
-    };
     auto tile = [&](int I, int J) { return Kt + (I * (I + 1) / 2 + J) * TS; };
 
     const T *x0 = p.x0 + (size_t)inst * nx;
@@ -176,13 +190,20 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
 #pragma unroll
     for (int c = 0; c < UC; c++) {
         const int i = lane + 64 * c;
-        T s = 0;
+        T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
         if (i < n) {
-            s = p.fc[i];
-            for (int a = 0; a < nx; a++) s = fma(p.Fx[(size_t)a * n + i], x0[a], s);
-            for (int b = 0; b < p.nY; b++) s = fma(p.Fy[(size_t)b * n + i], Y[b], s);
+            s0 = p.fc[i];
+            for (int a = 0; a < nx; a++) s1 = fma(p.Fx[(size_t)a * n + i], x0[a], s1);
+            int b = 0;
+            for (; b + 3 < p.nY; b += 4) {
+                s0 = fma(p.Fy[(size_t)b * n + i], Y[b], s0);
+                s1 = fma(p.Fy[(size_t)(b + 1) * n + i], Y[b + 1], s1);
+                s2 = fma(p.Fy[(size_t)(b + 2) * n + i], Y[b + 2], s2);
+                s3 = fma(p.Fy[(size_t)(b + 3) * n + i], Y[b + 3], s3);
+            }
+            for (; b < p.nY; b++) s0 = fma(p.Fy[(size_t)b * n + i], Y[b], s0);
         }
-        f[c] = s;
+        f[c] = (s0 + s1) + (s2 + s3);
     }
     // ---- initial U: the u part of yref (LINEAR_LS with selection Vx/Vu) or 0, inside the bounds
 #pragma unroll
@@ -232,26 +253,28 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
         }
     }
     CSYNC();
-    // C v for the broadcast vector v (LDS): u rows read v, x rows Gx(r, :) v over its nonzero columns
+    // C v for the broadcast vector v (LDS): u rows read v, x rows Gx(r, :) v over the nonzero
+    // columns j < k nu of their stage (4 independent accumulators keep 8 LDS reads in flight)
     auto Cmul = [&](const T *v, T (&out)[RC]) {
 #pragma unroll
         for (int c = 0; c < RC; c++) {
             const int rho = lane + 64 * c;
-            T s = 0;
+            T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
             if (rho < n) {
-                s = v[rho];
+                s0 = v[rho];
             } else if (rho < mc) {
                 const int r = rho - n, nc = p.xcols[r];
-                T s1 = 0;
+                const T *g = G + r;
                 int j = 0;
-                for (; j + 1 < nc; j += 2) {
-                    s = fma(G[j * ldg + r], v[j], s);
-                    s1 = fma(G[(j + 1) * ldg + r], v[j + 1], s1);
+                for (; j + 3 < nc; j += 4) {
+                    s0 = fma(g[j * ldg], v[j], s0);
+                    s1 = fma(g[(j + 1) * ldg], v[j + 1], s1);
+                    s2 = fma(g[(j + 2) * ldg], v[j + 2], s2);
+                    s3 = fma(g[(j + 3) * ldg], v[j + 3], s3);
                 }
-                if (j < nc) s = fma(G[j * ldg + r], v[j], s);
-                s += s1;
+                for (; j < nc; j++) s0 = fma(g[j * ldg], v[j], s0);
             }
-            out[c] = s;
+            out[c] = (s0 + s1) + (s2 + s3);
         }
     };
     // C' w (lanes = rows of U): u part lane-local, x part Gx' w over the rows with nonzeros
@@ -265,17 +288,20 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
 #pragma unroll
         for (int c = 0; c < UC; c++) {
             const int i = lane + 64 * c;
-            T s = 0, s1 = 0;
+            T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
             if (i < n) {
-                s = w[c];   // rho = i lives in the same lane and chunk (n <= 64 UC <= 64 RC)
+                s0 = w[c];   // rho = i lives in the same lane and chunk (n <= 64 UC <= 64 RC)
+                const T *g = G + i * ldg;
                 int r = p.rstart[i];
-                for (; r + 1 < mx; r += 2) {
-                    s = fma(G[i * ldg + r], WX[r], s);
-                    s1 = fma(G[i * ldg + r + 1], WX[r + 1], s1);
+                for (; r + 3 < mx; r += 4) {
+                    s0 = fma(g[r], WX[r], s0);
+                    s1 = fma(g[r + 1], WX[r + 1], s1);
+                    s2 = fma(g[r + 2], WX[r + 2], s2);
+                    s3 = fma(g[r + 3], WX[r + 3], s3);
                 }
-                if (r < mx) s = fma(G[i * ldg + r], WX[r], s);
+                for (; r < mx; r++) s0 = fma(g[r], WX[r], s0);
             }
-            out[c] = s + s1;
+            out[c] = (s0 + s1) + (s2 + s3);
         }
         CSYNC();
     };
@@ -290,8 +316,8 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
         const T d = (hl[c] && hu[c]) ? T(0.01) * (hi[c] - lo[c]) : T(0.01) * fmax(fabs(hl[c] ? lo[c] : hi[c]), T(1));
         tl[c] = hl[c] ? fmax(cu[c] - lo[c], d) : T(1);
         tu[c] = hu[c] ? fmax(hi[c] - cu[c], d) : T(1);
-        ll[c] = hl[c] ? mu0 / tl[c] : T(0);
-        lu[c] = hu[c] ? mu0 / tu[c] : T(0);
+        ll[c] = hl[c] ? mu0 * frcp(tl[c]) : T(0);
+        lu[c] = hu[c] ? mu0 * frcp(tu[c]) : T(0);
     }
     auto sum = [](T a, T b) { return a + b; };
     auto vmin = [](T a, T b) { return fmin(a, b); };
@@ -310,70 +336,69 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
     T rres = 0;   // max |residual| (dual rd, primal rpl / rpu) at the current iterate
     int status = 2, iters = 0;
     const int ksteps = mxp >> 2;
+    // element (chunk c) of a per-lane register array, chunk chosen by a wave-uniform index
+    auto pick = [&](const T (&v)[UC], int c) {
+        T x = v[0];
+#pragma unroll
+        for (int k = 1; k < UC; k++) x = (c == k) ? v[k] : x;
+        return x;
+    };
 
-    // Newton solve for complementarity targets (rcl, rcu): dU -> Sv, C dU, dt, dlambda
-    T rd[UC], rpl[RC], rpu[RC];
+    // Newton solve for complementarity targets (rcl, rcu): dU -> Sv, C dU, dt, dlambda.
+    // itl / itu: reciprocal slacks of the iterate
+    T rd[UC], rpl[RC], rpu[RC], itl[RC], itu[RC];
     auto solve = [&](const T (&rcl)[RC], const T (&rcu)[RC], T (&cd)[RC], T (&dtl)[RC], T (&dtu)[RC], T (&dll)[RC],
                      T (&dlu)[RC]) {
         T w[RC], b[UC];
 #pragma unroll
         for (int c = 0; c < RC; c++)
-            w[c] = (hl[c] ? (rcl[c] + ll[c] * rpl[c]) / tl[c] : T(0)) - (hu[c] ? (rcu[c] + lu[c] * rpu[c]) / tu[c] : T(0));
+            w[c] = (hl[c] ? (rcl[c] + ll[c] * rpl[c]) * itl[c] : T(0)) - (hu[c] ? (rcu[c] + lu[c] * rpu[c]) * itu[c] : T(0));
         CTmul(w, b);
 #pragma unroll
         for (int c = 0; c < UC; c++) b[c] = (lane + 64 * c < n) ? -(rd[c] + b[c]) : T(0);
-        // forward substitution L y = b (lanes = rows; column j broadcast by readlane)
+        // forward substitution L y = b: per 16-column block the lanes' L entries are loaded
+        // into registers at once, then column j is broadcast by readlane
+        for (int J = 0; J < nb; J++) {
+            T pn[UC][16];
 #pragma unroll
-        for (int cj = 0; cj < UC; cj++) {
-            if (64 * cj >= np) break;
-            for (int jj = 0; jj < 64 && 64 * cj + jj < np; jj += 4) {
-                T kij[4][UC];
+            for (int c = 0; c < UC; c++) {
+                const int i = lane + 64 * c;
+                const bool own = i >= 16 * J && i < np;
+                const int I = own ? i >> 4 : J;
+                const T *src = tile(I, J) + (i & 15);
 #pragma unroll
-                for (int u4 = 0; u4 < 4; u4++) {
-                    const int j = 64 * cj + jj + u4;
+                for (int kk = 0; kk < 16; kk++) pn[c][kk] = own ? src[kk * TP] : T(0);
+            }
 #pragma unroll
-                    for (int c = cj; c < UC; c++) {
-                        const int i = lane + 64 * c;
-                        kij[u4][c] = (i > j && i < np) ? K(i, j) : T(0);
-                    }
-                }
+            for (int jj = 0; jj < 16; jj++) {
+                const int j = 16 * J + jj, cj = j >> 6;
+                const T y = rl(pick(b, cj) * pick(invd, cj), j & 63);
 #pragma unroll
-                for (int u4 = 0; u4 < 4; u4++) {
-                    const int j = 64 * cj + jj + u4;
-                    const T y = rl(b[cj] * invd[cj], jj + u4);
-#pragma unroll
-                    for (int c = cj; c < UC; c++) {
-                        const int i = lane + 64 * c;
-                        b[c] = (i == j) ? y : fma(-kij[u4][c], y, b[c]);
-                    }
+                for (int c = 0; c < UC; c++) {
+                    const int i = lane + 64 * c;
+                    b[c] = (i == j) ? y : ((i > j) ? fma(-pn[c][jj], y, b[c]) : b[c]);
                 }
             }
         }
-        // backward substitution L' x = y
+        // backward substitution L' x = y: lane i needs L(j, i) of the block's rows j
+        for (int J = nb - 1; J >= 0; J--) {
+            T pr[UC][16];
 #pragma unroll
-        for (int cj = UC - 1; cj >= 0; cj--) {
-            if (64 * cj >= np) continue;
-            const int top = (np - 64 * cj < 64 ? np - 64 * cj : 64);
-            for (int jj = top - 1; jj >= 0; jj -= 4) {
-                T kji[4][UC];
+            for (int c = 0; c < UC; c++) {
+                const int i = lane + 64 * c;
+                const bool own = (i >> 4) <= J;
+                const T *src = tile(J, own ? i >> 4 : 0) + (i & 15) * TP;
 #pragma unroll
-                for (int u4 = 0; u4 < 4; u4++) {
-                    const int j = 64 * cj + jj - u4;
+                for (int kk = 0; kk < 16; kk++) pr[c][kk] = own ? src[kk] : T(0);
+            }
 #pragma unroll
-                    for (int c = 0; c <= cj; c++) {
-                        const int i = lane + 64 * c;
-                        kji[u4][c] = (i < j) ? K(j, i) : T(0);
-                    }
-                }
+            for (int jj = 15; jj >= 0; jj--) {
+                const int j = 16 * J + jj, cj = j >> 6;
+                const T x = rl(pick(b, cj) * pick(invd, cj), j & 63);
 #pragma unroll
-                for (int u4 = 0; u4 < 4; u4++) {
-                    const int j = 64 * cj + jj - u4;
-                    const T x = rl(b[cj] * invd[cj], jj - u4);
-#pragma unroll
-                    for (int c = 0; c <= cj; c++) {
-                        const int i = lane + 64 * c;
-                        b[c] = (i == j) ? x : fma(-kji[u4][c], x, b[c]);
-                    }
+                for (int c = 0; c < UC; c++) {
+                    const int i = lane + 64 * c;
+                    b[c] = (i == j) ? x : ((i < j) ? fma(-pr[c][jj], x, b[c]) : b[c]);
                 }
             }
         }
@@ -388,8 +413,8 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
         for (int c = 0; c < RC; c++) {
             dtl[c] = hl[c] ? cd[c] + rpl[c] : T(0);
             dtu[c] = hu[c] ? -cd[c] + rpu[c] : T(0);
-            dll[c] = hl[c] ? (-rcl[c] - ll[c] * dtl[c]) / tl[c] : T(0);
-            dlu[c] = hu[c] ? (-rcu[c] - lu[c] * dtu[c]) / tu[c] : T(0);
+            dll[c] = hl[c] ? (-rcl[c] - ll[c] * dtl[c]) * itl[c] : T(0);
+            dlu[c] = hu[c] ? (-rcu[c] - lu[c] * dtu[c]) * itu[c] : T(0);
         }
     };
     // largest primal (slacks) and dual (multipliers) steps that keep them non-negative
@@ -398,15 +423,16 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
         ad = 1;
 #pragma unroll
         for (int c = 0; c < RC; c++) {
-            if (hl[c] && dtl[c] < T(0)) ap = fmin(ap, -tl[c] / dtl[c]);
-            if (hu[c] && dtu[c] < T(0)) ap = fmin(ap, -tu[c] / dtu[c]);
-            if (hl[c] && dll[c] < T(0)) ad = fmin(ad, -ll[c] / dll[c]);
-            if (hu[c] && dlu[c] < T(0)) ad = fmin(ad, -lu[c] / dlu[c]);
+            if (hl[c] && dtl[c] < T(0)) ap = fmin(ap, -tl[c] * frcp(dtl[c]));
+            if (hu[c] && dtu[c] < T(0)) ap = fmin(ap, -tu[c] * frcp(dtu[c]));
+            if (hl[c] && dll[c] < T(0)) ad = fmin(ad, -ll[c] * frcp(dll[c]));
+            if (hu[c] && dlu[c] < T(0)) ad = fmin(ad, -lu[c] * frcp(dlu[c]));
         }
         ap = wred(ap, vmin);
         ad = wred(ad, vmin);
     };
 
+    CT(0);
     for (int it = 0;; it++) {
         // ---- residuals at the current iterate: rd = H0 U + f - C' (lambda_l - lambda_u), primal
         {
@@ -417,28 +443,30 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
 #pragma unroll
             for (int c = 0; c < UC; c++) {
                 const int i = lane + 64 * c;
-                T s = 0, s1 = 0;
+                T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
                 if (i < n) {
+                    const T *h = H0 + i;
                     int j = 0;
-                    for (; j + 1 < n; j += 2) {
-                        s = fma(p.H0[(size_t)j * n + i], Uv[j], s);
-                        s1 = fma(p.H0[(size_t)(j + 1) * n + i], Uv[j + 1], s1);
+                    for (; j + 3 < n; j += 4) {
+                        s0 = fma(h[j * n], Uv[j], s0);
+                        s1 = fma(h[(j + 1) * n], Uv[j + 1], s1);
+                        s2 = fma(h[(j + 2) * n], Uv[j + 2], s2);
+                        s3 = fma(h[(j + 3) * n], Uv[j + 3], s3);
                     }
-                    if (j < n) s = fma(p.H0[(size_t)j * n + i], Uv[j], s);
-                    s = s + s1 + f[c] - ct[c];
+                    for (; j < n; j++) s0 = fma(h[j * n], Uv[j], s0);
+                    s0 = ((s0 + s1) + (s2 + s3)) + f[c] - ct[c];
                 }
-                rd[c] = s;
-            }
-#pragma unroll
-            for (int c = 0; c < RC; c++) {
-                rpl[c] = hl[c] ? cu[c] - lo[c] - tl[c] : T(0);
-                rpu[c] = hu[c] ? hi[c] - cu[c] - tu[c] : T(0);
+                rd[c] = s0;
             }
             T m = 0;
 #pragma unroll
             for (int c = 0; c < UC; c++) m = fmax(m, fabs(rd[c]));
 #pragma unroll
-            for (int c = 0; c < RC; c++) m = fmax(m, fmax(fabs(rpl[c]), fabs(rpu[c])));
+            for (int c = 0; c < RC; c++) {
+                rpl[c] = hl[c] ? cu[c] - lo[c] - tl[c] : T(0);
+                rpu[c] = hu[c] ? hi[c] - cu[c] - tu[c] : T(0);
+                m = fmax(m, fmax(fabs(rpl[c]), fabs(rpu[c])));
+            }
             rres = wred(m, vmax);
         }
         const bool conv = mu <= p.tol_comp && rres <= p.tol_res;
@@ -452,21 +480,25 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
             iters = it;
             break;
         }
+        CT(1);
         // ---- barrier Hessian of the rows
 #pragma unroll
         for (int c = 0; c < RC; c++) {
             const int rho = lane + 64 * c;
-            const T d = (hl[c] ? ll[c] / tl[c] : T(0)) + (hu[c] ? lu[c] / tu[c] : T(0));
+            itl[c] = hl[c] ? frcp(tl[c]) : T(0);
+            itu[c] = hu[c] ? frcp(tu[c]) : T(0);
+            const T d = ll[c] * itl[c] + lu[c] * itu[c];
             if (rho < n) DU[rho] = d;
             else if (rho < mc) DX[rho - n] = d;
         }
         CSYNC();
-        // ---- K = H0 + diag(D_u) + Gx' diag(D_x) Gx: lower tiles, MFMA over the x rows
+        // ---- K = H0 + diag(D_u) + Gx' diag(D_x) Gx: lower tiles, MFMA over the x rows (two
+        //      independent accumulation chains)
         for (int I = 0; I < nb; I++) {
             const int k0 = p.ks[I];
             for (int J = 0; J <= I; J++) {
                 const T *h0 = p.H0t + (size_t)(I * (I + 1) / 2 + J) * 256;
-                v4 acc;
+                v4 acc, acc2 = {0, 0, 0, 0};
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int row = M::row(lane, r);
@@ -476,54 +508,78 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
                 }
                 const T *ga = G + (16 * I + c16) * ldg + q;
                 const T *gb = G + (16 * J + c16) * ldg + q;
-                for (int s = k0; s < ksteps; s++) {
-                    const T a = ga[4 * s];
-                    const T b = DX[4 * s + q] * gb[4 * s];
-                    acc = M::mma(a, b, acc);
+                const T *dx = DX + q;
+                int s2 = k0;
+                for (; s2 + 1 < ksteps; s2 += 2) {
+                    const T a0 = ga[4 * s2], b0 = dx[4 * s2] * gb[4 * s2];
+                    const T a1 = ga[4 * s2 + 4], b1 = dx[4 * s2 + 4] * gb[4 * s2 + 4];
+                    acc = M::mma(a0, b0, acc);
+                    acc2 = M::mma(a1, b1, acc2);
                 }
+                if (s2 < ksteps) acc = M::mma(ga[4 * s2], dx[4 * s2] * gb[4 * s2], acc);
                 T *t = tile(I, J);
 #pragma unroll
-                for (int r = 0; r < 4; r++) t[c16 * TP + M::row(lane, r)] = acc[r];
+                for (int r = 0; r < 4; r++) t[c16 * TP + M::row(lane, r)] = acc[r] + acc2[r];
             }
         }
         CSYNC();
-        // ---- blocked Cholesky K = L L' in place (tiles): unblocked 16-column panels, MFMA
-        //      trailing updates
+        CT(2);
+        // ---- blocked Cholesky K = L L' in place (tiles): each 16-column panel is factorised in
+        //      registers (lane = row, pivots and column entries broadcast by readlane), then the
+        //      trailing tiles are updated with MFMA
         bool fail = false;
         for (int J = 0; J < nb; J++) {
+            const int j0 = 16 * J;
+            T pn[UC][16];
+#pragma unroll
+            for (int c = 0; c < UC; c++) {
+                const int i = lane + 64 * c;
+                const bool own = i >= j0 && i < np;
+                const int I = own ? i >> 4 : J;
+                const T *src = tile(I, J) + (i & 15);
+#pragma unroll
+                for (int kk = 0; kk < 16; kk++) pn[c][kk] = own ? src[kk * TP] : T(0);
+            }
 #pragma unroll
             for (int jj = 0; jj < 16; jj++) {
-                const int j = 16 * J + jj;
+                const int j = j0 + jj, cj = j >> 6;
+                T dsel[UC];
+#pragma unroll
+                for (int c = 0; c < UC; c++) dsel[c] = pn[c][jj];
+                const T d = rl(pick(dsel, cj), j & 63);
                 const bool real = j < n;
-                const T d = K(j, j);
                 const bool pd = d > T(0) || !real;
                 fail |= !pd;
                 const T rj = real ? frsq(pd ? d : T(1)) : T(0);
-#pragma unroll
-                for (int c = 0; c < UC; c++)
-                    if ((j >> 6) == c && lane == (j & 63)) invd[c] = rj;
                 T li[UC];
 #pragma unroll
                 for (int c = 0; c < UC; c++) {
                     const int i = lane + 64 * c;
-                    li[c] = 0;
-                    if (i > j && i < np) {
-                        li[c] = K(i, j) * rj;
-                        K(i, j) = li[c];
-                    }
+                    if (i == j) invd[c] = rj;
+                    li[c] = (i > j) ? pn[c][jj] * rj : ((i == j) ? d * rj : pn[c][jj]);
+                    pn[c][jj] = li[c];
                 }
-                CSYNC();
 #pragma unroll
-                for (int k = jj + 1; k < 16; k++) {
-                    const T lkj = K(16 * J + k, j);
+                for (int kk = jj + 1; kk < 16; kk++) {
+                    const int k = j0 + kk;
+                    const T lkj = rl(pick(li, k >> 6), k & 63);
 #pragma unroll
                     for (int c = 0; c < UC; c++) {
                         const int i = lane + 64 * c;
-                        if (i >= 16 * J + k && i < np) K(i, 16 * J + k) = fma(-li[c], lkj, K(i, 16 * J + k));
+                        pn[c][kk] = (i >= k) ? fma(-li[c], lkj, pn[c][kk]) : pn[c][kk];
                     }
                 }
-                CSYNC();
             }
+#pragma unroll
+            for (int c = 0; c < UC; c++) {
+                const int i = lane + 64 * c;
+                if (i >= j0 && i < np) {
+                    T *dst = tile(i >> 4, J) + (i & 15);
+#pragma unroll
+                    for (int kk = 0; kk < 16; kk++) dst[kk * TP] = pn[c][kk];
+                }
+            }
+            CSYNC();
             for (int I = J + 1; I < nb; I++) {
                 const T *la = tile(I, J);
                 for (int I2 = J + 1; I2 <= I; I2++) {
@@ -545,6 +601,7 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
             iters = it;
             break;
         }
+        CT(3);
         // ---- predictor (affine)
         T rcl[RC], rcu[RC], cd[RC], atl[RC], atu[RC], all_[RC], alu[RC];
 #pragma unroll
@@ -563,8 +620,9 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
                 s += (tl[c] + ap * atl[c]) * (ll[c] + ad * all_[c]) + (tu[c] + ap * atu[c]) * (lu[c] + ad * alu[c]);
             mu_aff = wred(s, sum) * p.inv_m;
         }
-        const T sg = mu > T(0) ? fmax(mu_aff, T(0)) / mu : T(0);
+        const T sg = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
         const T smu = sg * sg * sg * mu;
+        CT(4);
         // ---- corrector (Mehrotra)
 #pragma unroll
         for (int c = 0; c < RC; c++) {
@@ -573,6 +631,7 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
         }
         T dtl[RC], dtu[RC], dll[RC], dlu[RC];
         solve(rcl, rcu, cd, dtl, dtu, dll, dlu);
+        CT(5);
         max_step(dtl, dtu, dll, dlu, ap, ad);
         ap = fmin(T(1), T(0.995) * ap);
         ad = fmin(T(1), T(0.995) * ad);
@@ -597,6 +656,7 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
         CSYNC();
     }
 
+    CT(6);
     // ---- outputs: U, X = Phi x0 + d + Gamma U (row 0 is x0 itself)
     const int nrow = (p.N + 1) * nx;
     T *xo = p.xout + (size_t)inst * nrow;
@@ -608,15 +668,27 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
             s = p.dall[r];
             for (int a2 = 0; a2 < nx; a2++) s = fma(p.Phall[(size_t)a2 * nrow + r], x0[a2], s);
             const int nc = (r / nx) * nu;   // x_k depends on u_0 .. u_{k-1}
-            for (int j = 0; j < nc; j++) s = fma(p.Gall[(size_t)j * nrow + r], Uv[j], s);
+            T s1 = 0;
+            int j = 0;
+            for (; j + 1 < nc; j += 2) {
+                s = fma(p.Gall[(size_t)j * nrow + r], Uv[j], s);
+                s1 = fma(p.Gall[(size_t)(j + 1) * nrow + r], Uv[j + 1], s1);
+            }
+            if (j < nc) s = fma(p.Gall[(size_t)j * nrow + r], Uv[j], s);
+            s += s1;
         }
         xo[r] = s;
     }
     T *uo = p.uout + (size_t)inst * n;
     for (int i = lane; i < n; i += 64) uo[i] = Uv[i];
+    CT(7);
     if (lane == 0) {
         p.status[inst] = status;
         p.iters[inst] = iters;
+#ifdef NMPC_COND_TIMING
+        if (p.cycles)
+            for (int j = 0; j < 8; j++) p.cycles[(size_t)inst * 9 + j] = ct_acc[j];
+#endif
     }
 }
 
@@ -650,7 +722,8 @@ hipError_t cond_launch(const CondParams<T> &p, int wpb, size_t lds, hipStream_t 
     return hipErrorInvalidValue;
 }
 
-// static LDS need (bytes) of one wavefront / of the shared part, and the largest dims compiled
+// LDS elements of one wavefront (its K tiles and vectors); the shared part is
+// 16 nb ldg + round4(n^2) (Gx and H0)
 template <typename T>
 size_t cond_wave_elems(int nb, int ldg)
 {

@@ -35,6 +35,8 @@ struct IpmParams {
     int *iters;     // [B]
     T *scratch;     // [ceil(B/(IPW*WPB))*IPW*WPB][scratch_elems_per_instance]
     unsigned long long *cycles;   // optional [B][5] clock cycles per sweep type A..D + total (tuning, env NMPC_SWEEP_CYCLES)
+    int ipw;                      // lane-per-instance kernel: instances per wavefront (lanes 0 .. ipw-1)
+    long long lpi_stride;         // lane-per-instance kernel: scratch elements between words (>= slots)
 };
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);
@@ -86,6 +88,7 @@ struct CondParams {
     const T *yref;     // [B][nY]
     T *xout, *uout;
     int *status, *iters;
+    unsigned long long *cycles;   // optional [B][9] phase cycles (NMPC_COND_TIMING builds)
 };
 template <typename T>
 hipError_t cond_launch(const CondParams<T> &p, int wpb, size_t lds_bytes, hipStream_t s);

@@ -40,6 +40,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 
 #include "nmpc_internal.h"
 #include "nmpc_lpc_geom.h"
@@ -974,6 +975,33 @@ static constexpr IpmEntry<T> entry_lpc()
                        SP::id, SP::id ? &lpc::structure_fits<SP, NX, NU> : nullptr};
 }
 
+// lane-per-instance kernels (nmpc_ipm_lpi.hip): W instances per wavefront, chosen so that the
+// batch gives about one wavefront per SIMD (1024 on MI355X); env NMPC_LPI_W overrides
+int lpi_instances_per_wave(int B)
+{
+    if (const char *e = getenv("NMPC_LPI_W")) {
+        const int w = atoi(e);
+        if (w >= 1 && w <= 64) return w;
+    }
+    const int w = (B + 1023) / 1024;
+    return w < 1 ? 1 : (w > 64 ? 64 : w);
+}
+
+template <typename T, int NX, int NU>
+static size_t lpi_scratch_elems(int B, int N)
+{
+    const int W = lpi_instances_per_wave(B);
+    const size_t S = ((size_t)B + W - 1) / W * W;
+    return (size_t)(N + 1) * lpi_words<NX, NU>() * S;
+}
+
+template <typename T, int NX, int NU, class SP = lpc::DenseStructure<NX, NU>>
+static constexpr IpmEntry<T> entry_lpi()
+{
+    return IpmEntry<T>{3, NX, NU, 1, 4, 1, &launch_ipm_lpi<T, NX, NU, SP>, 0, &lpi_scratch_elems<T, NX, NU>, SP::id,
+                       SP::id ? &lpc::structure_fits<SP, NX, NU> : nullptr};
+}
+
 template <typename T>
 static const IpmEntry<T> *table(int *n)
 {
@@ -992,6 +1020,9 @@ static const IpmEntry<T> *table(int *n)
         entry_lpc<T, 13, 4, 4, 3, lpc::Quad13Structure>(), entry_lpc<T, 13, 4, 1, 3, lpc::Quad13Structure>(),
         entry_lpc<T, 13, 4, 2, 2, lpc::Quad13Structure>(), entry_lpc<T, 4, 2, 4, 2, lpc::ForceStructure>(),
         entry_lpc<T, 6, 2, 4, 2, lpc::JerkStructure>(),
+        // lane-per-instance kernels for the small models, dense and structure-specialised
+        entry_lpi<T, 4, 2>(), entry_lpi<T, 6, 2>(),
+        entry_lpi<T, 4, 2, lpc::ForceStructure>(), entry_lpi<T, 6, 2, lpc::JerkStructure>(),
     };
     *n = (int)(sizeof(t) / sizeof(t[0]));
     return t;
@@ -1007,6 +1038,7 @@ static int kernel_kind(int nx, int nu, int batch)
 {
     const char *k = getenv("NMPC_KERNEL");
     if (k && (k[0] == 'w' || k[0] == 'W')) return 0;
+    if (k && (strcmp(k, "lpi") == 0 || strcmp(k, "LPI") == 0)) return 3;
     if (k && (k[0] == 'l' || k[0] == 'L')) return 1;
     const int nz = nx + nu;
     if (nz > 64) return 0;
@@ -1037,10 +1069,12 @@ int ipm_find(int nx, int nu, int ipw_req, int batch, int *ipw_out, int *lds_out,
     }
     bool have = false;
     for (int i = 0; i < n; i++) have |= t[i].nx == nx && t[i].nu == nu && t[i].kind == kind && !t[i].sid;
-    const int fam = have ? kind : 1 - kind;
+    const int fam = have ? kind : (kind == 3 ? 1 : 1 - kind);   // no lane-per-instance twin: lane per component
     for (int i = 0; i < n; i++) {
         if (t[i].nx != nx || t[i].nu != nu || t[i].kind != fam || t[i].sid) continue;
         if (fam == 1) {   // lane-per-component: instances per wave fixed by nx + nu, first listed
+            if (best < 0) best = i;
+        } else if (fam == 3) {   // lane-per-instance: instances per wave from the batch
             if (best < 0) best = i;
         } else if (ipw_req > 0) {
             if (t[i].ipw == ipw_req && best < 0) best = i;   // first listed = preferred variant
@@ -1049,7 +1083,7 @@ int ipm_find(int nx, int nu, int ipw_req, int batch, int *ipw_out, int *lds_out,
         }
     }
     if (best < 0) return -1;
-    *ipw_out = t[best].ipw;
+    *ipw_out = t[best].kind == 3 ? lpi_instances_per_wave(batch) : t[best].ipw;
     *lds_out = t[best].lds_bytes;
     if (wpb_out) *wpb_out = t[best].wpb;
     return best;

@@ -68,6 +68,13 @@ inline size_t scratch_elems(int B, int N)
 template <typename T, int NX, int NU, int WPB, int MW, class SP>
 hipError_t launch_ipm_lpc(const IpmParams<T> &p, hipStream_t s);
 
+// lane-per-instance kernels (nmpc_ipm_lpi.hip)
+template <typename T, int NX, int NU, class SP>
+hipError_t launch_ipm_lpi(const IpmParams<T> &p, hipStream_t s);
+template <int NX, int NU>
+size_t lpi_words();
+int lpi_instances_per_wave(int B);
+
 }  // namespace nmpc
 
 namespace nmpc {

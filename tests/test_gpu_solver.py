@@ -129,6 +129,30 @@ def test_structure_specialised_matches_dense(key, cases):
     assert ea.max() < TOL64 and eb.max() < TOL64
 
 
+@pytest.mark.parametrize("key", ["force_N20", "force_N30", "jerk_N40", "jerk_N30"])
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+@pytest.mark.parametrize("W", [1, 3, 64])
+def test_lane_per_instance_family(key, precision, W, cases):
+    """The lane-per-instance kernels (nmpc_ipm_lpi.hip, one lane = one instance, W instances per
+    wavefront — 1, a ragged 3 and a full 64) against the certified oracle, with the same
+    iteration counts as the C baseline (same algorithm, +-1 from rounding order)."""
+    os.environ["NMPC_LPI_W"] = str(W)
+    try:
+        s, st = solve_batch(key, cases, precision=precision, kernel="lpi")
+    finally:
+        os.environ.pop("NMPC_LPI_W", None)
+    assert s.launch_info()["kernel"] == "ipm_lpi_kernel"
+    assert s.launch_info()["instances_per_wave"] == W
+    status = s.get_batch_int("status")
+    assert (status == 0).all(), status
+    e = rel_err(s.get_batch("x"), s.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
+    assert e.max() < (TOL64 if precision == "fp64" else TOL32), e.max()
+    if precision == "fp64":
+        name, N = split(key)
+        _, _, _, itc = cref.RiccatiIpmRef(models.MODELS[name](N)).solve(cases[key + "_x0"], cases[key + "_yref"])
+        assert np.abs(s.get_batch_int("qp_iter") - itc).max() <= 1
+
+
 def test_default_family_is_batch_aware(cases):
     """quad13 always runs lane-per-component; the small force model switches to it only when
     the batch fills enough wavefronts (nmpc_ipm.hip kernel_kind)."""
