@@ -11,8 +11,8 @@
 //   D  forward corrector; step length on the fly),
 // mapped for small models (force nx=4 nu=2, jerk nx=6 nu=2): ONE LANE owns one instance and
 // runs the whole stage recursion in its registers — no LDS exchange, no cross-lane reduction,
-// nothing but the per-stage records in a lane-interleaved scratch (word w of stage k of the
-// lane's instance at (k NW + w) S + slot: every access of a wavefront is one contiguous run).
+// nothing but the per-stage records in a wavefront-private scratch block (word w of stage k of
+// lane l at (k NW + w) W + l: every access of a wavefront is one contiguous run).
 // A small model's stage is a few hundred FMAs with plenty of independent work, so one lane's
 // instruction stream is short; the host packs W = ceil(B / 1024) instances per wavefront (the
 // other lanes idle) so that every SIMD of the GPU gets about one wavefront: the whole batch
@@ -99,11 +99,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (lane >= W || slot >= p.B) return;
     const int inst = (int)slot;
     const int N = p.N;
-    // scratch stride between words (>= slots); 32-bit word offsets (stage * NW + word) * S. S is
-    // re-obscured per stage with the constants (fresh()): hoisting all NW offsets word * S out of
-    // the stage loops made 70+ loop-invariant registers and spilled the stage state
-    int So = (int)p.lpi_stride;
-    T *scr = p.scratch + slot;
+    // scratch: each wavefront owns one contiguous block of (N+1) NW W elements, stage-major, word
+    // w of stage k of lane l at (k NW + w) W + l: a stage's words are a few dense cache lines that
+    // stay in the XCD's L2 (instance-major interleaving over the whole batch put every lane's word
+    // in a line shared with 15 other instances, most of them on other XCDs: 16x the L2 footprint).
+    // The 32-bit offsets use W re-obscured per stage (fresh()): hoisting all NW offsets word * W
+    // out of the stage loops made 70+ loop-invariant registers and spilled the stage state.
+    int So = W;
+    T *scr = p.scratch + (size_t)wave * (size_t)(N + 1) * NW * W + lane;
     auto ld = [&](int k, int w) { return scr[(unsigned)((k * NW + w) * So)]; };
     auto st = [&](int k, int w, T v) { scr[(unsigned)((k * NW + w) * So)] = v; };
     // the model constants are re-read from LDS at every stage: co is made opaque once per stage
@@ -233,6 +236,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     mu *= p.inv_m;
     const T m_bounds = T(1) / p.inv_m;
+#ifdef NMPC_SWEEP_TIMING
+    // experiment builds: clock cycles per sweep (A -> slot 1, B -> 2, C -> 5, D -> 6, total 8)
+    unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = __builtin_amdgcn_s_memtime();
+    const unsigned long long tstart = tmark;
+    auto tick = [&](int slot) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        tcy[slot] += t - tmark;
+        tmark = t;
+    };
+#define LPI_TICK(s) tick(s)
+#else
+#define LPI_TICK(s) ((void)0)
+#endif
 
     T theta = 1, alpha = 0, smu = 0;
     bool pending = false, fail = false;
@@ -457,6 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         pending = false;
         mu = musum * p.inv_m;
+        LPI_TICK(1);
         // ---- termination (the iterate is the one reached after `it` steps)
         const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
         const bool bad = !isfinite(mu) || !isfinite(theta);
@@ -578,6 +595,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
         const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
         smu = sgm * sgm * sgm * mu;
+        LPI_TICK(2);
 
         // ============================ C: backward corrector vector
         {
@@ -653,6 +671,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
 
+        LPI_TICK(5);
         // ============================ D: forward corrector + step length
         T amax, dm1, dm2;
         forward(true, amax, dm1, dm2);
@@ -660,6 +679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         pending = true;
         theta *= T(1) - alpha;
         (void)m_bounds;
+        LPI_TICK(6);
     }
 
     // ------------------------------------------------------------------ outputs
@@ -677,6 +697,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     p.status[inst] = status;
     p.iters[inst] = iters;
+#ifdef NMPC_SWEEP_TIMING
+    if (p.cycles) {
+        unsigned long long *c = p.cycles + (size_t)inst * 9;
+        for (int j = 0; j < 8; j++) c[j] = tcy[j];
+        c[8] = __builtin_amdgcn_s_memtime() - tstart;
+    }
+#endif
 }
 
 }  // namespace lpi
