@@ -17,7 +17,7 @@ NMPC_FP64, NMPC_FP32 = 0, 1
 NMPC_DYN_CONTINUOUS_AFFINE, NMPC_DYN_DISCRETE_AFFINE = 0, 1
 NMPC_IRK, NMPC_ERK = 0, 1
 NMPC_COST_SCALING_TIME_STEPS, NMPC_COST_SCALING_NONE = 0, 1
-NMPC_ABI_VERSION = 1
+NMPC_ABI_VERSION = 2
 
 STATUS_TEXT = {0: "success", 1: "failure", 2: "maximum number of iterations reached",
                3: "minimum step size in QP solver reached", 4: "qp solver failed"}
@@ -42,6 +42,7 @@ class OcpDesc(ctypes.Structure):
         ("x0", _dp),
         ("qp_solver_iter_max", ctypes.c_int), ("qp_solver_tol_comp", ctypes.c_double),
         ("qp_solver_tol_res", ctypes.c_double), ("qp_solver_mu0", ctypes.c_double),
+        ("qp_solver_polish_mu", ctypes.c_double),
     ]
 
 

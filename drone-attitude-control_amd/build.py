@@ -31,17 +31,41 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in deps if os.path.exists(d))
 
 
+def _compile_link(out, defines=(), verbose=False):
+    """One object per source, compiled in parallel (each kernel is launched from its own
+    translation unit, so no relocatable device code is needed), then one shared link."""
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"] + [f"-D{d}" for d in defines]
+
+    def cc(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = ["hipcc", *cflags, "-c", src, "-o", obj]
+        if verbose:
+            print("[nmpc build]", " ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        return obj
+
+    jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    # the longest translation units first
+    srcs = sorted(sources(), key=lambda p: -os.path.getsize(p))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(cc, srcs))
+    tmp = out + ".tmp"
+    subprocess.check_call(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])
+    os.replace(tmp, out)
+    for o in objs:
+        os.remove(o)
+    os.rmdir(objdir)
+    return out
+
+
 def build(force=False, verbose=True):
     if not force and up_to_date():
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = ["hipcc", *FLAGS, *sources(), "-o", tmp]
-    if verbose:
-        print("[nmpc build]", " ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    return LIB
+    return _compile_link(LIB, verbose=verbose)
 
 
 def build_experiment(tag, defines):
@@ -49,8 +73,7 @@ def build_experiment(tag, defines):
     run time with NMPC_LIB=<path>)."""
     out = os.path.join(PKG, "lib", "exp", f"libnmpc_hip_{tag}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    subprocess.check_call(["hipcc", *FLAGS, *[f"-D{d}" for d in defines], *sources(), "-o", out])
-    return out
+    return _compile_link(out, defines)
 
 
 if __name__ == "__main__":

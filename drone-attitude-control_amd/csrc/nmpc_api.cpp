@@ -195,6 +195,7 @@ struct nmpc_solver {
     int kidx = -1, ipw = 1, wpb = 1, lds = 0, yref_is_z = 0;
     int max_iter = 50;
     double tol_comp = 0, tol_res = 0, mu0 = 0, inv_m = 1, ts = 0, scale_e = 1;
+    double polish_mu = 0, polish_rho = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
@@ -337,6 +338,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
     p.tol_res = (T)h->tol_res;
     p.mu0 = (T)h->mu0;
     p.inv_m = (T)h->inv_m;
+    p.polish_mu = (T)h->polish_mu;
+    p.polish_rho = (T)h->polish_rho;
     const char *m = (const char *)h->d_model;
     p.AB = (const T *)(m + h->off_AB);
     p.ABt = (const T *)(m + h->off_ABt);
@@ -606,6 +609,15 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         h->tol_res = std::max(h->tol_res, 1e-5);
     }
     h->mu0 = d->qp_solver_mu0 > 0 ? d->qp_solver_mu0 : 1e-2;
+    // exact finish: fp64 only (the penalty weight below needs ~16 digits); the penalty is 1e8 x
+    // the largest cost curvature, as in oracle/c/riccati_ipm.c (POLISH_RHO)
+    h->polish_mu = !f64 || d->qp_solver_polish_mu < 0 ? 0.0 : (d->qp_solver_polish_mu > 0 ? d->qp_solver_polish_mu : 1e-6);
+    {
+        double hmax = 1.0;
+        for (int i = 0; i < nz; i++) hmax = std::max(hmax, std::fabs(h->H[i * nz + i]));
+        for (int i = 0; i < nx; i++) hmax = std::max(hmax, std::fabs(h->He[i * nx + i]));
+        h->polish_rho = 1e8 * hmax;
+    }
     // ---- host staging
     h->h_x0.assign((size_t)batch * nx, 0.0);
     if (d->x0)

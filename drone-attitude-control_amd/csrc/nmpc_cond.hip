@@ -218,6 +218,7 @@ __global__ __launch_bounds__(256) void cond_ipm_kernel(CondParams<T> p)
                 const bool hl = has(lb), hu = has(ub);
                 if (hl && hu) {
                     const T d = T(0.01) * (ub - lb);
+                    z = T(0.5) * (lb + ub);   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
                     z = fmin(fmax(z, lb + d), ub - d);
                 } else if (hl) {
                     z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));

@@ -18,6 +18,8 @@ struct IpmParams {
     int yref_is_z;  // y = [x; u] (selection Vx, Vu): use yref as the initial guess
     int max_iter;
     T tol_comp, tol_res, mu0, inv_m;
+    T polish_mu;    // exact finish threshold (0: off)
+    T polish_rho;   // penalty on the identified active bounds in the finish
     const T *AB;    // [nx][nx+nu]   discrete [A B], row-major
     const T *ABt;   // [nx+nu][nx]   its transpose
     const T *c;     // [nx]

@@ -391,6 +391,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 const bool hl = has_bound(lb), hu = has_bound(ub);
                 if (hl && hu) {
                     const T d = T(0.01) * (ub - lb);
+                    z = i >= NX ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
                     z = fmin(fmax(z, lb + d), ub - d);
                 } else if (hl) {
                     z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
@@ -440,6 +441,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     int status = 2, iters = 0;
     bool fail = false, pending = false;
     T alpha = 0, smu = 0;      // step and sigma*mu of the pending (lazily applied) update
+    // exact finish (oracle/c/riccati_ipm.c "exact finish"; nmpc_ipm_lpc.hip): attempts so far,
+    // groups polishing in the current pass; status -1 = completed by the finish (step in dz)
+    int fin_att = 0;
+    bool pol = false;
 
 #ifdef NMPC_SWEEP_TIMING
     // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per phase
@@ -511,17 +516,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 dxn[ll] = dot2<NZ>(rec[FRE + ll], [&](int j) { return arow[j]; },
                                    [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
             }
-            if (ll < NZ) S.st(dst + k * NZ, ll, ll < NX ? dxc[ll] : du_l[ll - NX]);
+            // the corrector skips groups the finish completed: their dz holds the finish step
+            if (ll < NZ && (dst != Ldz || status >= 0)) S.st(dst + k * NZ, ll, ll < NX ? dxc[ll] : du_l[ll - NX]);
             rec_put(r[(j + 1) % DF], (k + 1) & 1, false);
             rec_issue(r[(j + 1) % DF], k + 1 + DF, false);
             cur = 1 - cur;
             WAVE_SYNC();
         }
-        if (ll < NX) S.st(dst + N * NZ, ll, dxb[cur * LDX + ll]);
+        if (ll < NX && (dst != Ldz || status >= 0)) S.st(dst + N * NZ, ll, dxb[cur * LDX + ll]);
         SWEEP_FENCE();
     };
 
     int it = 0;
+    bool pfail = false;
     for (;; it++) {
         const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
         const bool bad = !isfinite(mu) || !isfinite(theta) || fail;
@@ -538,6 +545,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         if (!__any(active)) break;
         NMPC_TICK(-1);
 
+        // E_A + A; the finish pass (finp, wave-uniform) forms the finish's penalty terms in place of
+        // the barrier for the polishing groups
+        auto factor = [&](bool finp) __attribute__((always_inline)) {
         // ============================ E_A: lazy step, Sigma, g = H z + gc, re = [A B] z_k + c - x_{k+1}
         // stage chunks whose z (plus one stage of overlap) fit the LDS window zw
         for (int k0 = 0; k0 <= N; k0 += Gm::CH) {
@@ -571,6 +581,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         T sig = 0;
                         if (lam_l > T(0)) sig += lam_l * frcp(z - lb);
                         if (lam_u > T(0)) sig += lam_u * frcp(ub - z);
+                        if (finp && pol) {
+                            // active where the multiplier exceeds the slack: penalty rho, else dropped
+                            const bool al = lam_l > T(0) && lam_l > z - lb, au = !al && lam_u > T(0) && lam_u > ub - z;
+                            sig = (al || au) ? p.polish_rho : T(0);
+                        }
                         S.st(Lsg, e, sig);
                     }
                 }
@@ -580,11 +595,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             for (int e = k0 * NZ + ll; e < k1 * NZ; e += G) {
                 const int k = e / NZ, i = e - k * NZ;
                 const T *zk = zw + (k - k0) * NZ;
+                T gadd = 0;
+                if (finp && pol && (k < N || i < NX)) {   // the finish's penalty gradient rho (z - bound)
+                    const T lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), z = zk[i];
+                    const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+                    const bool al = lam_l > T(0) && lam_l > z - lb, au = !al && lam_u > T(0) && lam_u > ub - z;
+                    gadd = (al || au) ? p.polish_rho * (z - (al ? lb : ub)) : T(0);
+                }
                 if (k < N) {
-                    S.st(Lgf, e, dot2<NZ>(S.ld(Lgc, e), [&](int b) { return ch[i * LDZ + b]; },
+                    S.st(Lgf, e, dot2<NZ>(S.ld(Lgc, e) + gadd, [&](int b) { return ch[i * LDZ + b]; },
                                           [&](int b) { return zk[b]; }));
                 } else if (i < NX) {
-                    S.st(Lgf, e, dot2<NX>(S.ld(Lgc, e), [&](int b) { return che[i * LDX + b]; },
+                    S.st(Lgf, e, dot2<NX>(S.ld(Lgc, e) + gadd, [&](int b) { return che[i * LDX + b]; },
                                           [&](int b) { return zk[b]; }));
                 }
             }
@@ -691,7 +713,8 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                         for (int l = 0; l < j; l++) s_ -= lf[tri(i, l)] * lf[tri(j, l)];
                         if (i == j) {
                             const bool pd = s_ > T(0);
-                            fail |= active & !pd;
+                            if (finp) pfail |= pol & !pd;
+                            else fail |= active & !pd;
                             lf[tri(i, i)] = frsq(pd ? s_ : T(1));
                         } else {
                             lf[tri(i, j)] = s_ * lf[tri(j, j)];
@@ -754,6 +777,47 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
             }
         }
         SWEEP_FENCE();
+        };
+
+        // ============================ exact finish (groups with mu <= polish_mu / 100^attempts):
+        // penalised factorisation, its step into dz, the oracle's acceptance tests; accepted groups
+        // are done, the others go on with this iteration
+        {
+            T thr = p.polish_mu;
+            for (int j = 0; j < fin_att; j++) thr *= T(0.01);
+            pol = active && p.polish_mu > T(0) && mu <= thr;
+        }
+        if (__any(pol)) {
+            pfail = false;
+            factor(true);
+            forward(Ldz);
+            T nbad = 0;
+            for (int e = ll; e < nel; e += G) {
+                const int k = e / NZ, i = e - k * NZ;
+                if (k == N && i >= NX) continue;
+                const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), zn = z + S.ld(Ldz, e);
+                const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+                const T sl = T(1) + fabs(lb), su = T(1) + fabs(ub);
+                const bool vl = lam_l > T(0), vu = lam_u > T(0);
+                const bool al = vl && lam_l > z - lb, au = !al && vu && lam_u > ub - z;
+                const bool bad = al ? zn > fma(T(1e-15), sl, lb)
+                                    : (au ? zn < fma(T(-1e-15), su, ub)
+                                          : ((vl && zn < fma(T(-1e-9), sl, lb)) || (vu && zn > fma(T(1e-9), su, ub))));
+                nbad += bad ? T(1) : T(0);
+            }
+            nbad = group_sum<G>(nbad);
+            if (pol) {
+                fin_att++;
+                if (nbad == T(0) && !pfail) {
+                    active = false;
+                    status = -1;
+                    iters = it + 1;
+                }
+            }
+            pol = false;
+            if (!__any(active)) break;
+        }
+        factor(false);
         NMPC_TICK(1);
 
         // ============================ B: forward predictor; E_B: ratio test + centring sums
@@ -914,11 +978,17 @@ _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
         if (k == N && i >= NX) continue;
         T z = S.ld(Lz, e);
         if (pending) z += alpha * S.ld(Ldz, e);
+        if (status < 0) {   // completed by the finish: its step, clamped onto the active bounds
+            const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+            z += S.ld(Ldz, e);
+            z = has_bound(lb) ? fmax(z, lb) : z;
+            z = has_bound(ub) ? fmin(z, ub) : z;
+        }
         if (i < NX) xo[k * NX + i] = z;
         else uo[k * NU + (i - NX)] = z;
     }
     if (ll == 0) {
-        p.status[inst] = status;
+        p.status[inst] = status < 0 ? 0 : status;
         p.iters[inst] = iters;
 #ifdef NMPC_SWEEP_TIMING
         if (timed) {

@@ -219,6 +219,13 @@ __device__ __forceinline__ T sp_dot(const SpL<T, NL> &q, const T *vec, T s0)
     return s0 + s1;
 }
 
+// compile-time pass selectors of the sweeps (forward: 0 predictor, 1 corrector, 2 finish;
+// Riccati: 0 ordinary, 1 finish)
+template <int V>
+struct Pass {
+    static constexpr int value = V;
+};
+
 template <typename T>
 __device__ __forceinline__ bool has_bound(T b)
 {
@@ -393,6 +400,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 const bool hl = has_bound(lb), hu = has_bound(ub);
                 if (hl && hu) {
                     const T d = T(0.01) * (ub - lb);
+                    z = ul ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
                     z = fmin(fmax(z, lb + d), ub - d);
                 } else if (hl) {
                     z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
@@ -442,6 +450,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     int status = 2, iters = 0;
     bool fail = false, pending = false;
     T alpha = 0, smu = 0;
+    // exact finish (oracle/c/riccati_ipm.c "exact finish"): attempts so far (the next one waits
+    // for mu <= polish_mu / 100^attempts); pol marks the groups polishing in the current pass.
+    // status -1: completed by the finish, whose step DZ is kept (the corrector skips the group)
+    int fin_att = 0;
+    bool pol = false;
 
     // elementwise state of element (k, r) fetched one stage ahead in the sweeps
     struct El {
@@ -475,6 +488,29 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     auto sigma = [&](const El &q, const Bd &b) {
         const T sl = q.ll * frcp(q.z - b.lb), su = q.lu * frcp(b.ub - q.z);
         return (q.ll > T(0) ? sl : T(0)) + (q.lu > T(0) ? su : T(0));
+    };
+    // exact finish: a bound is active where its multiplier exceeds its slack; the finish holds
+    // active bounds by the penalty rho (Hessian rho, gradient rho (z - bound)) and drops the
+    // barrier of the others (branch-free)
+    auto finish_terms = [&](const El &q, const Bd &b, T &sg, T &gadd) {
+        const bool al = q.ll > T(0) && q.ll > q.z - b.lb;
+        const bool au = !al && q.lu > T(0) && q.lu > b.ub - q.z;
+        const T rho = p.polish_rho;
+        sg = (al || au) ? rho : T(0);
+        gadd = (al || au) ? rho * (q.z - (al ? b.lb : b.ub)) : T(0);
+    };
+    // acceptance of the finish at element (k, r): active bounds keep a non-negative multiplier
+    // rho (bound - z_new) (to a few ulps), inactive ones hold (to 1e-9, then clamped) — the
+    // POLISH_TOL_ACTIVE / POLISH_TOL tests of the oracle
+    auto finish_bad = [&](T dz, const El &q, const Bd &b) {
+        const bool vl = q.ll > T(0), vu = q.lu > T(0);
+        const bool al = vl && q.ll > q.z - b.lb, au = !al && vu && q.lu > b.ub - q.z;
+        const T zn = q.z + dz;
+        const T sl = T(1) + fabs(b.lb), su = T(1) + fabs(b.ub);
+        const bool bad = al ? zn > fma(T(1e-15), sl, b.lb)
+                            : (au ? zn < fma(T(-1e-15), su, b.ub)
+                                  : ((vl && zn < fma(T(-1e-9), sl, b.lb)) || (vu && zn > fma(T(1e-9), su, b.ub))));
+        return bad ? T(1) : T(0);
     };
     // the same lazy step split in two for the Riccati stages k < N: the primal update first (it
     // is all the stage's first LDS exchange needs), the dual update after that exchange, where
@@ -536,7 +572,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #define LPC_FTICK(slot) ((void)0)
 #endif
 
-    auto forward = [&](bool corr, T &s_min, T &s_a, T &s_b, T &s_c) {
+    auto forward = [&](auto PASS, T &s_min, T &s_a, T &s_b, T &s_c) __attribute__((always_inline)) {
+        constexpr bool corr = decltype(PASS)::value == 1, fin = decltype(PASS)::value == 2;
         const T *arow = abr + (xl ? r : 0) * LDZ;   // row r of [A B] (LDS, read per stage)
         s_min = 1;
         s_a = s_b = s_c = 0;
@@ -549,7 +586,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             const bool vl = q.ll > T(0), vu = q.lu > T(0);
             const T tl = q.z - lb, tu = ub - q.z;
             T c = 1;
-            if (!corr) {
+            if constexpr (fin) {
+                s_c += finish_bad(dz, q, b);   // the finish: acceptance count only
+            } else if constexpr (!corr) {
                 // predictor: the largest inverse step ratio, division-free — primal -dz/t_l and
                 // dual -dlam_l/lam_l = 1 + dz/t_l (the affine dual step is -lam (1 + dz/t)), and
                 // the mirrored pair for the upper bound; alpha_aff = 1 / max(1, ...) per group
@@ -593,7 +632,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
             q.c0 = q.kq[UKFF];
         };
-        const int dst = corr ? L::DZ : L::DZA;
+        const int dst = (corr || fin) ? L::DZ : L::DZA;   // the finish's step goes to DZ
         T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
         // dx_{k+1}(r) = c_r + [A B](r, :) (z_k + dz_k) - z_{k+1}(r): the dynamics residual is
         // folded in, so the sweep carries xt = dx_{k+1} + z_{k+1} and subtracts z_{k+1} when
@@ -695,7 +734,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     xt = xl ? s0 + s1 : xt;
                 }
                 LPC_FTICK(4);
-                stE(dst, k, my);
+                // the corrector skips groups the finish completed: their DZ holds the finish step
+                if (!corr || status >= 0) stE(dst, k, my);
 #if NMPC_LPC_DEFER
                 pm = my;
                 pe = q.e;
@@ -718,7 +758,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             e.lu = ldE(L::LU, N);
             if (corr) e.dza = ldE(L::DZA, N);
             const T dx = xt - e.z;
-            stE(dst, N, dx);
+            if (!corr || status >= 0) stE(dst, N, dx);
             stats(dx, e, bnd(N));
         }
         s_min = corr ? gmin(s_min) : frcp(gmax(s_min));
@@ -746,8 +786,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         if (!__any(active)) break;
         LPC_TICK(-1);
 
-        // ============================ A: backward Riccati factorisation (+ lazy step, Sigma, g, re)
-        {
+        // ============================ A: backward Riccati factorisation (+ lazy step, Sigma, g, re);
+        // the finish pass factors with the finish's penalty terms instead of the barrier
+        bool pfail = false;
+        auto riccati = [&](auto PASS) __attribute__((always_inline)) {
+            constexpr bool FIN = decltype(PASS)::value == 1;
             T prow[NX], sdiag, pv;
             T znext;
             El q, qn;
@@ -764,10 +807,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             fetchA(N - 1, qn);
             lazy(N, q, bnd(N));
             {
-                const T sg = xl ? sigma(q, bnd(N)) : T(0);
+                T sg = xl ? sigma(q, bnd(N)) : T(0), gadd = 0;
+                if constexpr (FIN) {
+                    finish_terms(q, bnd(N), sg, gadd);
+                    sg = xl ? sg : T(0);
+                }
                 zb[r] = xl ? q.z : T(0);
                 LPC_SYNC();
-                T g = q.g;
+                T g = q.g + gadd;
                 const int rx = xl ? r : 0;
                 if (SP::hdiag) {
                     g = fma(hem[rx * LDX + rx], q.z, g);
@@ -800,15 +847,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 zb[r] = q.z;
                 LPC_SYNC();
                 lazy_duals(k, q, zo, bk);
-                const T sg = sigma(q, bk);
+                T sg = sigma(q, bk), gadd = 0;
+                if constexpr (FIN) finish_terms(q, bk, sg, gadd);
 #else
                 lazy(k, q, bk);
-                const T sg = sigma(q, bk);
+                T sg = sigma(q, bk), gadd = 0;
+                if constexpr (FIN) finish_terms(q, bk, sg, gadd);
                 zb[r] = q.z;
                 LPC_SYNC();
 #endif
-                // g = H z + G yref, re = [A B] z_k + c - x_{k+1}
-                T g = q.g, re = 0;
+                // g = H z + G yref (+ the finish's penalty gradient), re = [A B] z_k + c - x_{k+1}
+                T g = q.g + gadd, re = 0;
                 if (SP::hdiag) {
                     g = fma(hrr, q.z, g);
                 } else {
@@ -941,7 +990,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         for (int l = 0; l < j; l++) s_ = fma(-lf[tri(i, l)], lf[tri(j, l)], s_);
                         if (i == j) {
                             const bool pd = s_ > T(0);
-                            fail |= active & !pd;
+                            if constexpr (FIN) pfail |= pol & !pd;
+                            else fail |= active & !pd;
                             lf[tri(i, i)] = frsq(pd ? s_ : T(1));
                         } else {
                             lf[tri(i, j)] = s_ * lf[tri(j, j)];
@@ -1034,14 +1084,40 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 LPC_SYNC();
                 LPC_PTICK(7);
             }
+        };
+
+        // ============================ exact finish (groups with mu <= polish_mu / 100^attempts):
+        // penalised factorisation + forward sweep writing the candidate to the outputs and counting
+        // violated acceptance tests; accepted groups are done, the others go on with this iteration
+        {
+            T thr = p.polish_mu;
+            for (int j = 0; j < fin_att; j++) thr *= T(0.01);
+            pol = active && p.polish_mu > T(0) && mu <= thr;
         }
+        if (__any(pol)) {
+            riccati(Pass<1>{});
+            pending = false;
+            T d0, d1, d2, nbad;
+            forward(Pass<2>{}, d0, d1, d2, nbad);
+            if (pol) {
+                fin_att++;
+                if (nbad == T(0) && !pfail) {
+                    active = false;
+                    status = -1;
+                    iters = it + 1;
+                }
+            }
+            pol = false;
+            if (!__any(active)) break;
+        }
+        riccati(Pass<0>{});
 
         LPC_TICK(1);
         pending = false;   // the previous step is applied (converged groups stay frozen from here)
 
         // ============================ B: forward predictor + ratio test / centring sums
         T a_aff, S0, S2, dummy;
-        forward(false, a_aff, S0, S2, dummy);
+        forward(Pass<0>{}, a_aff, S0, S2, dummy);
         LPC_TICK(2);
         // mu_aff = [(1 - a) S0 - a^2 S2'] / m with S2' = sum lam dz (t + dz) / t (closed form)
         const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
@@ -1146,7 +1222,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         LPC_TICK(5);
         // ============================ D: forward corrector + step length / new mu
         T amax, T0, C1, C2;
-        forward(true, amax, T0, C1, C2);
+        forward(Pass<1>{}, amax, T0, C1, C2);
         LPC_TICK(6);
         const T a = fmin(T(1), T(0.995) * amax);
         // a failed factorisation (F_uu not positive definite) leaves the iterate as it stood at the
@@ -1168,11 +1244,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         if (k == N && ul) continue;
         T z = ldE(L::Z, k);
         if (pending) z += alpha * ldE(L::DZ, k);
+        if (status < 0) {   // completed by the finish: its step, clamped onto the active bounds
+            const T lb = LB(k), ub = UB(k);
+            z += ldE(L::DZ, k);
+            z = has_bound(lb) ? fmax(z, lb) : z;
+            z = has_bound(ub) ? fmin(z, ub) : z;
+        }
         if (xl) xo[k * NX + r] = z;
         else uo[k * NU + u] = z;
     }
     if (r == 0) {
-        p.status[inst] = status;
+        p.status[inst] = status < 0 ? 0 : status;
         p.iters[inst] = iters;
 #ifdef NMPC_SWEEP_TIMING
         if (timed) {

@@ -198,6 +198,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                         const bool hl = has(lb), hu = has(ub);
                         if (hl && hu) {
                             const T d = T(0.01) * (ub - lb);
+                            v = a >= NX ? T(0.5) * (lb + ub) : v;   // boxed inputs start mid-box
                             v = fmin(fmax(v, lb + d), ub - d);
                         } else if (hl) {
                             v = fmax(v, lb + T(0.01) * fmax(fabs(lb), T(1)));

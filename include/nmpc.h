@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define NMPC_ABI_VERSION 1
+#define NMPC_ABI_VERSION 2
 
 /* solver status codes (acados, src/Readme.md:14-20) */
 #define NMPC_SUCCESS 0
@@ -114,6 +114,11 @@ typedef struct nmpc_ocp_desc {
     double qp_solver_tol_comp; /* <= 0: 1e-15 (fp64) / 1e-7 (fp32); fp32 clamps to >= 1e-7 */
     double qp_solver_tol_res;  /* <= 0: 1e-12 (fp64) / 1e-5 (fp32); fp32 clamps to >= 1e-5 */
     double qp_solver_mu0;      /* <= 0: 1e-2 */
+    /* exact finish (active-set polish): once mu <= qp_solver_polish_mu (retried at
+     * mu / 100 after a rejected attempt) one Newton step with the identified active bounds held
+     * and the others dropped; accepted when it satisfies the QP's KKT sign and bound conditions.
+     * 0: 1e-6 (fp64 handles; fp32 handles never polish); < 0: off */
+    double qp_solver_polish_mu;
 } nmpc_ocp_desc;
 
 typedef struct nmpc_solver nmpc_solver;

@@ -38,14 +38,26 @@ typedef struct {
     const double *lbe, *ube;    /* nx, stage N */
     double tol_comp, tol_res, mu0;
     int max_iter;
+    double polish_mu;           /* > 0: exact finish (active-set polish) once mu <= polish_mu */
 } ocp_ref_desc;
 
 static int has(double b) { return fabs(b) < INFB; }
 
 /* per-instance workspace sizes */
 typedef struct {
-    double *z, *ll, *lu, *dza, *dz, *gc, *gf, *gh, *re, *Pr, *Luu, *Lxu, *lu_vec;
+    double *z, *ll, *lu, *dza, *dz, *gc, *gf, *gh, *re, *Pr, *Luu, *Lxu, *lu_vec, *sg;
 } ws_t;
+
+/* Relative weight of the exact finish's penalty on the identified active bounds: the
+ * penalised solution sits lambda / rho from the bound, and rho / |F| costs about
+ * eps * rho / |F| in the Schur complements, so sqrt(1/eps) balances the two. */
+#define POLISH_RHO 1e8
+/* acceptance of the exact finish, relative to 1 + |bound|: an inactive bound may be violated by
+ * POLISH_TOL (the result is clamped onto it); an active bound's multiplier rho * (bound - z)
+ * must not fall below -rho * POLISH_TOL_ACTIVE (a few ulps: a wrongly fixed bound shows up as
+ * a negative multiplier, i.e. z on the feasible side of the bound) */
+#define POLISH_TOL 1e-9
+#define POLISH_TOL_ACTIVE 1e-15
 
 static void interior(double *v, double l, double u)
 {
@@ -76,6 +88,91 @@ static double UBk(const ocp_ref_desc *d, int k, int i)
     return d->ub[i];
 }
 
+/* Backward Riccati factorisation of the Newton system with barrier / penalty Hessian diagonal
+ * w->sg and gradient `gr` (stage-stacked, nz per stage): fills the per-stage records Pr, Luu,
+ * Lxu, lu_vec used by the forward substitution. Returns 1 on a non-positive pivot. */
+static int backward(const ocp_ref_desc *d, ws_t *w, const double *gr)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu;
+    const double *A = d->A, *B = d->B;
+    double P[NZMAX * NZMAX], M[NZMAX * NZMAX], F[NZMAX * NZMAX], p[NZMAX], v[NZMAX], h[NZMAX];
+    int k, i, j, l;
+    for (i = 0; i < nx; i++) {
+        for (j = 0; j < nx; j++) P[i * nx + j] = d->He[i * nx + j];
+        P[i * nx + i] += w->sg[N * nz + i];
+        p[i] = gr[N * nz + i];
+    }
+    for (k = N - 1; k >= 0; k--) {
+        double *Pr = &w->Pr[k * nx], *Luu = &w->Luu[k * nu * nu], *Lxu = &w->Lxu[k * nx * nu];
+        double *luv = &w->lu_vec[k * nu];
+        for (i = 0; i < nx; i++) {
+            double s = 0.0;
+            for (j = 0; j < nx; j++) s += P[i * nx + j] * w->re[k * nx + j];
+            Pr[i] = s;
+            v[i] = s + p[i];
+        }
+        /* M = P [A B]  (nx x nz) */
+        for (i = 0; i < nx; i++)
+            for (j = 0; j < nz; j++) {
+                double s = 0.0;
+                for (l = 0; l < nx; l++)
+                    s += P[i * nx + l] * (j < nx ? A[l * nx + j] : B[l * nu + (j - nx)]);
+                M[i * nz + j] = s;
+            }
+        /* F = [A B]' M + H + Sigma ; h = [A B]' v + gr */
+        for (i = 0; i < nz; i++) {
+            for (j = 0; j < nz; j++) {
+                double s = d->H[i * nz + j];
+                for (l = 0; l < nx; l++)
+                    s += (i < nx ? A[l * nx + i] : B[l * nu + (i - nx)]) * M[l * nz + j];
+                F[i * nz + j] = s;
+            }
+            double s = gr[k * nz + i];
+            for (l = 0; l < nx; l++) s += (i < nx ? A[l * nx + i] : B[l * nu + (i - nx)]) * v[l];
+            h[i] = s;
+            F[i * nz + i] += w->sg[k * nz + i];
+        }
+        /* Luu = chol(F_uu) (row-major lower) */
+        for (i = 0; i < nu; i++)
+            for (j = 0; j <= i; j++) {
+                double s = F[(nx + i) * nz + nx + j];
+                for (l = 0; l < j; l++) s -= Luu[i * nu + l] * Luu[j * nu + l];
+                if (i == j) {
+                    if (!(s > 0.0)) return 1;
+                    Luu[i * nu + i] = sqrt(s);
+                } else {
+                    Luu[i * nu + j] = s / Luu[j * nu + j];
+                }
+            }
+        /* Lxu = F_xu Luu^-T  (row i: forward substitution) */
+        for (i = 0; i < nx; i++)
+            for (j = 0; j < nu; j++) {
+                double s = F[i * nz + nx + j];
+                for (l = 0; l < j; l++) s -= Lxu[i * nu + l] * Luu[j * nu + l];
+                Lxu[i * nu + j] = s / Luu[j * nu + j];
+            }
+        /* l_u = Luu^-1 h_u */
+        for (j = 0; j < nu; j++) {
+            double s = h[nx + j];
+            for (l = 0; l < j; l++) s -= Luu[j * nu + l] * luv[l];
+            luv[j] = s / Luu[j * nu + j];
+        }
+        if (k > 0) {
+            for (i = 0; i < nx; i++) {
+                for (j = 0; j < nx; j++) {
+                    double s = F[i * nz + j];
+                    for (l = 0; l < nu; l++) s -= Lxu[i * nu + l] * Lxu[j * nu + l];
+                    P[i * nx + j] = s;
+                }
+                double s = h[i];
+                for (l = 0; l < nu; l++) s -= Lxu[i * nu + l] * luv[l];
+                p[i] = s;
+            }
+        }
+    }
+    return 0;
+}
+
 static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref,
                      double *xo, double *uo, int *iters_out, ws_t *w)
 {
@@ -100,13 +197,16 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
             w->gc[k * nz + i] = s;
         }
     }
-    /* initial point: reference projected strictly inside the boxes, x0 pinned */
+    /* initial point: states at the reference, inputs with a two-sided box at its midpoint (the
+     * projected input reference of the force model sits next to the thrust bound and costs ~6
+     * short-step iterations at the start), everything strictly inside the boxes, x0 pinned */
     for (k = 0; k <= N; k++) {
         int n = k < N ? nz : nx;
         const double *y = yref + (size_t)k * ny;
         for (i = 0; i < n; i++) {
-            double val = y[i];   /* LINEAR_LS with Vx=[I;0], Vu=[0;I] layout: y = [x;u] */
+            double val;   /* LINEAR_LS with Vx=[I;0], Vu=[0;I] layout: y = [x;u] */
             if (k < N ? (i < ny) : (i < d->ny_e)) val = y[i]; else val = 0.0;
+            if (i >= nx && has(LBk(d, k, i)) && has(UBk(d, k, i))) val = 0.5 * (LBk(d, k, i) + UBk(d, k, i));
             interior(&val, LBk(d, k, i), UBk(d, k, i));
             Z(k, i) = val;
         }
@@ -149,7 +249,32 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
         }
     double theta = 1.0;
     if (m == 0) m = 1;
+    double polish_at = d->polish_mu > 0.0 ? d->polish_mu : -1.0, rho = 1.0;
+    int polished = 0;
+    for (i = 0; i < nz * nz; i += nz + 1) rho = fmax(rho, fabs(d->H[i]));
+    for (i = 0; i < nx * nx; i += nx + 1) rho = fmax(rho, fabs(d->He[i]));
+    rho *= POLISH_RHO;
 
+    /* ---- forward substitution: direction into out[] ---- */
+#define FORWARD(out) do { \
+        double dx_[NZMAX]; for (i = 0; i < nx; i++) dx_[i] = 0.0; \
+        for (k = 0; k < N; k++) { \
+            const double *Luu_ = &w->Luu[k * nu * nu], *Lxu_ = &w->Lxu[k * nx * nu], *lu_ = &w->lu_vec[k * nu]; \
+            double t_[NZMAX]; \
+            for (j = 0; j < nu; j++) { double s_ = lu_[j]; \
+                for (i = 0; i < nx; i++) s_ += Lxu_[i * nu + j] * dx_[i]; t_[j] = s_; } \
+            for (j = nu - 1; j >= 0; j--) { double s_ = t_[j]; \
+                for (l = j + 1; l < nu; l++) s_ -= Luu_[l * nu + j] * t_[l]; t_[j] = s_ / Luu_[j * nu + j]; } \
+            for (i = 0; i < nx; i++) (out)[k * nz + i] = dx_[i]; \
+            for (j = 0; j < nu; j++) (out)[k * nz + nx + j] = -t_[j]; \
+            for (i = 0; i < nx; i++) { double s_ = w->re[k * nx + i]; \
+                for (j = 0; j < nx; j++) s_ += A[i * nx + j] * dx_[j]; \
+                for (j = 0; j < nu; j++) s_ += B[i * nu + j] * (out)[k * nz + nx + j]; \
+                t_[nu + i] = s_; } \
+            for (i = 0; i < nx; i++) dx_[i] = t_[nu + i]; \
+        } \
+        for (i = 0; i < nx; i++) (out)[N * nz + i] = dx_[i]; \
+    } while (0)
     for (it = 0; it < d->max_iter; it++) {
         /* complementarity measure */
         double mu = 0.0;
@@ -173,104 +298,71 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
                 for (j = 0; j < nu; j++) s += B[i * nu + j] * Z(k, nx + j);
                 w->re[k * nx + i] = s;
             }
+        if (mu <= polish_at) {
+            /* exact finish: a bound is active where its multiplier exceeds its slack; one Newton
+             * step on the QP with those bounds held by a penalty of weight rho (inactive bounds
+             * dropped) lands on the active-set solution. Accepted when every inactive bound
+             * holds and every active one keeps a non-negative multiplier rho * (bound - z);
+             * otherwise the IPM iterate is untouched and the next attempt waits for
+             * mu <= polish_at / 100. */
+            polish_at *= 1e-2;
+            for (k = 0; k <= N; k++) {
+                int n = k < N ? nz : nx;
+                for (i = 0; i < n; i++) {
+                    double sgv = 0.0, g = w->gf[k * nz + i];
+                    if (!(k == 0 && i < nx)) {
+                        double lbv = LBk(d, k, i), ubv = UBk(d, k, i);
+                        if (LL(k, i) > 0.0 && LL(k, i) > Z(k, i) - lbv) { sgv = rho; g += rho * (Z(k, i) - lbv); }
+                        else if (LU(k, i) > 0.0 && LU(k, i) > ubv - Z(k, i)) { sgv = rho; g += rho * (Z(k, i) - ubv); }
+                    }
+                    w->sg[k * nz + i] = sgv;
+                    w->gh[k * nz + i] = g;
+                }
+            }
+            if (backward(d, w, w->gh) == 0) {
+                FORWARD(w->dz);
+                int ok = 1;
+                for (k = 0; k <= N && ok; k++) {
+                    int n = k < N ? nz : nx;
+                    for (i = (k == 0 ? nx : 0); i < n; i++) {
+                        double zn = Z(k, i) + w->dz[k * nz + i], lbv = LBk(d, k, i), ubv = UBk(d, k, i);
+                        if (w->sg[k * nz + i] > 0.0) {
+                            if (LL(k, i) > 0.0 && LL(k, i) > Z(k, i) - lbv
+                                    ? zn > lbv + POLISH_TOL_ACTIVE * (1.0 + fabs(lbv))
+                                    : zn < ubv - POLISH_TOL_ACTIVE * (1.0 + fabs(ubv))) { ok = 0; break; }
+                        } else if ((has(lbv) && zn < lbv - POLISH_TOL * (1.0 + fabs(lbv))) ||
+                                   (has(ubv) && zn > ubv + POLISH_TOL * (1.0 + fabs(ubv)))) { ok = 0; break; }
+                    }
+                }
+                if (ok) {
+                    for (k = 0; k <= N; k++) {
+                        int n = k < N ? nz : nx;
+                        for (i = (k == 0 ? nx : 0); i < n; i++) {
+                            double zn = Z(k, i) + w->dz[k * nz + i], lbv = LBk(d, k, i), ubv = UBk(d, k, i);
+                            if (has(lbv) && zn < lbv) zn = lbv;
+                            if (has(ubv) && zn > ubv) zn = ubv;
+                            Z(k, i) = zn;
+                        }
+                    }
+                    status = 0;
+                    polished = 1;
+                    break;
+                }
+            }
+        }
         /* ---- backward factorisation (+ predictor vector) ---- */
-        for (i = 0; i < nx; i++) {
-            for (j = 0; j < nx; j++) P[i * nx + j] = d->He[i * nx + j];
-            double lbv = LBk(d, N, i), ubv = UBk(d, N, i);
-            if (LL(N, i) > 0.0) P[i * nx + i] += LL(N, i) / (Z(N, i) - lbv);
-            if (LU(N, i) > 0.0) P[i * nx + i] += LU(N, i) / (ubv - Z(N, i));
-            p[i] = w->gf[N * nz + i];
-        }
-        for (k = N - 1; k >= 0; k--) {
-            double *Pr = &w->Pr[k * nx], *Luu = &w->Luu[k * nu * nu], *Lxu = &w->Lxu[k * nx * nu];
-            double *luv = &w->lu_vec[k * nu];
-            for (i = 0; i < nx; i++) {
-                double s = 0.0;
-                for (j = 0; j < nx; j++) s += P[i * nx + j] * w->re[k * nx + j];
-                Pr[i] = s;
-                v[i] = s + p[i];
-            }
-            /* M = P [A B]  (nx x nz) */
-            for (i = 0; i < nx; i++)
-                for (j = 0; j < nz; j++) {
-                    double s = 0.0;
-                    for (l = 0; l < nx; l++)
-                        s += P[i * nx + l] * (j < nx ? A[l * nx + j] : B[l * nu + (j - nx)]);
-                    M[i * nz + j] = s;
+        for (k = 0; k <= N; k++) {
+            int n = k < N ? nz : nx;
+            for (i = 0; i < n; i++) {
+                double sgv = 0.0;
+                if (!(k == 0 && i < nx)) {
+                    if (LL(k, i) > 0.0) sgv += LL(k, i) / (Z(k, i) - LBk(d, k, i));
+                    if (LU(k, i) > 0.0) sgv += LU(k, i) / (UBk(d, k, i) - Z(k, i));
                 }
-            /* F = [A B]' M + H + Sigma ; h = [A B]' v + gf */
-            for (i = 0; i < nz; i++) {
-                for (j = 0; j < nz; j++) {
-                    double s = d->H[i * nz + j];
-                    for (l = 0; l < nx; l++)
-                        s += (i < nx ? A[l * nx + i] : B[l * nu + (i - nx)]) * M[l * nz + j];
-                    F[i * nz + j] = s;
-                }
-                double s = w->gf[k * nz + i];
-                for (l = 0; l < nx; l++) s += (i < nx ? A[l * nx + i] : B[l * nu + (i - nx)]) * v[l];
-                h[i] = s;
-                if (k == 0 && i < nx) continue;
-                if (LL(k, i) > 0.0) F[i * nz + i] += LL(k, i) / (Z(k, i) - LBk(d, k, i));
-                if (LU(k, i) > 0.0) F[i * nz + i] += LU(k, i) / (UBk(d, k, i) - Z(k, i));
-            }
-            /* Luu = chol(F_uu) (row-major lower) */
-            for (i = 0; i < nu; i++)
-                for (j = 0; j <= i; j++) {
-                    double s = F[(nx + i) * nz + nx + j];
-                    for (l = 0; l < j; l++) s -= Luu[i * nu + l] * Luu[j * nu + l];
-                    if (i == j) {
-                        if (!(s > 0.0)) { status = 4; goto done; }
-                        Luu[i * nu + i] = sqrt(s);
-                    } else {
-                        Luu[i * nu + j] = s / Luu[j * nu + j];
-                    }
-                }
-            /* Lxu = F_xu Luu^-T  (row i: forward substitution) */
-            for (i = 0; i < nx; i++)
-                for (j = 0; j < nu; j++) {
-                    double s = F[i * nz + nx + j];
-                    for (l = 0; l < j; l++) s -= Lxu[i * nu + l] * Luu[j * nu + l];
-                    Lxu[i * nu + j] = s / Luu[j * nu + j];
-                }
-            /* l_u = Luu^-1 h_u */
-            for (j = 0; j < nu; j++) {
-                double s = h[nx + j];
-                for (l = 0; l < j; l++) s -= Luu[j * nu + l] * luv[l];
-                luv[j] = s / Luu[j * nu + j];
-            }
-            if (k > 0) {
-                for (i = 0; i < nx; i++) {
-                    for (j = 0; j < nx; j++) {
-                        double s = F[i * nz + j];
-                        for (l = 0; l < nu; l++) s -= Lxu[i * nu + l] * Lxu[j * nu + l];
-                        P[i * nx + j] = s;
-                    }
-                    double s = h[i];
-                    for (l = 0; l < nu; l++) s -= Lxu[i * nu + l] * luv[l];
-                    p[i] = s;
-                }
+                w->sg[k * nz + i] = sgv;
             }
         }
-        /* ---- forward substitution: direction into out[] ---- */
-#define FORWARD(out) do { \
-        double dx_[NZMAX]; for (i = 0; i < nx; i++) dx_[i] = 0.0; \
-        for (k = 0; k < N; k++) { \
-            const double *Luu_ = &w->Luu[k * nu * nu], *Lxu_ = &w->Lxu[k * nx * nu], *lu_ = &w->lu_vec[k * nu]; \
-            double t_[NZMAX]; \
-            for (j = 0; j < nu; j++) { double s_ = lu_[j]; \
-                for (i = 0; i < nx; i++) s_ += Lxu_[i * nu + j] * dx_[i]; t_[j] = s_; } \
-            for (j = nu - 1; j >= 0; j--) { double s_ = t_[j]; \
-                for (l = j + 1; l < nu; l++) s_ -= Luu_[l * nu + j] * t_[l]; t_[j] = s_ / Luu_[j * nu + j]; } \
-            for (i = 0; i < nx; i++) (out)[k * nz + i] = dx_[i]; \
-            for (j = 0; j < nu; j++) (out)[k * nz + nx + j] = -t_[j]; \
-            for (i = 0; i < nx; i++) { double s_ = w->re[k * nx + i]; \
-                for (j = 0; j < nx; j++) s_ += A[i * nx + j] * dx_[j]; \
-                for (j = 0; j < nu; j++) s_ += B[i * nu + j] * (out)[k * nz + nx + j]; \
-                t_[nu + i] = s_; } \
-            for (i = 0; i < nx; i++) dx_[i] = t_[nu + i]; \
-        } \
-        for (i = 0; i < nx; i++) (out)[N * nz + i] = dx_[i]; \
-    } while (0)
+        if (backward(d, w, w->gf)) { status = 4; goto done; }
         FORWARD(w->dza);
 
         /* affine step length and mu_aff */
@@ -395,7 +487,7 @@ done:
         for (i = 0; i < nx; i++) xo[k * nx + i] = Z(k, i);
     for (k = 0; k < N; k++)
         for (j = 0; j < nu; j++) uo[k * nu + j] = Z(k, nx + j);
-    *iters_out = it;
+    *iters_out = it + polished;
     return status;
 #undef Z
 #undef LL
@@ -422,12 +514,13 @@ int riccati_ipm_solve_batch(const ocp_ref_desc *d, int batch, const double *x0, 
 #pragma omp parallel num_threads(nthreads) reduction(+ : nfail)
     {
         size_t S = (size_t)(N + 1) * nz;
-        double *buf = (double *)malloc(sizeof(double) * (8 * S + (size_t)N * (2 * nx + nu * nu + nx * nu + nu)));
+        double *buf = (double *)malloc(sizeof(double) * (9 * S + (size_t)N * (2 * nx + nu * nu + nx * nu + nu)));
         ws_t w;
         w.z = buf; w.ll = w.z + S; w.lu = w.ll + S; w.dza = w.lu + S; w.dz = w.dza + S;
         w.gc = w.dz + S; w.gf = w.gc + S; w.gh = w.gf + S;
         w.re = w.gh + S; w.Pr = w.re + (size_t)N * nx; w.Luu = w.Pr + (size_t)N * nx;
         w.Lxu = w.Luu + (size_t)N * nu * nu; w.lu_vec = w.Lxu + (size_t)N * nx * nu;
+        w.sg = w.lu_vec + (size_t)N * nu;
 #pragma omp for schedule(dynamic, 16)
         for (int b = 0; b < batch; b++) {
             int st = solve_one(d, x0 + (size_t)b * nx, yref + (size_t)b * ystride,

@@ -7,6 +7,7 @@ window are stored together with the C oracle's answer (oracle/c/riccati_ipm.c): 
 F_uu loses positive definiteness, the iterate as it stood at the start of that iteration.
 
     python tests/golden/make_failure_case.py [gpurun_out/fail.npz]
+    python tests/golden/make_failure_case.py --refresh   # same inputs, the current oracle's answer
 """
 import os
 import sys
@@ -20,16 +21,21 @@ from oracle import cref, models  # noqa: E402
 
 
 def main(src):
-    d = np.load(src)
-    N = int(d["N"])
-    step, off, x0 = int(d["step"][0]), int(d["offset"][0]), d["x0"][0]
-    spec = models.MODELS["jerk"](N)
-    table = d["table"]
-    t = (off + step) % 500
-    y = np.concatenate([table[t:t + N, :spec.ny].ravel(), table[t + N, :spec.nx]])
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "qp_failure.npz")
+    if src == "--refresh":
+        d = np.load(out)
+        x0, y, N, step, off = d["jerk_N40_x0"][0], d["jerk_N40_yref"][0], 40, -1, -1
+        spec = models.MODELS["jerk"](N)
+    else:
+        d = np.load(src)
+        N = int(d["N"])
+        step, off, x0 = int(d["step"][0]), int(d["offset"][0]), d["x0"][0]
+        spec = models.MODELS["jerk"](N)
+        table = d["table"]
+        t = (off + step) % 500
+        y = np.concatenate([table[t:t + N, :spec.ny].ravel(), table[t + N, :spec.nx]])
     X, U, st, it = cref.RiccatiIpmRef(spec).solve(x0[None], y[None], nthreads=1)
     assert st[0] == 4, st
-    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "qp_failure.npz")
     np.savez(out, jerk_N40_x0=x0[None], jerk_N40_yref=y[None], jerk_N40_X=X, jerk_N40_U=U,
              jerk_N40_status=st, jerk_N40_iters=it)
     print(f"{out}: step {step} offset {off} x0 {x0} -> status {st[0]} after {it[0]} iterations")

@@ -73,9 +73,8 @@ def test_batch_parity_fp64(key, cases):
     assert e.max() < TOL64, e.max()
     # same algorithm as the C baseline: iteration counts agree (+-1 from rounding order)
     name, N = split(key)
-    o = OCPS[name](N).solver_options   # the OCP's IPM tolerances (quad13 sets its own)
-    R = cref.RiccatiIpmRef(models.MODELS[name](N), tol_comp=o.qp_solver_tol_comp or 1e-15,
-                           tol_res=o.qp_solver_tol_stat or 1e-12)
+    o = OCPS[name](N).solver_options   # the OCP's IPM tolerances (quad13 sets its own) + exact finish
+    R = cref.RiccatiIpmRef.for_options(models.MODELS[name](N), o)
     _, _, stc, itc = R.solve(cases[key + "_x0"], cases[key + "_yref"])
     it = s.get_batch_int("qp_iter")
     assert np.abs(it - itc).max() <= 1, (it, itc)
