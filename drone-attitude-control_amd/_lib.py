@@ -42,7 +42,7 @@ class OcpDesc(ctypes.Structure):
         ("x0", _dp),
         ("qp_solver_iter_max", ctypes.c_int), ("qp_solver_tol_comp", ctypes.c_double),
         ("qp_solver_tol_res", ctypes.c_double), ("qp_solver_mu0", ctypes.c_double),
-        ("qp_solver_polish_mu", ctypes.c_double),
+        ("qp_solver_polish_mu", ctypes.c_double), ("qp_solver_polish_steps", ctypes.c_int),
     ]
 
 

@@ -140,9 +140,11 @@ class AcadosOcpOptions:
         self.qp_solver_tol_comp = None
         self.qp_solver_tol_stat = None
         self.qp_solver_mu0 = None
-        # engine extension (no acados counterpart): exact-finish threshold, None = library default
-        # (1e-6 on fp64 handles), < 0 = off (include/nmpc.h qp_solver_polish_mu)
+        # engine extensions (no acados counterpart): exact-finish threshold and active-set steps,
+        # None = library defaults (1 and 12 on fp64 handles), threshold < 0 = off
+        # (include/nmpc.h qp_solver_polish_mu / qp_solver_polish_steps)
         self.qp_solver_polish_mu = None
+        self.qp_solver_polish_steps = None
         self.cost_scaling = "time_steps"   # acados default: stage cost x time step
 
 
@@ -229,7 +231,8 @@ def describe_ocp(ocp):
         qp_solver_tol_comp=float(opts.qp_solver_tol_comp or (opts.qp_tol or 0.0) or 0.0),
         qp_solver_tol_res=float(opts.qp_solver_tol_stat or (opts.qp_tol or 0.0) or 0.0),
         qp_solver_mu0=float(opts.qp_solver_mu0 or 0.0),
-        qp_solver_polish_mu=float(getattr(opts, "qp_solver_polish_mu", None) or 0.0))
+        qp_solver_polish_mu=float(getattr(opts, "qp_solver_polish_mu", None) or 0.0),
+        qp_solver_polish_steps=int(getattr(opts, "qp_solver_polish_steps", None) or 0))
 
 
 class AcadosOcpSolver:
@@ -285,6 +288,7 @@ class AcadosOcpSolver:
         d.qp_solver_tol_res = D["qp_solver_tol_res"]
         d.qp_solver_mu0 = D["qp_solver_mu0"]
         d.qp_solver_polish_mu = D["qp_solver_polish_mu"]
+        d.qp_solver_polish_steps = D["qp_solver_polish_steps"]
         h = ctypes.c_void_p()
         rc = self.lib.nmpc_create(ctypes.byref(d), self.batch, int(device), prec, ctypes.byref(h))
         if rc != 0:

@@ -196,6 +196,7 @@ struct nmpc_solver {
     int max_iter = 50;
     double tol_comp = 0, tol_res = 0, mu0 = 0, inv_m = 1, ts = 0, scale_e = 1;
     double polish_mu = 0, polish_rho = 0;
+    int polish_steps = 12;
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
@@ -219,7 +220,8 @@ struct nmpc_solver {
     void *d_table = nullptr, *d_state = nullptr, *d_plant = nullptr, *d_wcl = nullptr;
     int *d_offsets = nullptr;
     double *d_acc = nullptr, *d_noise = nullptr;
-    int cl_step = 0, cl_last_launches = 0;
+    int cl_step = 0, cl_last_launches = 0, cl_last_steps = 0;
+    double *d_fnoise = nullptr;   // fused closed loop: noise draws of a launch's steps [B][64]
     std::vector<hipEvent_t> cl_events;
     double cl_last_ms = 0.0;
     double cost_s = 1.0;  // stage cost factor (time step or 1)
@@ -255,7 +257,8 @@ void free_all(nmpc_solver *h)
     hipSetDevice(h->device);
     for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
-                    (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i})
+                    (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
+                    (void *)h->d_fnoise})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -324,10 +327,19 @@ int launch_cond(nmpc_solver *h, hipEvent_t e0, hipEvent_t e1)
 }
 
 template <typename T>
-int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
+nmpc::ClParams<T> cl_params(nmpc_solver *h);
+
+// cl_steps > 0: fused closed loop of that many steps (lane-per-component / wavefront kernels)
+template <typename T>
+int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0)
 {
     if (h->cond) return launch_cond<T>(h, e0, e1);
-    nmpc::IpmParams<T> p;
+    nmpc::IpmParams<T> p{};
+    p.cl_steps = cl_steps;
+    if (cl_steps > 0) {
+        p.cl = cl_params<T>(h);
+        p.cl_noise = h->d_fnoise;
+    }
     p.B = h->batch;
     p.N = h->N;
     p.ny = h->ny;
@@ -340,6 +352,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
     p.inv_m = (T)h->inv_m;
     p.polish_mu = (T)h->polish_mu;
     p.polish_rho = (T)h->polish_rho;
+    p.polish_steps = h->polish_steps;
     const char *m = (const char *)h->d_model;
     p.AB = (const T *)(m + h->off_AB);
     p.ABt = (const T *)(m + h->off_ABt);
@@ -609,14 +622,15 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         h->tol_res = std::max(h->tol_res, 1e-5);
     }
     h->mu0 = d->qp_solver_mu0 > 0 ? d->qp_solver_mu0 : 1e-2;
-    // exact finish: fp64 only (the penalty weight below needs ~16 digits); the penalty is 1e8 x
-    // the largest cost curvature, as in oracle/c/riccati_ipm.c (POLISH_RHO)
-    h->polish_mu = !f64 || d->qp_solver_polish_mu < 0 ? 0.0 : (d->qp_solver_polish_mu > 0 ? d->qp_solver_polish_mu : 1e-6);
+    // exact finish: fp64 only (the penalised solve needs ~16 digits); the penalty is 1e6 x the
+    // largest cost curvature, as in oracle/c/riccati_ipm.c (POLISH_RHO)
+    h->polish_mu = !f64 || d->qp_solver_polish_mu < 0 ? 0.0 : (d->qp_solver_polish_mu > 0 ? d->qp_solver_polish_mu : 1.0);
+    h->polish_steps = d->qp_solver_polish_steps > 0 ? d->qp_solver_polish_steps : 12;
     {
         double hmax = 1.0;
         for (int i = 0; i < nz; i++) hmax = std::max(hmax, std::fabs(h->H[i * nz + i]));
         for (int i = 0; i < nx; i++) hmax = std::max(hmax, std::fabs(h->He[i * nx + i]));
-        h->polish_rho = 1e8 * hmax;
+        h->polish_rho = 1e6 * hmax;
     }
     // ---- host staging
     h->h_x0.assign((size_t)batch * nx, 0.0);
@@ -1081,6 +1095,7 @@ namespace {
 template <typename T>
 nmpc::ClParams<T> cl_params(nmpc_solver *h)
 {
+    // (declared above launch)
     nmpc::ClParams<T> p{};
     const nmpc_closed_loop_desc &d = h->cl;
     p.B = h->batch;
@@ -1122,6 +1137,30 @@ nmpc::ClParams<T> cl_params(nmpc_solver *h)
     p.noise_len = d.noise_len;
     p.acc = h->d_acc;
     return p;
+}
+
+// fused closed loop: the kernel families that run the steps inside the solve kernel
+bool cl_fused(nmpc_solver *h)
+{
+    const char *env = std::getenv("NMPC_CL_FUSED");
+    if (env && env[0] == '0') return false;
+    if (h->cond) return false;
+    const int kind = h->precision == NMPC_FP64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
+    return kind == 0 || kind == 1;
+}
+
+constexpr int CL_FUSED_CHUNK = 64;
+
+template <typename T>
+int cl_fused_enqueue(nmpc_solver *h, int launch_idx, int n)
+{
+    nmpc::ClParams<T> p = cl_params<T>(h);
+    hipError_t e = nmpc::cl_noise_launch<T>(p, h->cl_step, n, h->d_fnoise, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
+    const int r = launch<T>(h, h->cl_events[2 * launch_idx], h->cl_events[2 * launch_idx + 1], n);
+    if (r < 0) return r;
+    h->cl_step += n;
+    return 0;
 }
 
 template <typename T>
@@ -1225,11 +1264,24 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
         h->cl_events.push_back(e);
     }
     h->out_valid = false;
-    for (int s = 0; s < steps; s++) {
-        const int r = h->precision == NMPC_FP64 ? cl_step_enqueue<double>(h, s) : cl_step_enqueue<float>(h, s);
-        if (r < 0) return r;
+    int launches = 0;
+    if (cl_fused(h)) {
+        if (!h->d_fnoise && hipMalloc((void **)&h->d_fnoise, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(double)) != hipSuccess)
+            return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: noise buffer");
+        for (int s = 0; s < steps; s += CL_FUSED_CHUNK, launches++) {
+            const int n = std::min(CL_FUSED_CHUNK, steps - s);
+            const int r = h->precision == NMPC_FP64 ? cl_fused_enqueue<double>(h, launches, n)
+                                                    : cl_fused_enqueue<float>(h, launches, n);
+            if (r < 0) return r;
+        }
+    } else {
+        for (int s = 0; s < steps; s++, launches++) {
+            const int r = h->precision == NMPC_FP64 ? cl_step_enqueue<double>(h, s) : cl_step_enqueue<float>(h, s);
+            if (r < 0) return r;
+        }
     }
-    h->cl_last_launches = steps;
+    h->cl_last_launches = launches;
+    h->cl_last_steps = steps;
     // the loop rewrote the device x0 / yref: the next nmpc_solve re-uploads the host-staged inputs
     h->x0_dirty = h->yref_dirty = true;
     if (sync) {
@@ -1248,7 +1300,7 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_stats");
     std::vector<double> acc((size_t)h->batch * 4);
     hipMemcpy(acc.data(), h->d_acc, acc.size() * sizeof(double), hipMemcpyDeviceToHost);
-    double v[7] = {0, 0, 0, 0, 0, 0, 0};
+    double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = 0; b < h->batch; b++)
         for (int j = 0; j < 4; j++) v[j] += acc[(size_t)b * 4 + j];
     double ms = 0.0;
@@ -1263,7 +1315,8 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
     double mean = 0.0;
     for (int b = 0; b < h->batch; b++) mean += it[b];
     v[6] = mean / h->batch;
-    for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+    v[7] = h->cl_last_steps;
+    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
     return 0;
 }
 

@@ -8,6 +8,32 @@
 
 namespace nmpc {
 
+// closed-loop step kernels (nmpc_closed_loop.hip)
+template <typename T>
+struct ClParams {
+    int B, N, ny, ny_e, nx, nu;
+    int plant;        // 0 controller model, 1 Crazyflie + force converter, 2 Crazyflie + jerk converter
+    int period;       // reference rows per period (start row = (offset + step) % period)
+    int table_cols;
+    int step;
+    int cost_stage;   // X_opt = x_{cost_stage} (0: force_model/controller.py:39, 1: jerk :39)
+    int ncl, aed_dims, noise_dims, substeps;
+    long long inst_base;
+    unsigned long long seed;
+    double noise_std, mass, g, dt, dt_conv;
+    const T *table;   // [rows][table_cols]
+    const int *offset;
+    T *state;         // [B][nx]
+    T *x0;            // engine input [B][nx]
+    T *yref;          // engine input [B][N*ny + ny_e]
+    const T *xout, *uout;
+    const int *status;
+    const T *A, *Bm, *c;   // plant == 0
+    const T *wcl;     // [ncl]
+    const double *noise_table;   // optional [B][noise_len] (replaces Philox draws)
+    int noise_len;
+    double *acc;      // [B][4] cost, aed numerator, failures, steps
+};
 // Kernel parameters of the batched IPM solve (nmpc_ipm.hip). All pointers are device
 // pointers. Model data (AB..ubnd) is shared by every instance of a handle.
 template <typename T>
@@ -20,6 +46,7 @@ struct IpmParams {
     T tol_comp, tol_res, mu0, inv_m;
     T polish_mu;    // exact finish threshold (0: off)
     T polish_rho;   // penalty on the identified active bounds in the finish
+    int polish_steps;   // active-set Newton steps per finish run
     const T *AB;    // [nx][nx+nu]   discrete [A B], row-major
     const T *ABt;   // [nx+nu][nx]   its transpose
     const T *c;     // [nx]
@@ -39,6 +66,12 @@ struct IpmParams {
     unsigned long long *cycles;   // optional [B][5] clock cycles per sweep type A..D + total (tuning, env NMPC_SWEEP_CYCLES)
     int ipw;                      // lane-per-instance kernel: instances per wavefront (lanes 0 .. ipw-1)
     long long lpi_stride;         // lane-per-instance kernel: scratch elements between words (>= slots)
+    // fused closed loop (lane-per-component and wavefront kernels): > 0 runs cl_steps closed-loop
+    // steps per instance inside the solve kernel — yref window and x0 read from cl.table / cl.state,
+    // the plant advance (cl_advance_instance) after each solve — with no grid-wide step barrier
+    int cl_steps;
+    ClParams<T> cl;
+    const double *cl_noise;   // [B][cl_steps] noise draws of the launch's steps (cl_noise_launch)
 };
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);
@@ -109,34 +142,12 @@ bool cond_build(int nx, int nu, int N, int ny, int ny_e, const std::vector<doubl
                 const std::vector<double> &He, const std::vector<double> &Ge, const std::vector<double> &lbnd,
                 const std::vector<double> &ubnd, CondHost &out);
 
-// closed-loop step kernels (nmpc_closed_loop.hip)
-template <typename T>
-struct ClParams {
-    int B, N, ny, ny_e, nx, nu;
-    int plant;        // 0 controller model, 1 Crazyflie + force converter, 2 Crazyflie + jerk converter
-    int period;       // reference rows per period (start row = (offset + step) % period)
-    int table_cols;
-    int step;
-    int cost_stage;   // X_opt = x_{cost_stage} (0: force_model/controller.py:39, 1: jerk :39)
-    int ncl, aed_dims, noise_dims, substeps;
-    long long inst_base;
-    unsigned long long seed;
-    double noise_std, mass, g, dt, dt_conv;
-    const T *table;   // [rows][table_cols]
-    const int *offset;
-    T *state;         // [B][nx]
-    T *x0;            // engine input [B][nx]
-    T *yref;          // engine input [B][N*ny + ny_e]
-    const T *xout, *uout;
-    const int *status;
-    const T *A, *Bm, *c;   // plant == 0
-    const T *wcl;     // [ncl]
-    const double *noise_table;   // optional [B][noise_len] (replaces Philox draws)
-    int noise_len;
-    double *acc;      // [B][4] cost, aed numerator, failures, steps
-};
 template <typename T>
 hipError_t cl_prepare_launch(const ClParams<T> &p, hipStream_t s);
+// noise draws of steps [step0, step0 + nsteps) for every instance: out[b][s] (cl_advance_instance's
+// draw: the user table if given, else Philox / Box-Muller, else 0)
+template <typename T>
+hipError_t cl_noise_launch(const ClParams<T> &p, int step0, int nsteps, double *out, hipStream_t s);
 template <typename T>
 hipError_t cl_advance_launch(const ClParams<T> &p, hipStream_t s);
 

@@ -42,6 +42,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "nmpc_cl_device.h"
 #include "nmpc_internal.h"
 #include "nmpc_lpc_geom.h"
 
@@ -201,7 +202,7 @@ __device__ __forceinline__ void chol_solve(const T (&lf)[NU * (NU + 1) / 2], T (
 //   crec[k] = [ F_uu^-1 factor (packed, inverse diagonal) | Pr_k (nx) | corrector rhs (nz) ]
 //                                                                         backward sweep C
 struct ScratchLayout {
-    size_t z, ll, lu, gc, gf, sg, dza, dz, frec, crec, total;
+    size_t z, ll, lu, gc, gf, sg, dza, dz, frec, crec, act, total;
     int rsf, rsc;   // record sizes (elements)
     __host__ __device__ ScratchLayout(int N, int nx, int nu)
     {
@@ -218,7 +219,8 @@ struct ScratchLayout {
         dz = dza + S;
         frec = dz + S;
         crec = frec + (size_t)N * rsf;
-        total = crec + (size_t)N * rsc;
+        act = crec + (size_t)N * rsc;   // the last solution's active flags (fused closed loop warm start)
+        total = act + S;
         total = (total + 31) & ~size_t(31);
     }
 };
@@ -365,638 +367,728 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                                             (int)(IPW * L.total * sizeof(T)), 0x00020000);
     S.go = (unsigned)grp * (unsigned)(L.total * sizeof(T));
     const unsigned Lz = L.z, Lll = L.ll, Llu = L.lu, Lgc = L.gc, Lgf = L.gf, Lsg = L.sg, Ldza = L.dza, Ldz = L.dz;
-    const unsigned Lfrec = L.frec, Lcrec = L.crec;
+    const unsigned Lfrec = L.frec, Lcrec = L.crec, Lact = L.act;
     T *rb = w + Gm::I_RB;
-    const T *yref = p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
-    const T *x0 = p.x0 + (size_t)inst * NX;
     const int nel = (N + 1) * NZ;
     auto stype = [&](int k) { return k == 0 ? 0 : (k == N ? 2 : 1); };
 
-    // ------------------------------------------------------------------ initial point
-    for (int e = ll; e < nel; e += G) {
-        const int k = e / NZ, i = e % NZ;
-        T z = 0, lam_l = 0, lam_u = 0, gc = 0;
-        if (k < N || i < NX) {
-            const T *yk = yref + (size_t)k * p.ny;
-            if (k < N) {
-                for (int j = 0; j < p.ny; j++) gc += p.G[i * p.ny + j] * yk[j];
-            } else {
-                for (int j = 0; j < p.ny_e; j++) gc += p.Ge[i * p.ny_e + j] * yk[j];
-            }
-            if (k == 0 && i < NX) {
-                z = x0[i];
-            } else {
-                z = p.yref_is_z ? yk[i] : T(0);
-                const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
-                const bool hl = has_bound(lb), hu = has_bound(ub);
-                if (hl && hu) {
-                    const T d = T(0.01) * (ub - lb);
-                    z = i >= NX ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
-                    z = fmin(fmax(z, lb + d), ub - d);
-                } else if (hl) {
-                    z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
-                } else if (hu) {
-                    z = fmin(z, ub - T(0.01) * fmax(fabs(ub), T(1)));
+    // one solve per closed-loop step; plain solves run one step (p.cl_steps = 0)
+    const bool fused = p.cl_steps > 0;
+    const int nsteps = fused ? p.cl_steps : 1;
+    for (int cstep = 0; cstep < nsteps; cstep++) {
+        // fused closed loop: the yref window straight from the reference table rows (offset + step) %
+        // period (cl_prepare_kernel's gather), x0 from the closed-loop state
+        const int t_ref = fused ? (p.cl.offset[inst] + p.cl.step + cstep) % p.cl.period : 0;
+        const T *yref = fused ? p.cl.table + (size_t)t_ref * p.cl.table_cols
+                              : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
+        const int yrow = fused ? p.cl.table_cols : p.ny;
+        const T *x0 = (fused ? p.cl.state : p.x0) + (size_t)inst * NX;
+        // ------------------------------------------------------------------ initial point
+        for (int e = ll; e < nel; e += G) {
+            const int k = e / NZ, i = e % NZ;
+            T z = 0, lam_l = 0, lam_u = 0, gc = 0;
+            if (k < N || i < NX) {
+                const T *yk = yref + (size_t)k * yrow;
+                if (k < N) {
+                    for (int j = 0; j < p.ny; j++) gc += p.G[i * p.ny + j] * yk[j];
+                } else {
+                    for (int j = 0; j < p.ny_e; j++) gc += p.Ge[i * p.ny_e + j] * yk[j];
                 }
-                if (hl) lam_l = p.mu0 / (z - lb);
-                if (hu) lam_u = p.mu0 / (ub - z);
+                if (k == 0 && i < NX) {
+                    z = x0[i];
+                } else {
+                    z = p.yref_is_z ? yk[i] : T(0);
+                    const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+                    const bool hl = has_bound(lb), hu = has_bound(ub);
+                    if (hl && hu) {
+                        const T d = T(0.01) * (ub - lb);
+                        z = i >= NX ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
+                        z = fmin(fmax(z, lb + d), ub - d);
+                    } else if (hl) {
+                        z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
+                    } else if (hu) {
+                        z = fmin(z, ub - T(0.01) * fmax(fabs(ub), T(1)));
+                    }
+                    if (hl) lam_l = p.mu0 / (z - lb);
+                    if (hu) lam_u = p.mu0 / (ub - z);
+                }
+            }
+            S.st(Lz, e, z);
+            S.st(Lll, e, lam_l);
+            S.st(Llu, e, lam_u);
+            S.st(Lgc, e, gc);
+        }
+        SWEEP_FENCE();
+        T r0 = 0, mu = 0;
+        for (int e = ll; e < nel; e += G) {
+            const int k = e / NZ, i = e % NZ;
+            if (k == N && i >= NX) continue;
+            const unsigned k0 = (unsigned)(k * NZ);
+            if (!(k == 0 && i < NX)) {
+                T g = S.ld(Lgc, e);
+                if (k < N) {
+                    for (int b = 0; b < NZ; b++) g += ch[i * LDZ + b] * S.ld(Lz, k0 + b);
+                } else {
+                    for (int b = 0; b < NX; b++) g += che[i * LDX + b] * S.ld(Lz, k0 + b);
+                }
+                const T la = S.ld(Lll, e), lu_ = S.ld(Llu, e);
+                r0 = fmax(r0, fabs(g - la + lu_));
+                const T z = S.ld(Lz, e);
+                if (la > T(0)) mu += la * (z - clb[stype(k) * LDZ + i]);
+                if (lu_ > T(0)) mu += lu_ * (cub[stype(k) * LDZ + i] - z);
+            }
+            if (k < N && i < NX) {
+                T r = cc[i] - S.ld(Lz, k0 + NZ + i);
+                for (int j = 0; j < NZ; j++) r += cab[i * LDZ + j] * S.ld(Lz, k0 + j);
+                r0 = fmax(r0, fabs(r));
             }
         }
-        S.st(Lz, e, z);
-        S.st(Lll, e, lam_l);
-        S.st(Llu, e, lam_u);
-        S.st(Lgc, e, gc);
-    }
-    SWEEP_FENCE();
-    T r0 = 0, mu = 0;
-    for (int e = ll; e < nel; e += G) {
-        const int k = e / NZ, i = e % NZ;
-        if (k == N && i >= NX) continue;
-        const unsigned k0 = (unsigned)(k * NZ);
-        if (!(k == 0 && i < NX)) {
-            T g = S.ld(Lgc, e);
-            if (k < N) {
-                for (int b = 0; b < NZ; b++) g += ch[i * LDZ + b] * S.ld(Lz, k0 + b);
-            } else {
-                for (int b = 0; b < NX; b++) g += che[i * LDX + b] * S.ld(Lz, k0 + b);
-            }
-            const T la = S.ld(Lll, e), lu_ = S.ld(Llu, e);
-            r0 = fmax(r0, fabs(g - la + lu_));
-            const T z = S.ld(Lz, e);
-            if (la > T(0)) mu += la * (z - clb[stype(k) * LDZ + i]);
-            if (lu_ > T(0)) mu += lu_ * (cub[stype(k) * LDZ + i] - z);
-        }
-        if (k < N && i < NX) {
-            T r = cc[i] - S.ld(Lz, k0 + NZ + i);
-            for (int j = 0; j < NZ; j++) r += cab[i * LDZ + j] * S.ld(Lz, k0 + j);
-            r0 = fmax(r0, fabs(r));
-        }
-    }
-    r0 = group_max<G>(r0);
-    mu = group_sum<G>(mu) * p.inv_m;
+        r0 = group_max<G>(r0);
+        mu = group_sum<G>(mu) * p.inv_m;
 
-    const T m_bounds = T(1) / p.inv_m;
-    T theta = 1;
-    bool active = inst_ok;
-    int status = 2, iters = 0;
-    bool fail = false, pending = false;
-    T alpha = 0, smu = 0;      // step and sigma*mu of the pending (lazily applied) update
-    // exact finish (oracle/c/riccati_ipm.c "exact finish"; nmpc_ipm_lpc.hip): attempts so far,
-    // groups polishing in the current pass; status -1 = completed by the finish (step in dz)
-    int fin_att = 0;
-    bool pol = false;
+        const T m_bounds = T(1) / p.inv_m;
+        T theta = 1;
+        bool active = inst_ok;
+        int status = 2, iters = 0;
+        bool fail = false, pending = false;
+        T alpha = 0, smu = 0;      // step and sigma*mu of the pending (lazily applied) update
+        // exact finish (oracle/c/riccati_ipm.c "exact finish"; nmpc_ipm_lpc.hip): a primal-dual
+        // active-set run of <= polish_steps penalised Newton steps + one refinement. polish_at: mu that
+        // triggers the next run; pol: the group is in a run; fref: its next step is the refinement.
+        // During a run dz holds the set step, dza the active flags (-1 lower, 1 upper, 0) and sg the
+        // refinement's correction; a group the finish completes writes its outputs at once (status -1)
+        T polish_at = p.polish_mu;
+        int fin_steps = 0;
+        bool pol = false, fref = false, fs0 = false;
+        // fused closed loop after its first step: the first finish run of a solve starts from the
+        // previous step's active set shifted by one stage (act array; a warm start, the acceptance
+        // tests are unchanged)
+        const bool warm = fused && (cstep > 0 || p.cl.step > 0);
+        bool fwarm = false;
+        // the solution's active flag of an element (z on a bound to 1e-7): the warm start's input
+        auto act_flag = [&](T z, T lb, T ub) {
+            const bool onl = has_bound(lb) && z <= lb + T(1e-7) * (T(1) + fabs(lb));
+            const bool onu = has_bound(ub) && z >= ub - T(1e-7) * (T(1) + fabs(ub));
+            return onl ? T(-1) : (onu ? T(1) : T(0));
+        };
 
 #ifdef NMPC_SWEEP_TIMING
-    // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per phase
-    const bool timed = p.cycles != nullptr;
-    unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = 0;
-    auto tick = [&](int slot) {
-        if (timed) {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            if (slot >= 0) tcy[slot] += t - tmark;
-            tmark = t;
-        }
-    };
-    const unsigned long long tstart = timed ? __builtin_amdgcn_s_memtime() : 0ull;
+        // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per phase
+        const bool timed = p.cycles != nullptr;
+        unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = 0;
+        auto tick = [&](int slot) {
+            if (timed) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                if (slot >= 0) tcy[slot] += t - tmark;
+                tmark = t;
+            }
+        };
+        const unsigned long long tstart = timed ? __builtin_amdgcn_s_memtime() : 0ull;
 #endif
 
-    // ---- stage-record streaming for the B/C/D recursions: records are loaded DF stages ahead
-    // into registers and written to the LDS ring one stage before use
-    auto rec_issue = [&](T (&r)[NSF + NSC], int k, bool with_c) {
-        const unsigned kk = (unsigned)(k < 0 ? 0 : (k < N ? k : N - 1));
+        // ---- stage-record streaming for the B/C/D recursions: records are loaded DF stages ahead
+        // into registers and written to the LDS ring one stage before use
+        auto rec_issue = [&](T (&r)[NSF + NSC], int k, bool with_c) {
+            const unsigned kk = (unsigned)(k < 0 ? 0 : (k < N ? k : N - 1));
 #pragma unroll
-        for (int s_ = 0; s_ < NSF; s_++) r[s_] = S.ld(Lfrec + kk * RSF + s_ * G, ll);
-        if (with_c) {
+            for (int s_ = 0; s_ < NSF; s_++) r[s_] = S.ld(Lfrec + kk * RSF + s_ * G, ll);
+            if (with_c) {
 #pragma unroll
-            for (int s_ = 0; s_ < NSC; s_++) r[NSF + s_] = S.ld(Lcrec + kk * RSC + s_ * G, ll);
-        }
-    };
-    auto rec_put = [&](const T (&r)[NSF + NSC], int buf, bool with_c) {
-        T *dstp = rb + buf * RB1;
-#pragma unroll
-        for (int s_ = 0; s_ < NSF; s_++) dstp[s_ * G + ll] = r[s_];
-        if (with_c) {
-#pragma unroll
-            for (int s_ = 0; s_ < NSC; s_++) dstp[(NSF + s_) * G + ll] = r[NSF + s_];
-        }
-    };
-    // The ring registers r[j] hold the records m = j (mod DF); the stage loops are unrolled by DF
-    // so that every slot is a fixed register set (moving an in-flight load's destination would
-    // force a wait on it).
-
-    // ---- forward recursion shared by predictor (dst = dza) and corrector (dst = dz):
-    // dx_0 = 0 (x0 pinned), du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx; du] + re_k
-    auto forward = [&](unsigned dst) {
-        T *dxb = w + Gm::I_DX;
-        if (ll < NX) dxb[ll] = T(0);
-        T arow[NZ];   // row ll of [A B], register-resident for the whole sweep
-#pragma unroll
-        for (int j = 0; j < NZ; j++) arow[j] = cab[(ll < NX ? ll : 0) * LDZ + j];
-        T r[DF][NSF + NSC];
-#pragma unroll
-        for (int j = 0; j < DF; j++) rec_issue(r[j], j, false);
-        rec_put(r[0], 0, false);
-        rec_issue(r[0], DF, false);
-        WAVE_SYNC();
-        int cur = 0;
-        for (int kb = 0; kb < N; kb += DF)
-#pragma unroll
-        for (int j = 0; j < DF; j++) {
-            const int k = kb + j;
-            if (k >= N) break;
-            const T *rec = rb + (k & 1) * RB1;
-            const T *dxc = dxb + cur * LDX;
-            T *dxn = dxb + (1 - cur) * LDX;
-            if (ll < NU) {
-                du_l[ll] = dot2<NX>(rec[FKFF + ll], [&](int i) { return rec[FK + ll * NX + i]; },
-                                    [&](int i) { return dxc[i]; });
+                for (int s_ = 0; s_ < NSC; s_++) r[NSF + s_] = S.ld(Lcrec + kk * RSC + s_ * G, ll);
             }
-            WAVE_SYNC();
-            if (ll < NX) {
-                dxn[ll] = dot2<NZ>(rec[FRE + ll], [&](int j) { return arow[j]; },
-                                   [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
+        };
+        auto rec_put = [&](const T (&r)[NSF + NSC], int buf, bool with_c) {
+            T *dstp = rb + buf * RB1;
+#pragma unroll
+            for (int s_ = 0; s_ < NSF; s_++) dstp[s_ * G + ll] = r[s_];
+            if (with_c) {
+#pragma unroll
+                for (int s_ = 0; s_ < NSC; s_++) dstp[(NSF + s_) * G + ll] = r[NSF + s_];
             }
-            // the corrector skips groups the finish completed: their dz holds the finish step
-            if (ll < NZ && (dst != Ldz || status >= 0)) S.st(dst + k * NZ, ll, ll < NX ? dxc[ll] : du_l[ll - NX]);
-            rec_put(r[(j + 1) % DF], (k + 1) & 1, false);
-            rec_issue(r[(j + 1) % DF], k + 1 + DF, false);
-            cur = 1 - cur;
+        };
+        // The ring registers r[j] hold the records m = j (mod DF); the stage loops are unrolled by DF
+        // so that every slot is a fixed register set (moving an in-flight load's destination would
+        // force a wait on it).
+
+        // ---- forward recursion shared by predictor (dst = dza) and corrector (dst = dz):
+        // dx_0 = 0 (x0 pinned), du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx; du] + re_k
+        auto forward = [&](unsigned dst, unsigned shift = 0) {   // shift: per-lane element offset of dst
+            T *dxb = w + Gm::I_DX;
+            if (ll < NX) dxb[ll] = T(0);
+            T arow[NZ];   // row ll of [A B], register-resident for the whole sweep
+#pragma unroll
+            for (int j = 0; j < NZ; j++) arow[j] = cab[(ll < NX ? ll : 0) * LDZ + j];
+            T r[DF][NSF + NSC];
+#pragma unroll
+            for (int j = 0; j < DF; j++) rec_issue(r[j], j, false);
+            rec_put(r[0], 0, false);
+            rec_issue(r[0], DF, false);
             WAVE_SYNC();
-        }
-        if (ll < NX && (dst != Ldz || status >= 0)) S.st(dst + N * NZ, ll, dxb[cur * LDX + ll]);
-        SWEEP_FENCE();
-    };
+            int cur = 0;
+            for (int kb = 0; kb < N; kb += DF)
+#pragma unroll
+            for (int j = 0; j < DF; j++) {
+                const int k = kb + j;
+                if (k >= N) break;
+                const T *rec = rb + (k & 1) * RB1;
+                const T *dxc = dxb + cur * LDX;
+                T *dxn = dxb + (1 - cur) * LDX;
+                if (ll < NU) {
+                    du_l[ll] = dot2<NX>(rec[FKFF + ll], [&](int i) { return rec[FK + ll * NX + i]; },
+                                        [&](int i) { return dxc[i]; });
+                }
+                WAVE_SYNC();
+                if (ll < NX) {
+                    dxn[ll] = dot2<NZ>(rec[FRE + ll], [&](int j) { return arow[j]; },
+                                       [&](int j) { return j < NX ? dxc[j] : du_l[j - NX]; });
+                }
+                if (ll < NZ) S.st(dst + k * NZ, ll + shift, ll < NX ? dxc[ll] : du_l[ll - NX]);
+                rec_put(r[(j + 1) % DF], (k + 1) & 1, false);
+                rec_issue(r[(j + 1) % DF], k + 1 + DF, false);
+                cur = 1 - cur;
+                WAVE_SYNC();
+            }
+            if (ll < NX) S.st(dst + N * NZ, ll + shift, dxb[cur * LDX + ll]);
+            SWEEP_FENCE();
+        };
 
-    int it = 0;
-    bool pfail = false;
-    for (;; it++) {
-        const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
-        const bool bad = !isfinite(mu) || !isfinite(theta) || fail;
-        if (active && (conv || bad)) {
-            active = false;
-            status = conv && !bad ? 0 : 4;
-            iters = fail ? it - 1 : it;   // a failed factorisation ends the iteration it began
-        }
-        if (active && it >= p.max_iter) {
-            active = false;
-            status = 2;
-            iters = it;
-        }
-        if (!__any(active)) break;
-        NMPC_TICK(-1);
+        int it = 0;
+        bool pfail = false;
+        for (;; it++) {
+            const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
+            const bool bad = !isfinite(mu) || !isfinite(theta) || fail;
+            if (active && (conv || bad)) {
+                active = false;
+                status = conv && !bad ? 0 : 4;
+                iters = (fail ? it - 1 : it) + fin_steps;   // a failed factorisation ends the iteration it began
+            }
+            if (active && it >= p.max_iter) {
+                active = false;
+                status = 2;
+                iters = it + fin_steps;
+            }
+            if (!__any(active)) break;
+            NMPC_TICK(-1);
 
-        // E_A + A; the finish pass (finp, wave-uniform) forms the finish's penalty terms in place of
-        // the barrier for the polishing groups
-        auto factor = [&](bool finp) __attribute__((always_inline)) {
-        // ============================ E_A: lazy step, Sigma, g = H z + gc, re = [A B] z_k + c - x_{k+1}
-        // stage chunks whose z (plus one stage of overlap) fit the LDS window zw
-        for (int k0 = 0; k0 <= N; k0 += Gm::CH) {
-            const int k1 = min(k0 + Gm::CH, N + 1);       // stages owned by this chunk
-            const int kz = min(k0 + Gm::CH + 1, N + 1);   // stages whose z the chunk reads
-            for (int e = k0 * NZ + ll; e < kz * NZ; e += G) {
-                const int k = e / NZ, i = e - k * NZ;
-                T z = 0;
-                if (k < N || i < NX) {
-                    z = S.ld(Lz, e);
-                    T lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
-                    const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
-                    if (pending) {
-                        const T dz = S.ld(Ldz, e), dza = S.ld(Ldza, e);
-                        if (lam_l > T(0)) {
-                            const T t = z - lb, it_ = frcp(t), dla = -lam_l * (T(1) + dza * it_);
-                            lam_l += alpha * ((smu - lam_l * t - dla * dza - lam_l * dz) * it_);
-                        }
-                        if (lam_u > T(0)) {
-                            const T t = ub - z, it_ = frcp(t), dla = -lam_u * (T(1) - dza * it_);
-                            lam_u += alpha * ((smu - lam_u * t + dla * dza + lam_u * dz) * it_);
-                        }
-                        z += alpha * dz;
-                    }
-                    if (k < k1) {
+            // active flag of element e in a finish step: first step of a run where the multiplier
+            // exceeds the slack, later steps from dza (x_0 never)
+            auto fin_flag = [&](int k, int i, int e, T z, T lam_l, T lam_u, T lb, T ub) {
+                if (k == 0 && i < NX) return T(0);
+                if (fs0 && fwarm) {
+                    const int ks = (k < N - 1 || (k == N - 1 && i < NX)) ? k + 1 : k;
+                    const T a = S.ld(Lact, (unsigned)(ks * NZ + i));
+                    return (a < T(-0.5) && lam_l > T(0)) ? T(-1) : ((a > T(0.5) && lam_u > T(0)) ? T(1) : T(0));
+                }
+                if (!fs0) return S.ld(Ldza, e);
+                const bool al = lam_l > T(0) && lam_l > z - lb, au = !al && lam_u > T(0) && lam_u > ub - z;
+                return al ? T(-1) : (au ? T(1) : T(0));
+            };
+            // E_A + A; the finish pass (finp, wave-uniform) forms the finish's penalty terms in place of
+            // the barrier for the polishing groups
+            auto factor = [&](bool finp) __attribute__((always_inline)) {
+            // ============================ E_A: lazy step, Sigma, g = H z + gc, re = [A B] z_k + c - x_{k+1}
+            // stage chunks whose z (plus one stage of overlap) fit the LDS window zw
+            for (int k0 = 0; k0 <= N; k0 += Gm::CH) {
+                const int k1 = min(k0 + Gm::CH, N + 1);       // stages owned by this chunk
+                const int kz = min(k0 + Gm::CH + 1, N + 1);   // stages whose z the chunk reads
+                for (int e = k0 * NZ + ll; e < kz * NZ; e += G) {
+                    const int k = e / NZ, i = e - k * NZ;
+                    T z = 0;
+                    if (k < N || i < NX) {
+                        z = S.ld(Lz, e);
+                        T lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
+                        const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
                         if (pending) {
-                            S.st(Lz, e, z);
-                            S.st(Lll, e, lam_l);
-                            S.st(Llu, e, lam_u);
+                            const T dz = S.ld(Ldz, e), dza = S.ld(Ldza, e);
+                            if (lam_l > T(0)) {
+                                const T t = z - lb, it_ = frcp(t), dla = -lam_l * (T(1) + dza * it_);
+                                lam_l += alpha * ((smu - lam_l * t - dla * dza - lam_l * dz) * it_);
+                            }
+                            if (lam_u > T(0)) {
+                                const T t = ub - z, it_ = frcp(t), dla = -lam_u * (T(1) - dza * it_);
+                                lam_u += alpha * ((smu - lam_u * t + dla * dza + lam_u * dz) * it_);
+                            }
+                            z += alpha * dz;
                         }
-                        T sig = 0;
-                        if (lam_l > T(0)) sig += lam_l * frcp(z - lb);
-                        if (lam_u > T(0)) sig += lam_u * frcp(ub - z);
-                        if (finp && pol) {
-                            // active where the multiplier exceeds the slack: penalty rho, else dropped
-                            const bool al = lam_l > T(0) && lam_l > z - lb, au = !al && lam_u > T(0) && lam_u > ub - z;
-                            sig = (al || au) ? p.polish_rho : T(0);
+                        if (k < k1) {
+                            if (pending) {
+                                S.st(Lz, e, z);
+                                S.st(Lll, e, lam_l);
+                                S.st(Llu, e, lam_u);
+                            }
+                            T sig = 0;
+                            if (lam_l > T(0)) sig += lam_l * frcp(z - lb);
+                            if (lam_u > T(0)) sig += lam_u * frcp(ub - z);
+                            if (finp && pol) sig = fin_flag(k, i, e, z, lam_l, lam_u, lb, ub) != T(0) ? p.polish_rho : T(0);
+                            S.st(Lsg, e, sig);
                         }
-                        S.st(Lsg, e, sig);
+                        if (finp && pol && fref) z += S.ld(Ldz, e);   // the refinement's base z_a = z + dz
+                    }
+                    zw[e - k0 * NZ] = z;
+                }
+                WAVE_SYNC();
+                for (int e = k0 * NZ + ll; e < k1 * NZ; e += G) {
+                    const int k = e / NZ, i = e - k * NZ;
+                    const T *zk = zw + (k - k0) * NZ;
+                    T gadd = 0;
+                    if (finp && pol && (k < N || i < NX)) {
+                        // the finish's penalty gradient rho (z - bound) (refinement: 2 rho (z_a - bound))
+                        const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+                        const T a = fin_flag(k, i, e, zk[i], S.ld(Lll, e), S.ld(Llu, e), lb, ub);
+                        gadd = a != T(0) ? (fref ? T(2) : T(1)) * p.polish_rho * (zk[i] - (a < T(0) ? lb : ub)) : T(0);
+                    }
+                    if (k < N) {
+                        S.st(Lgf, e, dot2<NZ>(S.ld(Lgc, e) + gadd, [&](int b) { return ch[i * LDZ + b]; },
+                                              [&](int b) { return zk[b]; }));
+                    } else if (i < NX) {
+                        S.st(Lgf, e, dot2<NX>(S.ld(Lgc, e) + gadd, [&](int b) { return che[i * LDX + b]; },
+                                              [&](int b) { return zk[b]; }));
                     }
                 }
-                zw[e - k0 * NZ] = z;
-            }
-            WAVE_SYNC();
-            for (int e = k0 * NZ + ll; e < k1 * NZ; e += G) {
-                const int k = e / NZ, i = e - k * NZ;
-                const T *zk = zw + (k - k0) * NZ;
-                T gadd = 0;
-                if (finp && pol && (k < N || i < NX)) {   // the finish's penalty gradient rho (z - bound)
-                    const T lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), z = zk[i];
-                    const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
-                    const bool al = lam_l > T(0) && lam_l > z - lb, au = !al && lam_u > T(0) && lam_u > ub - z;
-                    gadd = (al || au) ? p.polish_rho * (z - (al ? lb : ub)) : T(0);
+                for (int e = k0 * NX + ll; e < min(k1, N) * NX; e += G) {
+                    const int k = e / NX, i = e - k * NX;
+                    const T *zk = zw + (k - k0) * NZ;
+                    S.st(Lfrec + k * RSF + FRE, i, dot2<NZ>(cc[i] - zk[NZ + i], [&](int j) { return cab[i * LDZ + j]; },
+                                                            [&](int j) { return zk[j]; }));
                 }
-                if (k < N) {
-                    S.st(Lgf, e, dot2<NZ>(S.ld(Lgc, e) + gadd, [&](int b) { return ch[i * LDZ + b]; },
-                                          [&](int b) { return zk[b]; }));
-                } else if (i < NX) {
-                    S.st(Lgf, e, dot2<NX>(S.ld(Lgc, e) + gadd, [&](int b) { return che[i * LDX + b]; },
-                                          [&](int b) { return zk[b]; }));
-                }
+                WAVE_SYNC();
             }
-            for (int e = k0 * NX + ll; e < min(k1, N) * NX; e += G) {
-                const int k = e / NX, i = e - k * NX;
-                const T *zk = zw + (k - k0) * NZ;
-                S.st(Lfrec + k * RSF + FRE, i, dot2<NZ>(cc[i] - zk[NZ + i], [&](int j) { return cab[i * LDZ + j]; },
-                                                        [&](int j) { return zk[j]; }));
-            }
-            WAVE_SYNC();
-        }
-        pending = false;
-        SWEEP_FENCE();
-        NMPC_TICK(0);
+            pending = false;
+            SWEEP_FENCE();
+            NMPC_TICK(0);
 
-        // ============================ A: backward Riccati factorisation + predictor vector
-        {
-            struct PreA {
-                T sg, g, re;
-            };
-            auto fetch_a = [&](int k, PreA &q) {
-                const unsigned kk = (unsigned)(k < 0 ? 0 : k);
-                q.sg = S.ld(Lsg + kk * NZ, ll);
-                q.g = S.ld(Lgf + kk * NZ, ll);
-                q.re = S.ld(Lfrec + (kk < (unsigned)N ? kk : N - 1) * RSF + FRE, ll);
-            };
-            // P_N = He + Sigma_N, p_N = g_N
+            // ============================ A: backward Riccati factorisation + predictor vector
             {
-                const T sgN = S.ld(Lsg + N * NZ, ll), gN = S.ld(Lgf + N * NZ, ll);
-                if (ll < NX) {
-                    sv[ll] = sgN;
-                    pv[ll] = gN;
+                struct PreA {
+                    T sg, g, re;
+                };
+                auto fetch_a = [&](int k, PreA &q) {
+                    const unsigned kk = (unsigned)(k < 0 ? 0 : k);
+                    q.sg = S.ld(Lsg + kk * NZ, ll);
+                    q.g = S.ld(Lgf + kk * NZ, ll);
+                    q.re = S.ld(Lfrec + (kk < (unsigned)N ? kk : N - 1) * RSF + FRE, ll);
+                };
+                // P_N = He + Sigma_N, p_N = g_N
+                {
+                    const T sgN = S.ld(Lsg + N * NZ, ll), gN = S.ld(Lgf + N * NZ, ll);
+                    if (ll < NX) {
+                        sv[ll] = sgN;
+                        pv[ll] = gN;
+                    }
                 }
-            }
-            PreA q{};
-            fetch_a(N - 1, q);
-            WAVE_SYNC();
-            if (gridl && col < NX) {
+                PreA q{};
+                fetch_a(N - 1, q);
+                WAVE_SYNC();
+                if (gridl && col < NX) {
 #pragma unroll
-                for (int qq = 0; qq < RM; qq++) {
-                    const int i = rg + R * qq;
-                    if (i < NX) fp[i * LDZ + col] = che[i * LDX + col] + (i == col ? sv[col] : T(0));
-                }
-            }
-            WAVE_SYNC();
-            if (ll < NX) rv[ll] = q.re;
-            if (ll < NZ) sv[ll] = q.sg;
-            WAVE_SYNC();
-            for (int k = N - 1; k >= 0; k--) {
-                PreA qn{};
-                fetch_a(k - 1, qn);
-                NMPC_PTICK(-1);
-                // 1: Pr = P re, v = Pr + p, M^T = (P [A B])^T
-                T abcol[NX];
-                load_abcol(abcol);
-                if (ll < NX) {
-                    const T s = dot2<NX>(T(0), [&](int l) { return fp[ll * LDZ + l]; }, [&](int l) { return rv[l]; });
-                    S.st(Lcrec + k * RSC + CPR, ll, s);
-                    vv[ll] = s + pv[ll];
-                }
-                if (ll < NZ) gv[ll] = q.g;
-                if (gridl) {
-_Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
                     for (int qq = 0; qq < RM; qq++) {
                         const int i = rg + R * qq;
-                        if (i < NX) {
-                            mt[col * LDX + i] = dot2<NX>(T(0), [&](int l) { return fp[i * LDZ + l]; },
-                                                         [&](int l) { return abcol[l]; });
-                        }
+                        if (i < NX) fp[i * LDZ + col] = che[i * LDX + col] + (i == col ? sv[col] : T(0));
                     }
                 }
                 WAVE_SYNC();
-                NMPC_PTICK(0);
-                // 2: F = [A B]' M + H + Sigma, lower triangle by column chunks, mirrored;
-                //    h = [A B]' v + g by the first chunk of each column
-                if (fc >= 0) {
-                    T ac[NX];
-#pragma unroll
-                    for (int l = 0; l < NX; l++) ac[l] = cab[l * LDZ + fc];
-#pragma unroll
-                    for (int t = 0; t < Gm::EF; t++) {
-                        const int bb = fb0 + t;
-                        if (t < fn) {
-                            T s_ = dot2<NX>(ch[fc * LDZ + bb], [&](int l) { return ac[l]; },
-                                            [&](int l) { return mt[bb * LDX + l]; });
-                            if (bb == fc) s_ += sv[fc];
-                            fp[fc * LDZ + bb] = s_;
-                            fp[bb * LDZ + fc] = s_;
-                        }
-                    }
-                    if (fb0 == fc) hv[fc] = dot2<NX>(gv[fc], [&](int l) { return ac[l]; }, [&](int l) { return vv[l]; });
-                }
+                if (ll < NX) rv[ll] = q.re;
+                if (ll < NZ) sv[ll] = q.sg;
                 WAVE_SYNC();
-                NMPC_PTICK(1);
-                // 3: F_uu = L L' (wave-uniform), kff = -F_uu^-1 h_u; per P column j: K(:, j) =
-                //    -F_uu^-1 F_ux(:, j), p_j = h_j + K(:, j)' h_u, P(i, j) = F(i, j) + F_xu(i, :) K(:, j)
-                T lf[NUT];
-#pragma unroll
-                for (int i = 0; i < NU; i++)
-#pragma unroll
-                    for (int j = 0; j <= i; j++) {
-                        T s_ = fp[(NX + i) * LDZ + NX + j];
-#pragma unroll
-                        for (int l = 0; l < j; l++) s_ -= lf[tri(i, l)] * lf[tri(j, l)];
-                        if (i == j) {
-                            const bool pd = s_ > T(0);
-                            if (finp) pfail |= pol & !pd;
-                            else fail |= active & !pd;
-                            lf[tri(i, i)] = frsq(pd ? s_ : T(1));
-                        } else {
-                            lf[tri(i, j)] = s_ * lf[tri(j, j)];
-                        }
+                for (int k = N - 1; k >= 0; k--) {
+                    PreA qn{};
+                    fetch_a(k - 1, qn);
+                    NMPC_PTICK(-1);
+                    // 1: Pr = P re, v = Pr + p, M^T = (P [A B])^T
+                    T abcol[NX];
+                    load_abcol(abcol);
+                    if (ll < NX) {
+                        const T s = dot2<NX>(T(0), [&](int l) { return fp[ll * LDZ + l]; }, [&](int l) { return rv[l]; });
+                        S.st(Lcrec + k * RSC + CPR, ll, s);
+                        vv[ll] = s + pv[ll];
                     }
-                T hu[NU];
-#pragma unroll
-                for (int j = 0; j < NU; j++) hu[j] = hv[NX + j];
-                {
-                    T x[NU];
-#pragma unroll
-                    for (int j = 0; j < NU; j++) x[j] = hu[j];
-                    chol_solve<T, NU>(lf, x);
-                    T mine = 0, lmine = 0;
-#pragma unroll
-                    for (int j = 0; j < NU; j++) mine = (ll == j) ? -x[j] : mine;
-#pragma unroll
-                    for (int j = 0; j < NUT; j++) lmine = (ll == j) ? lf[j] : lmine;
-                    if (ll < NU) S.st(Lfrec + k * RSF + FKFF, ll, mine);
-                    if (ll < NUT) S.st(Lcrec + k * RSC + CFI, ll, lmine);
-                }
-                if (pj >= 0) {
-                    T kc[NU];
-#pragma unroll
-                    for (int u = 0; u < NU; u++) kc[u] = fp[(NX + u) * LDZ + pj];
-                    chol_solve<T, NU>(lf, kc);
-#pragma unroll
-                    for (int u = 0; u < NU; u++) kc[u] = -kc[u];
-                    if (pi0 == pj) {
-                        T s_ = hv[pj];
-#pragma unroll
-                        for (int u = 0; u < NU; u++) {
-                            S.st(Lfrec + k * RSF + FK + u * NX, pj, kc[u]);
-                            s_ += kc[u] * hu[u];
-                        }
-                        if (k > 0) pv[pj] = s_;
-                    }
-                    if (k > 0) {
-#pragma unroll
-                        for (int t = 0; t < Gm::EP; t++) {
-                            const int i = pi0 + t;
-                            if (t < pn) {
-                                T s_ = fp[i * LDZ + pj];
-#pragma unroll
-                                for (int u = 0; u < NU; u++) s_ += fp[i * LDZ + NX + u] * kc[u];
-                                fp[i * LDZ + pj] = s_;
-                                fp[pj * LDZ + i] = s_;
+                    if (ll < NZ) gv[ll] = q.g;
+                    if (gridl) {
+    _Pragma(NMPC_STR(unroll NMPC_UNROLL_A))
+                        for (int qq = 0; qq < RM; qq++) {
+                            const int i = rg + R * qq;
+                            if (i < NX) {
+                                mt[col * LDX + i] = dot2<NX>(T(0), [&](int l) { return fp[i * LDZ + l]; },
+                                                             [&](int l) { return abcol[l]; });
                             }
                         }
                     }
+                    WAVE_SYNC();
+                    NMPC_PTICK(0);
+                    // 2: F = [A B]' M + H + Sigma, lower triangle by column chunks, mirrored;
+                    //    h = [A B]' v + g by the first chunk of each column
+                    if (fc >= 0) {
+                        T ac[NX];
+#pragma unroll
+                        for (int l = 0; l < NX; l++) ac[l] = cab[l * LDZ + fc];
+#pragma unroll
+                        for (int t = 0; t < Gm::EF; t++) {
+                            const int bb = fb0 + t;
+                            if (t < fn) {
+                                T s_ = dot2<NX>(ch[fc * LDZ + bb], [&](int l) { return ac[l]; },
+                                                [&](int l) { return mt[bb * LDX + l]; });
+                                if (bb == fc) s_ += sv[fc];
+                                fp[fc * LDZ + bb] = s_;
+                                fp[bb * LDZ + fc] = s_;
+                            }
+                        }
+                        if (fb0 == fc) hv[fc] = dot2<NX>(gv[fc], [&](int l) { return ac[l]; }, [&](int l) { return vv[l]; });
+                    }
+                    WAVE_SYNC();
+                    NMPC_PTICK(1);
+                    // 3: F_uu = L L' (wave-uniform), kff = -F_uu^-1 h_u; per P column j: K(:, j) =
+                    //    -F_uu^-1 F_ux(:, j), p_j = h_j + K(:, j)' h_u, P(i, j) = F(i, j) + F_xu(i, :) K(:, j)
+                    T lf[NUT];
+#pragma unroll
+                    for (int i = 0; i < NU; i++)
+#pragma unroll
+                        for (int j = 0; j <= i; j++) {
+                            T s_ = fp[(NX + i) * LDZ + NX + j];
+#pragma unroll
+                            for (int l = 0; l < j; l++) s_ -= lf[tri(i, l)] * lf[tri(j, l)];
+                            if (i == j) {
+                                const bool pd = s_ > T(0);
+                                if (finp) pfail |= pol & !pd;
+                                else fail |= active & !pd;
+                                lf[tri(i, i)] = frsq(pd ? s_ : T(1));
+                            } else {
+                                lf[tri(i, j)] = s_ * lf[tri(j, j)];
+                            }
+                        }
+                    T hu[NU];
+#pragma unroll
+                    for (int j = 0; j < NU; j++) hu[j] = hv[NX + j];
+                    {
+                        T x[NU];
+#pragma unroll
+                        for (int j = 0; j < NU; j++) x[j] = hu[j];
+                        chol_solve<T, NU>(lf, x);
+                        T mine = 0, lmine = 0;
+#pragma unroll
+                        for (int j = 0; j < NU; j++) mine = (ll == j) ? -x[j] : mine;
+#pragma unroll
+                        for (int j = 0; j < NUT; j++) lmine = (ll == j) ? lf[j] : lmine;
+                        if (ll < NU) S.st(Lfrec + k * RSF + FKFF, ll, mine);
+                        if (ll < NUT) S.st(Lcrec + k * RSC + CFI, ll, lmine);
+                    }
+                    if (pj >= 0) {
+                        T kc[NU];
+#pragma unroll
+                        for (int u = 0; u < NU; u++) kc[u] = fp[(NX + u) * LDZ + pj];
+                        chol_solve<T, NU>(lf, kc);
+#pragma unroll
+                        for (int u = 0; u < NU; u++) kc[u] = -kc[u];
+                        if (pi0 == pj) {
+                            T s_ = hv[pj];
+#pragma unroll
+                            for (int u = 0; u < NU; u++) {
+                                S.st(Lfrec + k * RSF + FK + u * NX, pj, kc[u]);
+                                s_ += kc[u] * hu[u];
+                            }
+                            if (k > 0) pv[pj] = s_;
+                        }
+                        if (k > 0) {
+#pragma unroll
+                            for (int t = 0; t < Gm::EP; t++) {
+                                const int i = pi0 + t;
+                                if (t < pn) {
+                                    T s_ = fp[i * LDZ + pj];
+#pragma unroll
+                                    for (int u = 0; u < NU; u++) s_ += fp[i * LDZ + NX + u] * kc[u];
+                                    fp[i * LDZ + pj] = s_;
+                                    fp[pj * LDZ + i] = s_;
+                                }
+                            }
+                        }
+                    }
+                    // next stage's re and Sigma -> LDS (their last readers ran in phases 1 and 2)
+                    if (k > 0) {
+                        if (ll < NX) rv[ll] = qn.re;
+                        if (ll < NZ) sv[ll] = qn.sg;
+                    }
+                    q = qn;
+                    WAVE_SYNC();
+                    NMPC_PTICK(3);
                 }
-                // next stage's re and Sigma -> LDS (their last readers ran in phases 1 and 2)
-                if (k > 0) {
-                    if (ll < NX) rv[ll] = qn.re;
-                    if (ll < NZ) sv[ll] = qn.sg;
-                }
-                q = qn;
-                WAVE_SYNC();
-                NMPC_PTICK(3);
             }
-        }
-        SWEEP_FENCE();
-        };
+            SWEEP_FENCE();
+            };
 
-        // ============================ exact finish (groups with mu <= polish_mu / 100^attempts):
-        // penalised factorisation, its step into dz, the oracle's acceptance tests; accepted groups
-        // are done, the others go on with this iteration
-        {
-            T thr = p.polish_mu;
-            for (int j = 0; j < fin_att; j++) thr *= T(0.01);
-            pol = active && p.polish_mu > T(0) && mu <= thr;
-        }
-        if (__any(pol)) {
-            pfail = false;
-            factor(true);
-            forward(Ldz);
-            T nbad = 0;
+            // ============================ exact finish (groups with mu <= polish_at): a primal-dual
+            // active-set run of penalised factorisations + forward sweeps (<= polish_steps set steps,
+            // then the refinement); accepted groups write their outputs and are done, the others go on
+            // with this iteration from their untouched IPM iterate
+            pol = active && p.polish_mu > T(0) && mu <= polish_at;
+            if (__any(pol)) {
+                polish_at = pol ? fmin(polish_at, mu) * T(0.01) : polish_at;
+                fref = false;
+                for (int fs = 0; fs <= p.polish_steps; fs++) {
+                    fs0 = fs == 0;
+                    fwarm = warm && fs0 && it == 0;
+                    pfail = false;
+                    factor(true);
+                    // set steps -> dz, refinement corrections -> sg (dz and the flags in dza stay)
+                    forward(Lsg, fref ? 0u : (unsigned)(Ldz - Lsg));
+                    T nbad = 0;
+                    for (int e = ll; e < nel; e += G) {
+                        const int k = e / NZ, i = e - k * NZ;
+                        if ((k == N && i >= NX) || (k == 0 && i < NX)) continue;
+                        const T lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
+                        const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+                        T z = S.ld(Lz, e);
+                        const T a = fin_flag(k, i, e, z, lam_l, lam_u, lb, ub);
+                        const T dz = fref ? S.ld(Lsg, e) : S.ld(Ldz, e);
+                        if (fref) z += S.ld(Ldz, e);
+                        const T zn = z + dz;
+                        const bool vl = lam_l > T(0), vu = lam_u > T(0);
+                        const T tl = T(1e-9) * (T(1) + fabs(lb)), tu = T(1e-9) * (T(1) + fabs(ub));
+                        const bool lo = vl && zn < lb - tl, hi = vu && zn > ub + tu;
+                        bool bad;
+                        T na = a;
+                        if (fref) {
+                            bad = fabs(dz) > T(1e-3) * (T(1) + fabs(z)) || (a < T(0) && fabs(zn - lb) > tl) ||
+                                  (a > T(0) && fabs(zn - ub) > tu) || (a == T(0) && (lo || hi));
+                        } else {
+                            const bool rl = a < T(0) && zn > fma(T(1e-15), T(1) + fabs(lb), lb);
+                            const bool ru = a > T(0) && zn < fma(T(-1e-15), T(1) + fabs(ub), ub);
+                            const bool al = a == T(0) && lo, au = a == T(0) && !lo && hi;
+                            bad = rl || ru || al || au;
+                            na = (rl || ru) ? T(0) : (al ? T(-1) : (au ? T(1) : a));
+                            if (pol) S.st(Ldza, e, na);
+                        }
+                        nbad += bad ? T(1) : T(0);
+                    }
+                    nbad = group_sum<G>(nbad);
+                    bool done = false;
+                    if (pol) {
+                        fin_steps++;
+                        const bool okp = nbad == T(0) && !pfail;
+                        if (fref) {
+                            done = okp;
+                            pol = false;
+                        } else if (okp) {
+                            fref = true;
+                        } else if (pfail || fs + 1 >= p.polish_steps) {
+                            pol = false;
+                        }
+                    }
+                    if (done) {   // outputs: z + set step + refinement, clamped onto the bounds
+                        active = false;
+                        status = -1;
+                        iters = it + fin_steps;
+                        if (inst_ok) {
+                            for (int e = ll; e < nel; e += G) {
+                                const int k = e / NZ, i = e - k * NZ;
+                                if (k == N && i >= NX) continue;
+                                const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
+                                T z = S.ld(Lz, e);
+                                if (!(k == 0 && i < NX)) z += S.ld(Ldz, e) + S.ld(Lsg, e);
+                                z = has_bound(lb) ? fmax(z, lb) : z;
+                                z = has_bound(ub) ? fmin(z, ub) : z;
+                                if (i < NX) p.xout[((size_t)inst * (N + 1) + k) * NX + i] = z;
+                                else p.uout[((size_t)inst * N + k) * NU + (i - NX)] = z;
+                                if (fused) S.st(Lact, e, act_flag(z, lb, ub));
+                            }
+                        }
+                    }
+                    SWEEP_FENCE();
+                    if (!__any(pol)) break;
+                }
+                pol = fref = false;
+                fwarm = false;
+                if (!__any(active)) break;
+            }
+            factor(false);
+            NMPC_TICK(1);
+
+            // ============================ B: forward predictor; E_B: ratio test + centring sums
+            forward(Ldza);
+            NMPC_TICK(2);
+            T a_aff = 1, S0 = 0, S2 = 0;
             for (int e = ll; e < nel; e += G) {
                 const int k = e / NZ, i = e - k * NZ;
                 if (k == N && i >= NX) continue;
-                const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), zn = z + S.ld(Ldz, e);
-                const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
-                const T sl = T(1) + fabs(lb), su = T(1) + fabs(ub);
-                const bool vl = lam_l > T(0), vu = lam_u > T(0);
-                const bool al = vl && lam_l > z - lb, au = !al && vu && lam_u > ub - z;
-                const bool bad = al ? zn > fma(T(1e-15), sl, lb)
-                                    : (au ? zn < fma(T(-1e-15), su, ub)
-                                          : ((vl && zn < fma(T(-1e-9), sl, lb)) || (vu && zn > fma(T(1e-9), su, ub))));
-                nbad += bad ? T(1) : T(0);
-            }
-            nbad = group_sum<G>(nbad);
-            if (pol) {
-                fin_att++;
-                if (nbad == T(0) && !pfail) {
-                    active = false;
-                    status = -1;
-                    iters = it + 1;
+                const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), dz = S.ld(Ldza, e);
+                if (lam_l > T(0)) {
+                    const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t);
+                    const T dl = -lam_l * (T(1) + dz * it_);
+                    if (dz < T(0)) a_aff = fmin(a_aff, -t * frcp(dz));
+                    if (dl < T(0)) a_aff = fmin(a_aff, -lam_l * frcp(dl));
+                    S0 += lam_l * t;
+                    S2 += lam_l * dz * (t + dz) * it_;
+                }
+                if (lam_u > T(0)) {
+                    const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t);
+                    const T dl = -lam_u * (T(1) - dz * it_);
+                    if (dz > T(0)) a_aff = fmin(a_aff, t * frcp(dz));
+                    if (dl < T(0)) a_aff = fmin(a_aff, -lam_u * frcp(dl));
+                    S0 += lam_u * t;
+                    S2 += lam_u * dz * (dz - t) * it_;
                 }
             }
-            pol = false;
-            if (!__any(active)) break;
-        }
-        factor(false);
-        NMPC_TICK(1);
+            a_aff = group_min<G>(a_aff);
+            S0 = group_sum<G>(S0);
+            S2 = group_sum<G>(S2);
+            // mu_aff = [(1 - a) S0 - a^2 S2'] / m  with S2' = sum lam dz (t + dz) / t (closed form)
+            const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
+            const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
+            smu = sgm * sgm * sgm * mu;
+            NMPC_TICK(3);
 
-        // ============================ B: forward predictor; E_B: ratio test + centring sums
-        forward(Ldza);
-        NMPC_TICK(2);
-        T a_aff = 1, S0 = 0, S2 = 0;
-        for (int e = ll; e < nel; e += G) {
-            const int k = e / NZ, i = e - k * NZ;
-            if (k == N && i >= NX) continue;
-            const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), dz = S.ld(Ldza, e);
-            if (lam_l > T(0)) {
-                const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t);
-                const T dl = -lam_l * (T(1) + dz * it_);
-                if (dz < T(0)) a_aff = fmin(a_aff, -t * frcp(dz));
-                if (dl < T(0)) a_aff = fmin(a_aff, -lam_l * frcp(dl));
-                S0 += lam_l * t;
-                S2 += lam_l * dz * (t + dz) * it_;
+            // ============================ E_C: corrector rhs g^ = g + (dlam_a dz_a -/+ sigma mu) / t
+            for (int e = ll; e < nel; e += G) {
+                const int k = e / NZ, i = e - k * NZ;
+                if (k == N && i >= NX) continue;
+                const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), dza = S.ld(Ldza, e);
+                T g = S.ld(Lgf, e);
+                if (lam_l > T(0)) {
+                    const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t), dl = -lam_l * (T(1) + dza * it_);
+                    g += (dl * dza - smu) * it_;
+                }
+                if (lam_u > T(0)) {
+                    const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t), dl = -lam_u * (T(1) - dza * it_);
+                    g += (dl * dza + smu) * it_;
+                }
+                if (k < N) S.st(Lcrec + k * RSC + CGH, i, g);
+                else S.st(Lgf, e, g);
             }
-            if (lam_u > T(0)) {
-                const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t);
-                const T dl = -lam_u * (T(1) - dz * it_);
-                if (dz > T(0)) a_aff = fmin(a_aff, t * frcp(dz));
-                if (dl < T(0)) a_aff = fmin(a_aff, -lam_u * frcp(dl));
-                S0 += lam_u * t;
-                S2 += lam_u * dz * (dz - t) * it_;
-            }
-        }
-        a_aff = group_min<G>(a_aff);
-        S0 = group_sum<G>(S0);
-        S2 = group_sum<G>(S2);
-        // mu_aff = [(1 - a) S0 - a^2 S2'] / m  with S2' = sum lam dz (t + dz) / t (closed form)
-        const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
-        const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
-        smu = sgm * sgm * sgm * mu;
-        NMPC_TICK(3);
+            SWEEP_FENCE();
+            NMPC_TICK(4);
 
-        // ============================ E_C: corrector rhs g^ = g + (dlam_a dz_a -/+ sigma mu) / t
-        for (int e = ll; e < nel; e += G) {
-            const int k = e / NZ, i = e - k * NZ;
-            if (k == N && i >= NX) continue;
-            const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e), dza = S.ld(Ldza, e);
-            T g = S.ld(Lgf, e);
-            if (lam_l > T(0)) {
-                const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t), dl = -lam_l * (T(1) + dza * it_);
-                g += (dl * dza - smu) * it_;
-            }
-            if (lam_u > T(0)) {
-                const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t), dl = -lam_u * (T(1) - dza * it_);
-                g += (dl * dza + smu) * it_;
-            }
-            if (k < N) S.st(Lcrec + k * RSC + CGH, i, g);
-            else S.st(Lgf, e, g);
-        }
-        SWEEP_FENCE();
-        NMPC_TICK(4);
-
-        // ============================ C: backward corrector vector (kff, p)
-        {
+            // ============================ C: backward corrector vector (kff, p)
             {
-                const T gN = S.ld(Lgf + N * NZ, ll);
-                if (ll < NX) pv[ll] = gN;
-            }
-            T abcol[NX];   // column ll of [A B], register-resident for the whole sweep
-            load_abcol(abcol);
-            T r[DF][NSF + NSC];
-#pragma unroll
-            for (int j = 0; j < DF; j++) rec_issue(r[j], N - 1 - j, true);
-            rec_put(r[0], 0, true);
-            rec_issue(r[0], N - 1 - DF, true);
-            WAVE_SYNC();
-            for (int kb = N - 1; kb >= 0; kb -= DF)
-#pragma unroll
-            for (int j = 0; j < DF; j++) {
-                const int k = kb - j;
-                if (k < 0) break;
-                const T *fr = rb + ((N - 1 - k) & 1) * RB1, *cr = fr + NSF * G;
-                if (ll < NX) vv[ll] = cr[CPR + ll] + pv[ll];
-                WAVE_SYNC();
-                if (ll < NZ) hv[ll] = dot2<NX>(cr[CGH + ll], [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
-                WAVE_SYNC();
-                T lf[NUT], hu[NU], x[NU];
-#pragma unroll
-                for (int j = 0; j < NUT; j++) lf[j] = cr[CFI + j];
-#pragma unroll
-                for (int j = 0; j < NU; j++) x[j] = hu[j] = hv[NX + j];
-                chol_solve<T, NU>(lf, x);
-                T mine = 0;
-#pragma unroll
-                for (int j = 0; j < NU; j++) mine = (ll == j) ? -x[j] : mine;
-                if (ll < NU) S.st(Lfrec + k * RSF + FKFF, ll, mine);
-                if (k > 0 && ll < NX) {
-                    T s_ = hv[ll];
-#pragma unroll
-                    for (int u = 0; u < NU; u++) s_ += fr[FK + u * NX + ll] * hu[u];
-                    pv[ll] = s_;
+                {
+                    const T gN = S.ld(Lgf + N * NZ, ll);
+                    if (ll < NX) pv[ll] = gN;
                 }
-                rec_put(r[(j + 1) % DF], (N - k) & 1, true);
-                rec_issue(r[(j + 1) % DF], k - 1 - DF, true);
+                T abcol[NX];   // column ll of [A B], register-resident for the whole sweep
+                load_abcol(abcol);
+                T r[DF][NSF + NSC];
+#pragma unroll
+                for (int j = 0; j < DF; j++) rec_issue(r[j], N - 1 - j, true);
+                rec_put(r[0], 0, true);
+                rec_issue(r[0], N - 1 - DF, true);
                 WAVE_SYNC();
+                for (int kb = N - 1; kb >= 0; kb -= DF)
+#pragma unroll
+                for (int j = 0; j < DF; j++) {
+                    const int k = kb - j;
+                    if (k < 0) break;
+                    const T *fr = rb + ((N - 1 - k) & 1) * RB1, *cr = fr + NSF * G;
+                    if (ll < NX) vv[ll] = cr[CPR + ll] + pv[ll];
+                    WAVE_SYNC();
+                    if (ll < NZ) hv[ll] = dot2<NX>(cr[CGH + ll], [&](int l) { return abcol[l]; }, [&](int l) { return vv[l]; });
+                    WAVE_SYNC();
+                    T lf[NUT], hu[NU], x[NU];
+#pragma unroll
+                    for (int j = 0; j < NUT; j++) lf[j] = cr[CFI + j];
+#pragma unroll
+                    for (int j = 0; j < NU; j++) x[j] = hu[j] = hv[NX + j];
+                    chol_solve<T, NU>(lf, x);
+                    T mine = 0;
+#pragma unroll
+                    for (int j = 0; j < NU; j++) mine = (ll == j) ? -x[j] : mine;
+                    if (ll < NU) S.st(Lfrec + k * RSF + FKFF, ll, mine);
+                    if (k > 0 && ll < NX) {
+                        T s_ = hv[ll];
+#pragma unroll
+                        for (int u = 0; u < NU; u++) s_ += fr[FK + u * NX + ll] * hu[u];
+                        pv[ll] = s_;
+                    }
+                    rec_put(r[(j + 1) % DF], (N - k) & 1, true);
+                    rec_issue(r[(j + 1) % DF], k - 1 - DF, true);
+                    WAVE_SYNC();
+                }
             }
-        }
-        SWEEP_FENCE();
-        NMPC_TICK(5);
+            SWEEP_FENCE();
+            NMPC_TICK(5);
 
-        // ============================ D: forward corrector; E_D: step length + new mu
-        forward(Ldz);
-        NMPC_TICK(6);
-        T amax = 1, T0 = 0, C1 = 0, C2 = 0;
-        for (int e = ll; e < nel; e += G) {
-            const int k = e / NZ, i = e - k * NZ;
-            if (k == N && i >= NX) continue;
-            const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
-            const T dz = S.ld(Ldz, e), dza = S.ld(Ldza, e);
-            if (lam_l > T(0)) {
-                const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t);
-                const T dla = -lam_l * (T(1) + dza * it_);
-                const T dl = (smu - lam_l * t - dla * dza - lam_l * dz) * it_;
-                if (dz < T(0)) amax = fmin(amax, -t * frcp(dz));
-                if (dl < T(0)) amax = fmin(amax, -lam_l * frcp(dl));
-                T0 += lam_l * t;
-                C1 += dla * dza;
-                C2 += dl * dz;
+            // ============================ D: forward corrector; E_D: step length + new mu
+            forward(Ldz);
+            NMPC_TICK(6);
+            T amax = 1, T0 = 0, C1 = 0, C2 = 0;
+            for (int e = ll; e < nel; e += G) {
+                const int k = e / NZ, i = e - k * NZ;
+                if (k == N && i >= NX) continue;
+                const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
+                const T dz = S.ld(Ldz, e), dza = S.ld(Ldza, e);
+                if (lam_l > T(0)) {
+                    const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t);
+                    const T dla = -lam_l * (T(1) + dza * it_);
+                    const T dl = (smu - lam_l * t - dla * dza - lam_l * dz) * it_;
+                    if (dz < T(0)) amax = fmin(amax, -t * frcp(dz));
+                    if (dl < T(0)) amax = fmin(amax, -lam_l * frcp(dl));
+                    T0 += lam_l * t;
+                    C1 += dla * dza;
+                    C2 += dl * dz;
+                }
+                if (lam_u > T(0)) {
+                    const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t);
+                    const T dla = -lam_u * (T(1) - dza * it_);
+                    const T dl = (smu - lam_u * t + dla * dza + lam_u * dz) * it_;
+                    if (dz > T(0)) amax = fmin(amax, t * frcp(dz));
+                    if (dl < T(0)) amax = fmin(amax, -lam_u * frcp(dl));
+                    T0 += lam_u * t;
+                    C1 += -dla * dza;
+                    C2 += -dl * dz;
+                }
             }
-            if (lam_u > T(0)) {
-                const T t = cub[stype(k) * LDZ + i] - z, it_ = frcp(t);
-                const T dla = -lam_u * (T(1) - dza * it_);
-                const T dl = (smu - lam_u * t + dla * dza + lam_u * dz) * it_;
-                if (dz > T(0)) amax = fmin(amax, t * frcp(dz));
-                if (dl < T(0)) amax = fmin(amax, -lam_u * frcp(dl));
-                T0 += lam_u * t;
-                C1 += -dla * dza;
-                C2 += -dl * dz;
+            amax = group_min<G>(amax);
+            T0 = group_sum<G>(T0);
+            C1 = group_sum<G>(C1);
+            C2 = group_sum<G>(C2);
+            const T a = fmin(T(1), T(0.995) * amax);
+            // a failed factorisation (F_uu not positive definite) leaves the iterate as it stood at the
+            // start of this iteration, like the oracle's early exit (oracle/c/riccati_ipm.c:222)
+            if (active && !fail) {
+                // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
+                mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
+                theta *= (T(1) - a);
+                alpha = a;
+                pending = true;
             }
+            NMPC_TICK(7);
         }
-        amax = group_min<G>(amax);
-        T0 = group_sum<G>(T0);
-        C1 = group_sum<G>(C1);
-        C2 = group_sum<G>(C2);
-        const T a = fmin(T(1), T(0.995) * amax);
-        // a failed factorisation (F_uu not positive definite) leaves the iterate as it stood at the
-        // start of this iteration, like the oracle's early exit (oracle/c/riccati_ipm.c:222)
-        if (active && !fail) {
-            // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
-            mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
-            theta *= (T(1) - a);
-            alpha = a;
-            pending = true;
-        }
-        NMPC_TICK(7);
-    }
 
-    // ------------------------------------------------------------------ apply pending step, outputs
-    if (!inst_ok) return;
-    T *xo = p.xout + (size_t)inst * (N + 1) * NX;
-    T *uo = p.uout + (size_t)inst * N * NU;
-    for (int e = ll; e < nel; e += G) {
-        const int k = e / NZ, i = e % NZ;
-        if (k == N && i >= NX) continue;
-        T z = S.ld(Lz, e);
-        if (pending) z += alpha * S.ld(Ldz, e);
-        if (status < 0) {   // completed by the finish: its step, clamped onto the active bounds
-            const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
-            z += S.ld(Ldz, e);
-            z = has_bound(lb) ? fmax(z, lb) : z;
-            z = has_bound(ub) ? fmin(z, ub) : z;
-        }
-        if (i < NX) xo[k * NX + i] = z;
-        else uo[k * NU + (i - NX)] = z;
-    }
-    if (ll == 0) {
-        p.status[inst] = status < 0 ? 0 : status;
-        p.iters[inst] = iters;
+        // ------------------------------------------------------------------ apply pending step, outputs
+        if (inst_ok) {
+            T *xo = p.xout + (size_t)inst * (N + 1) * NX;
+            T *uo = p.uout + (size_t)inst * N * NU;
+            for (int e = ll; e < nel; e += G) {
+                const int k = e / NZ, i = e % NZ;
+                if (k == N && i >= NX) continue;
+                if (status < 0) break;   // completed by the finish, outputs already written
+                T z = S.ld(Lz, e);
+                if (pending) z += alpha * S.ld(Ldz, e);
+                if (i < NX) xo[k * NX + i] = z;
+                else uo[k * NU + (i - NX)] = z;
+                if (fused) S.st(Lact, e, act_flag(z, clb[stype(k) * LDZ + i], cub[stype(k) * LDZ + i]));
+            }
+            if (ll == 0) {
+                p.status[inst] = status < 0 ? 0 : status;
+                p.iters[inst] = iters;
 #ifdef NMPC_SWEEP_TIMING
-        if (timed) {
-            unsigned long long *c = p.cycles + (size_t)inst * 9;
-            for (int j = 0; j < 8; j++) c[j] = tcy[j];
-            c[8] = __builtin_amdgcn_s_memtime() - tstart;
-        }
+                if (timed) {
+                    unsigned long long *c = p.cycles + (size_t)inst * 9;
+                    for (int j = 0; j < 8; j++) c[j] = tcy[j];
+                    c[8] = __builtin_amdgcn_s_memtime() - tstart;
+                }
 #endif
+            }
+        }
+        if (fused) {
+            // closed-loop advance of this step by the instance's lanes (nmpc_cl_device.h), after the
+            // outputs written above by this wavefront; the next step reads the new state
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (inst_ok)
+                cl_advance_group<T, NX, NU>(p.cl, inst, p.cl.step + cstep, status < 0 ? 0 : status, ll,
+                                            p.cl_noise[(size_t)inst * nsteps + cstep]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
     }
 }
 

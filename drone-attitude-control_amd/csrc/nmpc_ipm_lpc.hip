@@ -31,6 +31,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "nmpc_cl_device.h"
 #include "nmpc_internal.h"
 #include "nmpc_lpc_geom.h"
 
@@ -372,897 +373,1023 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     auto ldU = [&](int k, int w) { return S.ld(off(k, L::REC + w), lo); };
     auto stU = [&](int k, int w, T v) { S.st(off(k, L::REC + w), lo, v); };
 
-    const T *yref = p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
-    const T *x0 = p.x0 + (size_t)inst * NX;
     auto gmin = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return fmin(a, b); }); };
     auto gmax = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return fmax(a, b); }); };
     auto gsum = [&](T v) { return gred<NZ>(v, lane, r, [](T a, T b) { return a + b; }); };
 
     const int row_base = (xl ? r : 0) * RN, col_base = NX * RN + r * CN;
 
-    // ------------------------------------------------------------------ initial point
-    T r0 = 0, mu = 0, abz = 0;
-    for (int k = 0; k <= N; k++) {
-        const bool ex = k < N || xl;
-        const T *yk = yref + (size_t)k * p.ny;
-        T z = 0, lam_l = 0, lam_u = 0, gc = 0;
-        const T lb = LB(k), ub = UB(k);
-        if (ex) {
-            if (k < N) {
-                for (int j = 0; j < p.ny; j++) gc += p.G[r * p.ny + j] * yk[j];
-            } else {
-                for (int j = 0; j < p.ny_e; j++) gc += p.Ge[r * p.ny_e + j] * yk[j];
-            }
-            if (k == 0 && xl) {
-                z = x0[r];
-            } else {
-                z = p.yref_is_z ? yk[r] : T(0);
-                const bool hl = has_bound(lb), hu = has_bound(ub);
-                if (hl && hu) {
-                    const T d = T(0.01) * (ub - lb);
-                    z = ul ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
-                    z = fmin(fmax(z, lb + d), ub - d);
-                } else if (hl) {
-                    z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
-                } else if (hu) {
-                    z = fmin(z, ub - T(0.01) * fmax(fabs(ub), T(1)));
+    // one solve per closed-loop step; plain solves run one step (p.cl_steps = 0)
+    const bool fused = p.cl_steps > 0;
+    const int nsteps = fused ? p.cl_steps : 1;
+#ifdef XLICM
+#pragma clang loop licm(disable)
+#endif
+    for (int cstep = 0; cstep < nsteps; cstep++) {
+        // fused closed loop: the yref window straight from the reference table rows (offset + step) %
+        // period (cl_prepare_kernel's gather), x0 from the closed-loop state
+        const int t_ref = fused ? (p.cl.offset[inst] + p.cl.step + cstep) % p.cl.period : 0;
+        const T *yref = fused ? p.cl.table + (size_t)t_ref * p.cl.table_cols
+                              : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
+        const int yrow = fused ? p.cl.table_cols : p.ny;
+        const T *x0 = (fused ? p.cl.state : p.x0) + (size_t)inst * NX;
+        // ------------------------------------------------------------------ initial point
+        T r0 = 0, mu = 0, abz = 0;
+        for (int k = 0; k <= N; k++) {
+            const bool ex = k < N || xl;
+            const T *yk = yref + (size_t)k * yrow;
+            T z = 0, lam_l = 0, lam_u = 0, gc = 0;
+            const T lb = LB(k), ub = UB(k);
+            if (ex) {
+                if (k < N) {
+                    for (int j = 0; j < p.ny; j++) gc += p.G[r * p.ny + j] * yk[j];
+                } else {
+                    for (int j = 0; j < p.ny_e; j++) gc += p.Ge[r * p.ny_e + j] * yk[j];
                 }
-                if (hl) lam_l = p.mu0 / (z - lb);
-                if (hu) lam_u = p.mu0 / (ub - z);
+                if (k == 0 && xl) {
+                    z = x0[r];
+                } else {
+                    z = p.yref_is_z ? yk[r] : T(0);
+                    const bool hl = has_bound(lb), hu = has_bound(ub);
+                    if (hl && hu) {
+                        const T d = T(0.01) * (ub - lb);
+                        z = ul ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
+                        z = fmin(fmax(z, lb + d), ub - d);
+                    } else if (hl) {
+                        z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
+                    } else if (hu) {
+                        z = fmin(z, ub - T(0.01) * fmax(fabs(ub), T(1)));
+                    }
+                    if (hl) lam_l = p.mu0 / (z - lb);
+                    if (hu) lam_u = p.mu0 / (ub - z);
+                }
             }
-        }
-        stE(L::Z, k, z);
-        stE(L::LL, k, lam_l);
-        stE(L::LU, k, lam_u);
-        stE(L::GC, k, gc);
-        zb[r] = z;
-        LPC_SYNC();
-        if (ex) {
-            T g = gc;
-            if (k < N) {
+            stE(L::Z, k, z);
+            stE(L::LL, k, lam_l);
+            stE(L::LU, k, lam_u);
+            stE(L::GC, k, gc);
+            zb[r] = z;
+            LPC_SYNC();
+            if (ex) {
+                T g = gc;
+                if (k < N) {
 #pragma unroll
-                for (int b = 0; b < NZ; b++) g = fma(hm[r * LDZ + b], zb[b], g);
+                    for (int b = 0; b < NZ; b++) g = fma(hm[r * LDZ + b], zb[b], g);
+                } else {
+#pragma unroll
+                    for (int b = 0; b < NX; b++) g = fma(hem[r * LDX + b], zb[b], g);
+                }
+                if (!(k == 0 && xl)) {
+                    r0 = fmax(r0, fabs(g - lam_l + lam_u));
+                    if (lam_l > T(0)) mu += lam_l * (z - lb);
+                    if (lam_u > T(0)) mu += lam_u * (ub - z);
+                }
+                if (xl && k > 0) r0 = fmax(r0, fabs(abz - z));
+                if (xl && k < N) {
+                    T s = c_r;
+#pragma unroll
+                    for (int j = 0; j < NZ; j++) s = fma(abr[r * LDZ + j], zb[j], s);
+                    abz = s;
+                }
+            }
+            LPC_SYNC();
+        }
+        r0 = gmax(r0);
+        mu = gsum(mu) * p.inv_m;
+
+        const T m_bounds = T(1) / p.inv_m;
+        T theta = 1;
+        bool active = inst_ok;
+        int status = 2, iters = 0;
+        bool fail = false, pending = false;
+        T alpha = 0, smu = 0;
+        // exact finish (oracle/c/riccati_ipm.c "exact finish"): a primal-dual active-set run of at
+        // most polish_steps penalised Newton steps from the IPM iterate, then one refinement step.
+        // polish_at: mu that triggers the next run; pol: the group is in a run; fref: its next step
+        // is the refinement; fin_steps: finish steps taken (counted in qp_iter). During a run DZ holds
+        // the step and DZA the active flags (-1 lower, 1 upper, 0); after the refinement DZA holds
+        // its correction. status -1: completed by the finish, outputs = Z + DZ + DZA (B and D skip
+        // the group's DZA / DZ)
+        T polish_at = p.polish_mu;
+        int fin_steps = 0;
+        bool pol = false, fref = false;
+        bool fs0 = false;   // wave-uniform: the current finish pass is the first step of its runs
+    // fused closed loop after its first step: the first finish run of a solve starts from the
+    // previous step's active set shifted by one stage (ACT word; warm start, the acceptance tests
+    // are unchanged), read into the dza slots, which the first iteration does not use otherwise
+    const bool warm = fused && (cstep > 0 || p.cl.step > 0);
+    bool fwarm = false;   // wave-uniform: the current finish pass reads the warm flags
+
+        // elementwise state of element (k, r) fetched one stage ahead in the sweeps
+        struct El {
+            T z, ll, lu, dz, dza, g;
+        };
+        // lazily apply the pending step of the previous iteration to element (k, r)
+        // lazily apply the pending step of the previous iteration to element (k, r); the arithmetic
+        // is branch-free (selects), the write-back a write-only divergent block
+        // the bounds of element (k, r) are read once per stage, ahead of their use (B)
+        struct Bd {
+            T lb, ub;
+        };
+        auto bnd = [&](int k) { return Bd{LB(k), UB(k)}; };
+        auto lazy = [&](int k, El &q, const Bd &b) {
+            const bool upd = pending && (k < N || xl);
+            const T lb = b.lb, ub = b.ub;
+            const bool vl = q.ll > T(0), vu = q.lu > T(0);
+            const T tl = q.z - lb, tu = ub - q.z, itl = frcp(tl), itu = frcp(tu);
+            const T dlal = -q.ll * (T(1) + q.dza * itl), dlau = -q.lu * (T(1) - q.dza * itu);
+            const T nl = q.ll + alpha * ((smu - q.ll * tl - dlal * q.dza - q.ll * q.dz) * itl);
+            const T nu_ = q.lu + alpha * ((smu - q.lu * tu + dlau * q.dza + q.lu * q.dz) * itu);
+            q.ll = (upd && vl) ? nl : q.ll;
+            q.lu = (upd && vu) ? nu_ : q.lu;
+            q.z = upd ? q.z + alpha * q.dz : q.z;
+            if (upd) {
+                stE(L::Z, k, q.z);
+                stE(L::LL, k, q.ll);
+                stE(L::LU, k, q.lu);
+            }
+        };
+        auto sigma = [&](const El &q, const Bd &b) {
+            const T sl = q.ll * frcp(q.z - b.lb), su = q.lu * frcp(b.ub - q.z);
+            return (q.ll > T(0) ? sl : T(0)) + (q.lu > T(0) ? su : T(0));
+        };
+        // exact finish, first active set: a bound is active where its multiplier exceeds its slack
+        auto finish_rule = [&](const El &q, const Bd &b) {
+            const bool al = q.ll > T(0) && q.ll > q.z - b.lb;
+            const bool au = !al && q.lu > T(0) && q.lu > b.ub - q.z;
+            return al ? T(-1) : (au ? T(1) : T(0));
+        };
+        // finish terms of element (k, r): active bounds held by the penalty rho (Hessian rho,
+        // gradient rho (z - bound); the refinement: 2 rho (z_a - bound) at z_a = z + dz), the others
+        // dropped. fs0: first step of the run (active set from the multipliers, else from DZA).
+        // Branch-free; q.z becomes the step's base point.
+        // active flag of a finish step from the dza slot (flags of the run, or the warm-start flags,
+        // kept to bounds the element has), or from the multipliers at the first step of a cold run
+        auto fin_flag = [&](const El &q, const Bd &b, bool first) {
+            if (first && !fwarm) return finish_rule(q, b);
+            return (q.dza < T(-0.5) && q.ll > T(0)) ? T(-1) : ((q.dza > T(0.5) && q.lu > T(0)) ? T(1) : T(0));
+        };
+        auto finish_terms = [&](El &q, const Bd &b, bool fs0, T &sg, T &gadd) {
+            const T a = fin_flag(q, b, fs0);
+            q.z = fref ? q.z + q.dz : q.z;
+            const T rho = p.polish_rho;
+            sg = a != T(0) ? rho : T(0);
+            gadd = a != T(0) ? (fref ? T(2) : T(1)) * rho * (q.z - (a < T(0) ? b.lb : b.ub)) : T(0);
+        };
+        // acceptance tests of a finish step at element (k, r) (the oracle's POLISH_TOL_*): q.z is the
+        // step's base, dz the step, a the active flag it used. A set step: active bounds keep a
+        // non-negative multiplier rho (bound - z_new) (to a few ulps), inactive ones hold (to 1e-9);
+        // the next active set (na) drops the first and adds the second kind of violation. The
+        // refinement: the correction stays below 1e-3 (1 + |z|) and the refined point sits on its
+        // active bounds and inside the others to 1e-9. Returns 1 for a violated test.
+        auto finish_check = [&](T dz, const El &q, const Bd &b, T a, T &na) {
+            const bool vl = q.ll > T(0), vu = q.lu > T(0);
+            const T zn = q.z + dz;
+            const T tl = T(1e-9) * (T(1) + fabs(b.lb)), tu = T(1e-9) * (T(1) + fabs(b.ub));
+            const bool lo = vl && zn < b.lb - tl, hi = vu && zn > b.ub + tu;
+            bool bad;
+            if (fref) {
+                bad = fabs(dz) > T(1e-3) * (T(1) + fabs(q.z)) || (a < T(0) && fabs(zn - b.lb) > tl) ||
+                      (a > T(0) && fabs(zn - b.ub) > tu) || (a == T(0) && (lo || hi));
+                na = a;
             } else {
-#pragma unroll
-                for (int b = 0; b < NX; b++) g = fma(hem[r * LDX + b], zb[b], g);
+                const bool rl = a < T(0) && zn > fma(T(1e-15), T(1) + fabs(b.lb), b.lb);
+                const bool ru = a > T(0) && zn < fma(T(-1e-15), T(1) + fabs(b.ub), b.ub);
+                const bool al = a == T(0) && lo, au = a == T(0) && !lo && hi;
+                bad = rl || ru || al || au;
+                na = (rl || ru) ? T(0) : (al ? T(-1) : (au ? T(1) : a));
             }
-            if (!(k == 0 && xl)) {
-                r0 = fmax(r0, fabs(g - lam_l + lam_u));
-                if (lam_l > T(0)) mu += lam_l * (z - lb);
-                if (lam_u > T(0)) mu += lam_u * (ub - z);
-            }
-            if (xl && k > 0) r0 = fmax(r0, fabs(abz - z));
-            if (xl && k < N) {
-                T s = c_r;
-#pragma unroll
-                for (int j = 0; j < NZ; j++) s = fma(abr[r * LDZ + j], zb[j], s);
-                abz = s;
-            }
-        }
-        LPC_SYNC();
-    }
-    r0 = gmax(r0);
-    mu = gsum(mu) * p.inv_m;
-
-    const T m_bounds = T(1) / p.inv_m;
-    T theta = 1;
-    bool active = inst_ok;
-    int status = 2, iters = 0;
-    bool fail = false, pending = false;
-    T alpha = 0, smu = 0;
-    // exact finish (oracle/c/riccati_ipm.c "exact finish"): attempts so far (the next one waits
-    // for mu <= polish_mu / 100^attempts); pol marks the groups polishing in the current pass.
-    // status -1: completed by the finish, whose step DZ is kept (the corrector skips the group)
-    int fin_att = 0;
-    bool pol = false;
-
-    // elementwise state of element (k, r) fetched one stage ahead in the sweeps
-    struct El {
-        T z, ll, lu, dz, dza, g;
-    };
-    // lazily apply the pending step of the previous iteration to element (k, r)
-    // lazily apply the pending step of the previous iteration to element (k, r); the arithmetic
-    // is branch-free (selects), the write-back a write-only divergent block
-    // the bounds of element (k, r) are read once per stage, ahead of their use (B)
-    struct Bd {
-        T lb, ub;
-    };
-    auto bnd = [&](int k) { return Bd{LB(k), UB(k)}; };
-    auto lazy = [&](int k, El &q, const Bd &b) {
-        const bool upd = pending && (k < N || xl);
-        const T lb = b.lb, ub = b.ub;
-        const bool vl = q.ll > T(0), vu = q.lu > T(0);
-        const T tl = q.z - lb, tu = ub - q.z, itl = frcp(tl), itu = frcp(tu);
-        const T dlal = -q.ll * (T(1) + q.dza * itl), dlau = -q.lu * (T(1) - q.dza * itu);
-        const T nl = q.ll + alpha * ((smu - q.ll * tl - dlal * q.dza - q.ll * q.dz) * itl);
-        const T nu_ = q.lu + alpha * ((smu - q.lu * tu + dlau * q.dza + q.lu * q.dz) * itu);
-        q.ll = (upd && vl) ? nl : q.ll;
-        q.lu = (upd && vu) ? nu_ : q.lu;
-        q.z = upd ? q.z + alpha * q.dz : q.z;
-        if (upd) {
+            return bad ? T(1) : T(0);
+        };
+        // the same lazy step split in two for the Riccati stages k < N: the primal update first (it
+        // is all the stage's first LDS exchange needs), the dual update after that exchange, where
+        // it fills the latency of the residual's LDS reads; the write-back is unconditional (a
+        // frozen group rewrites its unchanged words), so the stage stays one scheduling region
+        auto lazy_z = [&](El &q) {
+            const T zo = q.z;
+            q.z = pending ? q.z + alpha * q.dz : q.z;
+            return zo;
+        };
+        auto lazy_duals = [&](int k, El &q, T zo, const Bd &b) {
+            const bool vl = q.ll > T(0), vu = q.lu > T(0);
+            const T tl = zo - b.lb, tu = b.ub - zo, itl = frcp(tl), itu = frcp(tu);
+            const T dlal = -q.ll * (T(1) + q.dza * itl), dlau = -q.lu * (T(1) - q.dza * itu);
+            const T nl = q.ll + alpha * ((smu - q.ll * tl - dlal * q.dza - q.ll * q.dz) * itl);
+            const T nu_ = q.lu + alpha * ((smu - q.lu * tu + dlau * q.dza + q.lu * q.dz) * itu);
+            q.ll = (pending && vl) ? nl : q.ll;
+            q.lu = (pending && vu) ? nu_ : q.lu;
             stE(L::Z, k, q.z);
             stE(L::LL, k, q.ll);
             stE(L::LU, k, q.lu);
-        }
-    };
-    auto sigma = [&](const El &q, const Bd &b) {
-        const T sl = q.ll * frcp(q.z - b.lb), su = q.lu * frcp(b.ub - q.z);
-        return (q.ll > T(0) ? sl : T(0)) + (q.lu > T(0) ? su : T(0));
-    };
-    // exact finish: a bound is active where its multiplier exceeds its slack; the finish holds
-    // active bounds by the penalty rho (Hessian rho, gradient rho (z - bound)) and drops the
-    // barrier of the others (branch-free)
-    auto finish_terms = [&](const El &q, const Bd &b, T &sg, T &gadd) {
-        const bool al = q.ll > T(0) && q.ll > q.z - b.lb;
-        const bool au = !al && q.lu > T(0) && q.lu > b.ub - q.z;
-        const T rho = p.polish_rho;
-        sg = (al || au) ? rho : T(0);
-        gadd = (al || au) ? rho * (q.z - (al ? b.lb : b.ub)) : T(0);
-    };
-    // acceptance of the finish at element (k, r): active bounds keep a non-negative multiplier
-    // rho (bound - z_new) (to a few ulps), inactive ones hold (to 1e-9, then clamped) — the
-    // POLISH_TOL_ACTIVE / POLISH_TOL tests of the oracle
-    auto finish_bad = [&](T dz, const El &q, const Bd &b) {
-        const bool vl = q.ll > T(0), vu = q.lu > T(0);
-        const bool al = vl && q.ll > q.z - b.lb, au = !al && vu && q.lu > b.ub - q.z;
-        const T zn = q.z + dz;
-        const T sl = T(1) + fabs(b.lb), su = T(1) + fabs(b.ub);
-        const bool bad = al ? zn > fma(T(1e-15), sl, b.lb)
-                            : (au ? zn < fma(T(-1e-15), su, b.ub)
-                                  : ((vl && zn < fma(T(-1e-9), sl, b.lb)) || (vu && zn > fma(T(1e-9), su, b.ub))));
-        return bad ? T(1) : T(0);
-    };
-    // the same lazy step split in two for the Riccati stages k < N: the primal update first (it
-    // is all the stage's first LDS exchange needs), the dual update after that exchange, where
-    // it fills the latency of the residual's LDS reads; the write-back is unconditional (a
-    // frozen group rewrites its unchanged words), so the stage stays one scheduling region
-    auto lazy_z = [&](El &q) {
-        const T zo = q.z;
-        q.z = pending ? q.z + alpha * q.dz : q.z;
-        return zo;
-    };
-    auto lazy_duals = [&](int k, El &q, T zo, const Bd &b) {
-        const bool vl = q.ll > T(0), vu = q.lu > T(0);
-        const T tl = zo - b.lb, tu = b.ub - zo, itl = frcp(tl), itu = frcp(tu);
-        const T dlal = -q.ll * (T(1) + q.dza * itl), dlau = -q.lu * (T(1) - q.dza * itu);
-        const T nl = q.ll + alpha * ((smu - q.ll * tl - dlal * q.dza - q.ll * q.dz) * itl);
-        const T nu_ = q.lu + alpha * ((smu - q.lu * tu + dlau * q.dza + q.lu * q.dz) * itu);
-        q.ll = (pending && vl) ? nl : q.ll;
-        q.lu = (pending && vu) ? nu_ : q.lu;
-        stE(L::Z, k, q.z);
-        stE(L::LL, k, q.ll);
-        stE(L::LU, k, q.lu);
-    };
+        };
 
-    // ---- forward recursion (B: predictor into dza with ratio test / centring sums;
-    //      D: corrector into dz with step length / new-mu sums):
-    //      dx_0 = 0, du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx_k; du_k] + re_k
+        // ---- forward recursion (B: predictor into dza with ratio test / centring sums;
+        //      D: corrector into dz with step length / new-mu sums):
+        //      dx_0 = 0, du_k = kff_k + K_k dx_k, dx_{k+1} = [A B] [dx_k; du_k] + re_k
 #if (defined(NMPC_PHASE_TIMING) || defined(NMPC_FWD_TIMING)) && !defined(NMPC_SWEEP_TIMING)
 #define NMPC_SWEEP_TIMING 1
 #endif
 #ifdef NMPC_SWEEP_TIMING
-    // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per
-    // sweep, reported through the E_A/A/B/../D slots of nmpc_api.cpp (A -> 1, B -> 2, C -> 5, D -> 6)
-    const bool timed = p.cycles != nullptr;
-    unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = timed ? __builtin_amdgcn_s_memtime() : 0ull;
-    const unsigned long long tstart = tmark;
-    auto tick = [&](int slot) {
-        if (timed) {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            if (slot >= 0) tcy[slot] += t - tmark;
-            tmark = t;
-        }
-    };
+        // experiment builds only (build_experiment(..., ["NMPC_SWEEP_TIMING"])): clock cycles per
+        // sweep, reported through the E_A/A/B/../D slots of nmpc_api.cpp (A -> 1, B -> 2, C -> 5, D -> 6)
+        const bool timed = p.cycles != nullptr;
+        unsigned long long tcy[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tmark = timed ? __builtin_amdgcn_s_memtime() : 0ull;
+        const unsigned long long tstart = tmark;
+        auto tick = [&](int slot) {
+            if (timed) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                if (slot >= 0) tcy[slot] += t - tmark;
+                tmark = t;
+            }
+        };
 #define LPC_TICK(slot) tick(slot)
 #else
 #define LPC_TICK(slot) ((void)0)
 #endif
-// NMPC_PHASE_TIMING: also split the Riccati stage into pre (lazy step, g, re) -> slot 0,
-// M -> 3, F -> 4, Cholesky / gains / P update -> 7
+    // NMPC_PHASE_TIMING: also split the Riccati stage into pre (lazy step, g, re) -> slot 0,
+    // M -> 3, F -> 4, Cholesky / gains / P update -> 7
 #ifdef NMPC_PHASE_TIMING
 #define LPC_PTICK(slot) tick(slot)
 #else
 #define LPC_PTICK(slot) ((void)0)
 #endif
-// NMPC_FWD_TIMING: split the predictor sweep B into x writes (slot 0), u sums (3), x update (4),
-// statistics / store (7); the sweep remainder stays in slot 2
+    // NMPC_FWD_TIMING: split the predictor sweep B into x writes (slot 0), u sums (3), x update (4),
+    // statistics / store (7); the sweep remainder stays in slot 2
 #ifdef NMPC_FWD_TIMING
 #define LPC_FTICK(slot) do { if (!corr) tick(slot); } while (0)
 #else
 #define LPC_FTICK(slot) ((void)0)
 #endif
 
-    auto forward = [&](auto PASS, T &s_min, T &s_a, T &s_b, T &s_c) __attribute__((always_inline)) {
-        constexpr bool corr = decltype(PASS)::value == 1, fin = decltype(PASS)::value == 2;
-        const T *arow = abr + (xl ? r : 0) * LDZ;   // row r of [A B] (LDS, read per stage)
-        s_min = 1;
-        s_a = s_b = s_c = 0;
-        // ratio tests and closed-form mu sums of element (k, r), branch-free (selects instead of
-        // divergent arms). The predictor's quantities only steer the step length (safety factor
-        // 0.995) and sigma, so they use the raw hardware reciprocal; the corrector's dual step
-        // feeds mu_new (termination) and keeps the refined one.
-        auto stats = [&](T dz, const El &q, const Bd &b) {
-            const T lb = b.lb, ub = b.ub;
-            const bool vl = q.ll > T(0), vu = q.lu > T(0);
-            const T tl = q.z - lb, tu = ub - q.z;
-            T c = 1;
-            if constexpr (fin) {
-                s_c += finish_bad(dz, q, b);   // the finish: acceptance count only
-            } else if constexpr (!corr) {
-                // predictor: the largest inverse step ratio, division-free — primal -dz/t_l and
-                // dual -dlam_l/lam_l = 1 + dz/t_l (the affine dual step is -lam (1 + dz/t)), and
-                // the mirrored pair for the upper bound; alpha_aff = 1 / max(1, ...) per group
-                const T itl = rcp_raw(tl), itu = rcp_raw(tu);
-                const T al = dz * itl, au = dz * itu;
-                c = vl ? fmax(c, fmax(-al, T(1) + al)) : c;
-                c = vu ? fmax(c, fmax(au, T(1) - au)) : c;
-                s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
-                s_b += (vl ? q.ll * dz * (tl + dz) * itl : T(0)) + (vu ? q.lu * dz * (dz - tu) * itu : T(0));
-            } else {
-                const T rdz = rcp_raw(dz);
-                const T dza = q.dza;
-                const T itl = frcp(tl), itu = frcp(tu);
-                const T dlal = -q.ll * (T(1) + dza * itl), dlau = -q.lu * (T(1) - dza * itu);
-                const T dll = (smu - q.ll * tl - dlal * dza - q.ll * dz) * itl;
-                const T dlu = (smu - q.lu * tu + dlau * dza + q.lu * dz) * itu;
-                c = (vl && dz < T(0)) ? fmin(c, -tl * rdz) : c;
-                c = (vl && dll < T(0)) ? fmin(c, -q.ll * rcp_raw(dll)) : c;
-                c = (vu && dz > T(0)) ? fmin(c, tu * rdz) : c;
-                c = (vu && dlu < T(0)) ? fmin(c, -q.lu * rcp_raw(dlu)) : c;
-                s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
-                s_b += (vl ? dlal * dza : T(0)) - (vu ? dlau * dza : T(0));
-                s_c += (vl ? dll * dz : T(0)) - (vu ? dlu * dz : T(0));
-            }
-            s_min = corr ? fmin(s_min, c) : fmax(s_min, c);
-        };
-        struct Rec {
-            El e;
-            T c0, kq[NU];   // x-lane: K_k(:, r); u-lane: kff_k(u)
-        };
-        auto fetch = [&](int k, Rec &q) {
-            k = k < N ? k : N;
-            const int kk = k < N ? k : N - 1;
-            q.e.z = ldE(L::Z, k);
-            q.e.ll = ldE(L::LL, k);
-            q.e.lu = ldE(L::LU, k);
-            if (corr) q.e.dza = ldE(L::DZA, k);
-            // every lane loads the same record words (x: K(:, r); u: word 0 = kff) — loads in
-            // divergent arms get merged with a divergent offset (waterfall + private array)
-#pragma unroll
-            for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
-            q.c0 = q.kq[UKFF];
-        };
-        const int dst = (corr || fin) ? L::DZ : L::DZA;   // the finish's step goes to DZ
-        T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
-        // dx_{k+1}(r) = c_r + [A B](r, :) (z_k + dz_k) - z_{k+1}(r): the dynamics residual is
-        // folded in, so the sweep carries xt = dx_{k+1} + z_{k+1} and subtracts z_{k+1} when
-        // stage k+1's iterate has arrived
-        T xt = 0;
-        // stage records in flight PD stages ahead (ring slot j holds stage k = j mod PD; the
-        // stage loop is unrolled by PD so every slot is a fixed register set)
-        Rec ring[PD];
-#pragma unroll
-        for (int j = 0; j < PD; j++) fetch(j, ring[j]);
-        SpL<T, RN> arl;
-        if constexpr (SPARSE) sp_load(arl, slv, sli, row_base);
-        const Bd b0 = bnd(0), bm = bnd(1);   // stage 0 and interior bounds (sweep constants)
-#if NMPC_LPC_DEFER
-        // statistics pending from the previous stage (neutral before stage 0: no bound active)
-        T pm = 0;
-        El pe{};
-        Bd pb = b0;
-#endif
-        for (int kb = 0; kb < N; kb += PD) {
-#pragma unroll
-            for (int j = 0; j < PD; j++) {
-                const int k = kb + j;
-                if (k >= N) break;
-                LPC_FTICK(2);
-                // the slot is read in place and refilled after its last use: copying it out
-                // first makes the compiler move the refill's registers at the loop back edge,
-                // which waits for those loads and exposes their whole latency
-                Rec &q = ring[j];
-                const Bd bk = k == 0 ? b0 : bm;
-                const T dx = (k == 0 || !xl) ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
-#if NMPC_LPC_DEFER
-                // branch-free stage (one scheduling region per LDS exchange): u-lanes write their
-                // partial-product row into the spare row NX, which nobody reads
-                {
-                    const int pr_ = xl ? r : NX;
-#pragma unroll
-                    for (int i = 0; i < NU; i++) part[pr_ * LDU + i] = q.kq[i] * dx;
-                }
-                LPC_SYNC();
-                LPC_FTICK(0);
-                // the statistics of stage k-1 run here, between issuing the partial-sum reads
-                // and their first use, instead of at the end of stage k-1 on its critical path
-                stats(pm, pe, pb);
-                T du;
-                {
-                    const int uu = ul ? u : 0;
-                    T s0 = q.c0, s1 = 0;
-#pragma unroll
-                    for (int jj = 0; jj + 1 < NX; jj += 2) {
-                        s0 += part[jj * LDU + uu];
-                        s1 += part[(jj + 1) * LDU + uu];
-                    }
-                    if (NX % 2) s0 += part[(NX - 1) * LDU + uu];
-                    du = ul ? s0 + s1 : T(0);
-                }
-                const T my = xl ? dx : du;
-                zb[r] = q.e.z + my;
-                LPC_SYNC();
-                LPC_FTICK(3);
-#else
-                if (xl) {   // write-only divergent block
-#pragma unroll
-                    for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
-                    zb[r] = q.e.z + dx;
-                }
-                LPC_SYNC();
-                LPC_FTICK(0);
-                // u-lanes: du_u = kff_u + sum_j K(u, j) dx_j; every lane runs the same straight-line
-                // code (x-lanes sum column 0 and discard it)
-                T du;
-                {
-                    const int uu = ul ? u : 0;
-                    T s0 = q.c0, s1 = 0;
-#pragma unroll
-                    for (int jj = 0; jj + 1 < NX; jj += 2) {
-                        s0 += part[jj * LDU + uu];
-                        s1 += part[(jj + 1) * LDU + uu];
-                    }
-                    if (NX % 2) s0 += part[(NX - 1) * LDU + uu];
-                    du = ul ? s0 + s1 : T(0);
-                }
-                if (ul) zb[r] = q.e.z + du;
-                LPC_SYNC();
-                LPC_FTICK(3);
-                const T my = xl ? dx : du;
-#endif
-                if constexpr (SPARSE) {
-                    const T s = sp_dot(arl, zb, c_r);
-                    xt = xl ? s : xt;
+        auto forward = [&](auto PASS, T &s_min, T &s_a, T &s_b, T &s_c) __attribute__((always_inline)) {
+            constexpr bool corr = decltype(PASS)::value == 1, fin = decltype(PASS)::value == 2;
+            const T *arow = abr + (xl ? r : 0) * LDZ;   // row r of [A B] (LDS, read per stage)
+            s_min = 1;
+            s_a = s_b = s_c = 0;
+            // ratio tests and closed-form mu sums of element (k, r), branch-free (selects instead of
+            // divergent arms). The predictor's quantities only steer the step length (safety factor
+            // 0.995) and sigma, so they use the raw hardware reciprocal; the corrector's dual step
+            // feeds mu_new (termination) and keeps the refined one.
+            auto stats = [&](T dz, const El &q, const Bd &b) {
+                const T lb = b.lb, ub = b.ub;
+                const bool vl = q.ll > T(0), vu = q.lu > T(0);
+                const T tl = q.z - lb, tu = ub - q.z;
+                T c = 1;
+                if constexpr (fin) {
+                    // the finish: acceptance count (finish_check, at the stage store)
+                } else if constexpr (!corr) {
+                    // predictor: the largest inverse step ratio, division-free — primal -dz/t_l and
+                    // dual -dlam_l/lam_l = 1 + dz/t_l (the affine dual step is -lam (1 + dz/t)), and
+                    // the mirrored pair for the upper bound; alpha_aff = 1 / max(1, ...) per group
+                    const T itl = rcp_raw(tl), itu = rcp_raw(tu);
+                    const T al = dz * itl, au = dz * itu;
+                    c = vl ? fmax(c, fmax(-al, T(1) + al)) : c;
+                    c = vu ? fmax(c, fmax(au, T(1) - au)) : c;
+                    s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
+                    s_b += (vl ? q.ll * dz * (tl + dz) * itl : T(0)) + (vu ? q.lu * dz * (dz - tu) * itu : T(0));
                 } else {
-                    T s0 = c_r, s1 = 0;
-#pragma unroll
-                    for (int jj = 0; jj + 1 < NZ; jj += 2) {
-                        s0 = fma(arow[jj], zb[jj], s0);
-                        s1 = fma(arow[jj + 1], zb[jj + 1], s1);
-                    }
-                    if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
-                    xt = xl ? s0 + s1 : xt;
+                    const T rdz = rcp_raw(dz);
+                    const T dza = q.dza;
+                    const T itl = frcp(tl), itu = frcp(tu);
+                    const T dlal = -q.ll * (T(1) + dza * itl), dlau = -q.lu * (T(1) - dza * itu);
+                    const T dll = (smu - q.ll * tl - dlal * dza - q.ll * dz) * itl;
+                    const T dlu = (smu - q.lu * tu + dlau * dza + q.lu * dz) * itu;
+                    c = (vl && dz < T(0)) ? fmin(c, -tl * rdz) : c;
+                    c = (vl && dll < T(0)) ? fmin(c, -q.ll * rcp_raw(dll)) : c;
+                    c = (vu && dz > T(0)) ? fmin(c, tu * rdz) : c;
+                    c = (vu && dlu < T(0)) ? fmin(c, -q.lu * rcp_raw(dlu)) : c;
+                    s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
+                    s_b += (vl ? dlal * dza : T(0)) - (vu ? dlau * dza : T(0));
+                    s_c += (vl ? dll * dz : T(0)) - (vu ? dlu * dz : T(0));
                 }
-                LPC_FTICK(4);
-                // the corrector skips groups the finish completed: their DZ holds the finish step
-                if (!corr || status >= 0) stE(dst, k, my);
-#if NMPC_LPC_DEFER
-                pm = my;
-                pe = q.e;
-                pb = bk;
-#else
-                stats(my, q.e, bk);
-#endif
-                fetch(k + PD, ring[j]);
-                LPC_SYNC();
-                LPC_FTICK(7);
-            }
-        }
-#if NMPC_LPC_DEFER
-        stats(pm, pe, pb);
-#endif
-        if (xl) {
-            El e;
-            e.z = ldE(L::Z, N);
-            e.ll = ldE(L::LL, N);
-            e.lu = ldE(L::LU, N);
-            if (corr) e.dza = ldE(L::DZA, N);
-            const T dx = xt - e.z;
-            if (!corr || status >= 0) stE(dst, N, dx);
-            stats(dx, e, bnd(N));
-        }
-        s_min = corr ? gmin(s_min) : frcp(gmax(s_min));
-        s_a = gsum(s_a);
-        s_b = gsum(s_b);
-        s_c = gsum(s_c);
-    };
-
-    cptr<T> abs_ = (cptr<T>)p.AB;   // [NX][NZ] row-major, wave-uniform SGPR operand
-
-
-    for (int it = 0;; it++) {
-        const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
-        const bool bad = !isfinite(mu) || !isfinite(theta) || fail;
-        if (active && (conv || bad)) {
-            active = false;
-            status = conv && !bad ? 0 : 4;
-            iters = fail ? it - 1 : it;   // a failed factorisation ends the iteration it began
-        }
-        if (active && it >= p.max_iter) {
-            active = false;
-            status = 2;
-            iters = it;
-        }
-        if (!__any(active)) break;
-        LPC_TICK(-1);
-
-        // ============================ A: backward Riccati factorisation (+ lazy step, Sigma, g, re);
-        // the finish pass factors with the finish's penalty terms instead of the barrier
-        bool pfail = false;
-        auto riccati = [&](auto PASS) __attribute__((always_inline)) {
-            constexpr bool FIN = decltype(PASS)::value == 1;
-            T prow[NX], sdiag, pv;
-            T znext;
-            El q, qn;
-            auto fetchA = [&](int k, El &e) {
-                e.z = ldE(L::Z, k);
-                e.ll = ldE(L::LL, k);
-                e.lu = ldE(L::LU, k);
-                e.g = ldE(L::GC, k);
-                e.dz = ldE(L::DZ, k);     // unconditional: a divergent load arm costs more than
-                e.dza = ldE(L::DZA, k);   // the bytes (first iteration: unused stale words)
+                s_min = corr ? fmin(s_min, c) : fmax(s_min, c);
             };
-            // terminal stage: P_N = He + Sigma_N, p_N = g_N
-            fetchA(N, q);
-            fetchA(N - 1, qn);
-            lazy(N, q, bnd(N));
-            {
-                T sg = xl ? sigma(q, bnd(N)) : T(0), gadd = 0;
-                if constexpr (FIN) {
-                    finish_terms(q, bnd(N), sg, gadd);
-                    sg = xl ? sg : T(0);
-                }
-                zb[r] = xl ? q.z : T(0);
-                LPC_SYNC();
-                T g = q.g + gadd;
-                const int rx = xl ? r : 0;
-                if (SP::hdiag) {
-                    g = fma(hem[rx * LDX + rx], q.z, g);
-                } else {
-#pragma unroll
-                    for (int b = 0; b < NX; b++) g = fma(hem[rx * LDX + b], zb[b], g);
-                }
-                if (xl && !SP::hdiag) stE(L::GF, N, g);   // diagonal costs: C recomputes g
-#pragma unroll
-                for (int i = 0; i < NX; i++) prow[i] = SP::hdiag ? T(0) : hem[rx * LDX + i];
-                sdiag = sg + (SP::hdiag ? hem[rx * LDX + rx] : T(0));
-                pv = g;
-                znext = q.z;
-                LPC_SYNC();
-            }
-            for (int k = N - 1; k >= 0; k--) {
-                LPC_PTICK(1);
-                q = qn;
-                if (k > 0) fetchA(k - 1, qn);
-                SpL<T, RN> arl;
-                SpL<T, CN> acl;
-                if constexpr (SPARSE) {
-                    sp_load(arl, slv, sli, row_base);
-                    sp_load(acl, slv, sli, col_base);
-                }
-                const Bd bk = bnd(k);
-                const T hrr = SP::hdiag ? hm[r * LDZ + r] : T(0);   // read once per stage
-#if NMPC_LPC_EARLY_Z
-                const T zo = lazy_z(q);
-                zb[r] = q.z;
-                LPC_SYNC();
-                lazy_duals(k, q, zo, bk);
-                T sg = sigma(q, bk), gadd = 0;
-                if constexpr (FIN) finish_terms(q, bk, sg, gadd);
-#else
-                lazy(k, q, bk);
-                T sg = sigma(q, bk), gadd = 0;
-                if constexpr (FIN) finish_terms(q, bk, sg, gadd);
-                zb[r] = q.z;
-                LPC_SYNC();
-#endif
-                // g = H z + G yref (+ the finish's penalty gradient), re = [A B] z_k + c - x_{k+1}
-                T g = q.g + gadd, re = 0;
-                if (SP::hdiag) {
-                    g = fma(hrr, q.z, g);
-                } else {
-                    T g1 = 0;
-#pragma unroll
-                    for (int b = 0; b + 1 < NZ; b += 2) {
-                        g = fma(hm[r * LDZ + b], zb[b], g);
-                        g1 = fma(hm[r * LDZ + b + 1], zb[b + 1], g1);
-                    }
-                    if (NZ % 2) g = fma(hm[r * LDZ + NZ - 1], zb[NZ - 1], g);
-                    g += g1;
-                }
-                if (!SP::hdiag) stE(L::GF, k, g);
-                if constexpr (SPARSE) {
-                    re = sp_dot(arl, zb, c_r - znext);
-                    if (xl) rb[r] = re;
-                } else if (xl) {
-                    T s0 = c_r - znext, s1 = 0;
-#pragma unroll
-                    for (int j = 0; j + 1 < NZ; j += 2) {
-                        s0 = fma(abr[r * LDZ + j], zb[j], s0);
-                        s1 = fma(abr[r * LDZ + j + 1], zb[j + 1], s1);
-                    }
-                    if (NZ % 2) s0 = fma(abr[r * LDZ + NZ - 1], zb[NZ - 1], s0);
-                    re = s0 + s1;
-                    rb[r] = re;
-                }
-                znext = q.z;
-                LPC_SYNC();
-                LPC_PTICK(0);
-                // M = P [A B] (row r per x-lane; [A B] from SGPRs), Pr = P re, v = Pr + p
-                cptr<T> ab = abs_;
-                asm volatile("" : "+s"(ab));
-                if (xl) {
-                    T pr0 = sdiag * re, pr1 = 0;
-#pragma unroll
-                    for (int l = 0; l + 1 < NX; l += 2) {
-                        pr0 = fma(prow[l], rb[l], pr0);
-                        pr1 = fma(prow[l + 1], rb[l + 1], pr1);
-                    }
-                    if (NX % 2) pr0 = fma(prow[NX - 1], rb[NX - 1], pr0);
-                    const T pr = pr0 + pr1;
-                    stX(k, XPR, pr);
-                    vb[r] = pr + pv;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (xl) {
-                    // structured kernels: the diagonal part Sigma_x [A B](r, :) of M's row r
-                    // touches only the <= RN structural nonzeros of row r; it is added to M^T in
-                    // LDS (atomic adds after the plain stores, in order within the wavefront)
-                    // instead of scaling the dense LDS row of [A B] into all NZ accumulators
-                    constexpr bool ADIAG = SPARSE && NMPC_LPC_ATOMIC_DIAG;
-                    SpL<T, RN> arm;
-                    if constexpr (ADIAG) sp_load(arm, slv, sli, row_base);
-                    T mrow[NZ];
-#pragma unroll
-                    for (int c = 0; c < NZ; c++) mrow[c] = ADIAG ? T(0) : sdiag * abr[r * LDZ + c];
-                    sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int l, const T (&row)[NZ]) {
-#pragma unroll
-                        for (int c = 0; c < NZ; c++)
-                            if (SP::ab(l, c)) mrow[c] = fma(prow[l], row[c], mrow[c]);
-                    });
-#pragma unroll
-                    for (int c = 0; c < NZ; c++) mt[c * LDX + r] = mrow[c];
-                    if constexpr (ADIAG) {
-#pragma unroll
-                        for (int j = 0; j < RN; j++)
-                            __hip_atomic_fetch_add((T *)((char *)mt + arm.o[j] * LDX) + r, sdiag * arm.v[j],
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    }
-                }
-                LPC_SYNC();
-                LPC_PTICK(3);
-                // F = [A B]' M + H (column r per lane; + Sigma on the diagonal, applied by the
-                // readers), h = [A B]' v + g
-                T fcol[NZ], h;
-                if constexpr (SPARSE) {
-                    h = sp_dot(acl, vb, g);
-                } else {
-                    T h0 = g, h1 = 0;
-#pragma unroll
-                    for (int i = 0; i + 1 < NX; i += 2) {
-                        h0 = fma(abt[r * LDX + i], vb[i], h0);
-                        h1 = fma(abt[r * LDX + i + 1], vb[i + 1], h1);
-                    }
-                    if (NX % 2) h0 = fma(abt[r * LDX + NX - 1], vb[NX - 1], h0);
-                    h = h0 + h1;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                {
-                    T mc[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; i++) mc[i] = mt[r * LDX + i];
-#pragma unroll
-                    for (int a = 0; a < NZ; a++) fcol[a] = SP::hdiag ? T(0) : hm[r * LDZ + a];
-                    asm volatile("" : "+s"(ab));
-                    sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int i, const T (&row)[NZ]) {
-#pragma unroll
-                        for (int a = 0; a < NZ; a++)
-                            if (SP::ab(i, a)) fcol[a] = fma(row[a], mc[i], fcol[a]);
-                    });
-                    // materialise F here (IR sinking would otherwise defer the x part to the P
-                    // update and keep every streamed row of [A B] alive in SGPRs until then)
-#pragma unroll
-                    for (int a = 0; a < NZ; a++) asm volatile("" : "+v"(fcol[a]));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (ul) {
-                    T fd = fcol[NX];
-#pragma unroll
-                    for (int a = 0; a < NU; a++) {
-                        fu[a * NU + u] = fcol[NX + a];
-                        fd = (u == a) ? fcol[NX + a] : fd;
-                    }
-                    fu[u * NU + u] = fd + sg + hrr;
-                    hub[u] = h;
-                }
-                LPC_SYNC();
-                LPC_PTICK(4);
-                // F_uu = L L' (every lane), kff = -F_uu^{-1} h_u
-                T lf[NUT], hu[NU];
-#pragma unroll
-                for (int i = 0; i < NU; i++) hu[i] = hub[i];
-#pragma unroll
-                for (int i = 0; i < NU; i++)
-#pragma unroll
-                    for (int j = 0; j <= i; j++) {
-                        T s_ = fu[i * NU + j];
-#pragma unroll
-                        for (int l = 0; l < j; l++) s_ = fma(-lf[tri(i, l)], lf[tri(j, l)], s_);
-                        if (i == j) {
-                            const bool pd = s_ > T(0);
-                            if constexpr (FIN) pfail |= pol & !pd;
-                            else fail |= active & !pd;
-                            lf[tri(i, i)] = frsq(pd ? s_ : T(1));
-                        } else {
-                            lf[tri(i, j)] = s_ * lf[tri(j, j)];
-                        }
-                    }
-                // x-lane r: Y(:, r) = L^{-1} F_ux(:, r), K(:, r) = -L^{-T} Y(:, r), p_r = h_r + K(:, r)' h_u;
-                // u-lane u: F_uu^{-1}(u, :) = L^{-T} L^{-1} e_u, kff_u = -F_uu^{-1}(u, :) h_u — the same
-                // two triangular solves on different right-hand sides, run by every lane at once
-                T y[NU], xs[NU], pnew;
-                {
-                    T f[NU];
-#pragma unroll
-                    for (int i = 0; i < NU; i++) f[i] = xl ? fcol[NX + i] : ((u == i) ? T(1) : T(0));
-#pragma unroll
-                    for (int i = 0; i < NU; i++) {
-                        T s_ = f[i];
-#pragma unroll
-                        for (int l = 0; l < i; l++) s_ = fma(-lf[tri(i, l)], y[l], s_);
-                        y[i] = s_ * lf[tri(i, i)];
-                    }
-#pragma unroll
-                    for (int i = NU - 1; i >= 0; i--) {
-                        T s_ = y[i];
-#pragma unroll
-                        for (int l = i + 1; l < NU; l++) s_ = fma(-lf[tri(l, i)], xs[l], s_);
-                        xs[i] = s_ * lf[tri(i, i)];
-                    }
-                    T d = 0;
-#pragma unroll
-                    for (int i = 0; i < NU; i++) d = fma(xs[i], hu[i], d);
-                    pnew = (xl ? h : T(0)) - d;   // x: p_r; u: kff_u
-                }
-                // stage record words 0..NU: x-lane r: K(:, r) = -xs (Pr_r sits in word NU, stored
-                // above); u-lane u: kff_u, F_uu^{-1}(u, :) = xs
-                if (xl) {   // write-only divergent block
-#pragma unroll
-                    for (int i = 0; i < NU; i++) ylds[r * LDU + i] = y[i];
-                }
-                stX(k, 0, xl ? -xs[0] : pnew);
-#pragma unroll
-                for (int i = 1; i < NU; i++) stX(k, i, xl ? -xs[i] : xs[i - 1]);
-                if (ul) stU(k, NU, xs[NU - 1]);
-                LPC_SYNC();
-                // P(r, :) = F(r, 0:nx) - Y(:, r)' Y  (+ Sigma_x of stage k on the diagonal); u-lanes
-                // compute a dummy row (keeps the loop-carried registers dead between stages)
-                // The rows of Y stream from LDS in chunks of PCH rows, one chunk in flight while
-                // the previous one is consumed: left to itself the scheduler reused one register
-                // quad for all 26 reads, i.e. 26 serialised LDS round trips per stage.
-#if NMPC_LPC_PCH == 0
-#pragma unroll
-                for (int i = 0; i < NX; i++) {
-                    T s_ = fcol[i];
-#pragma unroll
-                    for (int a = 0; a < NU; a++) s_ = fma(-ylds[i * LDU + a], y[a], s_);
-                    prow[i] = s_;
-                }
-#else
-                {
-                    constexpr int PCH = NMPC_LPC_PCH, NPC = (NX + PCH - 1) / PCH;
-                    T yb[2][PCH][NU];
-                    auto yload = [&](int ch, T (&dst)[PCH][NU]) {
-#pragma unroll
-                        for (int ii = 0; ii < PCH; ii++) {
-                            const int i = ch * PCH + ii;
-#pragma unroll
-                            for (int a = 0; a < NU; a++) dst[ii][a] = i < NX ? ylds[i * LDU + a] : T(0);
-                        }
-                    };
-                    yload(0, yb[0]);
-#pragma unroll
-                    for (int ch = 0; ch < NPC; ch++) {
-                        if (ch + 1 < NPC) yload(ch + 1, yb[(ch + 1) & 1]);
-                        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                        for (int ii = 0; ii < PCH; ii++) {
-                            const int i = ch * PCH + ii;
-                            if (i < NX) {
-                                T s_ = fcol[i];
-#pragma unroll
-                                for (int a = 0; a < NU; a++) s_ = fma(-yb[ch & 1][ii][a], y[a], s_);
-                                prow[i] = s_;
-                            }
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-#endif
-                sdiag = sg + hrr;   // F(r, r) = F_col(r) + H_rr + Sigma
-                pv = pnew;
-                LPC_SYNC();
-                LPC_PTICK(7);
-            }
-        };
-
-        // ============================ exact finish (groups with mu <= polish_mu / 100^attempts):
-        // penalised factorisation + forward sweep writing the candidate to the outputs and counting
-        // violated acceptance tests; accepted groups are done, the others go on with this iteration
-        {
-            T thr = p.polish_mu;
-            for (int j = 0; j < fin_att; j++) thr *= T(0.01);
-            pol = active && p.polish_mu > T(0) && mu <= thr;
-        }
-        if (__any(pol)) {
-            riccati(Pass<1>{});
-            pending = false;
-            T d0, d1, d2, nbad;
-            forward(Pass<2>{}, d0, d1, d2, nbad);
-            if (pol) {
-                fin_att++;
-                if (nbad == T(0) && !pfail) {
-                    active = false;
-                    status = -1;
-                    iters = it + 1;
-                }
-            }
-            pol = false;
-            if (!__any(active)) break;
-        }
-        riccati(Pass<0>{});
-
-        LPC_TICK(1);
-        pending = false;   // the previous step is applied (converged groups stay frozen from here)
-
-        // ============================ B: forward predictor + ratio test / centring sums
-        T a_aff, S0, S2, dummy;
-        forward(Pass<0>{}, a_aff, S0, S2, dummy);
-        LPC_TICK(2);
-        // mu_aff = [(1 - a) S0 - a^2 S2'] / m with S2' = sum lam dz (t + dz) / t (closed form)
-        const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
-        const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
-        smu = sgm * sgm * sgm * mu;
-
-        // ============================ C: backward corrector vector
-        {
-            // sweep constants: H_rr, interior and stage-0 bounds
-            const T hrr = SP::hdiag ? hm[r * LDZ + r] : T(0);
-            const Bd b0 = bnd(0), bm = bnd(1);
-            auto ghat = [&](int k, const El &e) {
-                T g = e.g;
-                if (SP::hdiag) g = fma(k < N ? hrr : hem[(xl ? r : 0) * LDX + (xl ? r : 0)], e.z, g);
-                const Bd b = k == N ? bnd(N) : (k == 0 ? b0 : bm);
-                const T tl = e.z - b.lb, tu = b.ub - e.z, itl = frcp(tl), itu = frcp(tu);
-                const T dll = -e.ll * (T(1) + e.dza * itl), dlu = -e.lu * (T(1) - e.dza * itu);
-                const T cl = (dll * e.dza - smu) * itl, cu = (dlu * e.dza + smu) * itu;
-                return g + (e.ll > T(0) ? cl : T(0)) + (e.lu > T(0) ? cu : T(0));
-            };
-            struct RecC {
+            struct Rec {
                 El e;
-                T pr, kq[NU];
+                T c0, kq[NU];   // x-lane: K_k(:, r); u-lane: kff_k(u)
             };
-            auto fetchC = [&](int k, RecC &q) {
-                k = k < 0 ? 0 : k;
+            auto fetch = [&](int k, Rec &q) {
+                k = k < N ? k : N;
+                const int kk = k < N ? k : N - 1;
                 q.e.z = ldE(L::Z, k);
                 q.e.ll = ldE(L::LL, k);
                 q.e.lu = ldE(L::LU, k);
-                q.e.dza = ldE(L::DZA, k);
-                q.e.g = ldE(SP::hdiag ? L::GC : L::GF, k);   // diagonal costs: g = G yref + H_rr z below
-                const int kk = k < N ? k : N - 1;
-                // same words for every lane (see fetch of the forward sweeps): x-lane K(:, r) and
-                // Pr_r in words 0..NU, u-lane F_uu^{-1}(u, :) in words 1..NU
-                T w[NU + 1];
+                if (corr || fin) q.e.dza = (fin && fwarm) ? ldE(L::ACT, k < N ? k + 1 : N) : ldE(L::DZA, k);
+                if constexpr (fin) {   // finish: the step's base point (refinement: z_a = z + dz)
+                    const T dzp = ldE(L::DZ, k);
+                    q.e.z = fref ? q.e.z + dzp : q.e.z;
+                }
+                // every lane loads the same record words (x: K(:, r); u: word 0 = kff) — loads in
+                // divergent arms get merged with a divergent offset (waterfall + private array)
 #pragma unroll
-                for (int i = 0; i <= NU; i++) w[i] = ldX(kk, i);
-                q.pr = w[XPR];
-#pragma unroll
-                for (int i = 0; i < NU; i++) q.kq[i] = xl ? w[i] : w[UFI + i];
+                for (int i = 0; i < NU; i++) q.kq[i] = ldX(kk, i);
+                q.c0 = q.kq[UKFF];
             };
-            const T *acol = abt + r * LDX;   // column r of [A B] (LDS, read per stage)
-            RecC qN;
-            fetchC(N, qN);
-            T pv = ghat(N, qN.e);
-            RecC ring[PD];
+            const int dst = (corr || fin) ? L::DZ : L::DZA;   // the finish's step goes to DZ
+            T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
+            // dx_{k+1}(r) = c_r + [A B](r, :) (z_k + dz_k) - z_{k+1}(r): the dynamics residual is
+            // folded in, so the sweep carries xt = dx_{k+1} + z_{k+1} and subtracts z_{k+1} when
+            // stage k+1's iterate has arrived
+            T xt = 0;
+            // stage records in flight PD stages ahead (ring slot j holds stage k = j mod PD; the
+            // stage loop is unrolled by PD so every slot is a fixed register set)
+            Rec ring[PD];
 #pragma unroll
-            for (int j = 0; j < PD; j++) fetchC(N - 1 - j, ring[j]);
-            SpL<T, CN> acl;
-            if constexpr (SPARSE) sp_load(acl, slv, sli, col_base);
+            for (int j = 0; j < PD; j++) fetch(j, ring[j]);
+            SpL<T, RN> arl;
+            if constexpr (SPARSE) sp_load(arl, slv, sli, row_base);
+            const Bd b0 = bnd(0), bm = bnd(1);   // stage 0 and interior bounds (sweep constants)
+#if NMPC_LPC_DEFER
+            // statistics pending from the previous stage (neutral before stage 0: no bound active)
+            T pm = 0;
+            El pe{};
+            Bd pb = b0;
+#endif
             for (int kb = 0; kb < N; kb += PD) {
 #pragma unroll
                 for (int j = 0; j < PD; j++) {
-                    const int k = N - 1 - kb - j;
-                    if (k < 0) break;
-                    RecC &q = ring[j];   // read in place, refilled after its last use (see forward)
-#if NMPC_LPC_EARLY_Z
-                    // v first: the corrector right-hand side is only needed after the exchange
-                    if (xl) vb[r] = q.pr + pv;
-                    LPC_SYNC();
-                    const T gh = ghat(k, q.e);
-#else
-                    const T gh = ghat(k, q.e);
-                    if (xl) vb[r] = q.pr + pv;
-                    LPC_SYNC();
-#endif
-                    T h;
-                    if constexpr (SPARSE) {
-                        h = sp_dot(acl, vb, gh);
-                    } else {
-                        T h0 = gh, h1 = 0;
+                    const int k = kb + j;
+                    if (k >= N) break;
+                    LPC_FTICK(2);
+                    // the slot is read in place and refilled after its last use: copying it out
+                    // first makes the compiler move the refill's registers at the loop back edge,
+                    // which waits for those loads and exposes their whole latency
+                    Rec &q = ring[j];
+                    const Bd bk = k == 0 ? b0 : bm;
+                    const T dx = (k == 0 || !xl) ? T(0) : xt - q.e.z;   // x-lanes: dx_k (x_0 pinned)
+#if NMPC_LPC_DEFER
+                    // branch-free stage (one scheduling region per LDS exchange): u-lanes write their
+                    // partial-product row into the spare row NX, which nobody reads
+                    {
+                        const int pr_ = xl ? r : NX;
 #pragma unroll
-                        for (int i = 0; i + 1 < NX; i += 2) {
-                            h0 = fma(acol[i], vb[i], h0);
-                            h1 = fma(acol[i + 1], vb[i + 1], h1);
+                        for (int i = 0; i < NU; i++) part[pr_ * LDU + i] = q.kq[i] * dx;
+                    }
+                    LPC_SYNC();
+                    LPC_FTICK(0);
+                    // the statistics of stage k-1 run here, between issuing the partial-sum reads
+                    // and their first use, instead of at the end of stage k-1 on its critical path
+                    stats(pm, pe, pb);
+                    T du;
+                    {
+                        const int uu = ul ? u : 0;
+                        T s0 = q.c0, s1 = 0;
+#pragma unroll
+                        for (int jj = 0; jj + 1 < NX; jj += 2) {
+                            s0 += part[jj * LDU + uu];
+                            s1 += part[(jj + 1) * LDU + uu];
                         }
-                        if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
-                        h = h0 + h1;
+                        if (NX % 2) s0 += part[(NX - 1) * LDU + uu];
+                        du = ul ? s0 + s1 : T(0);
                     }
-                    if (ul) hub[u] = h;
+                    const T my = xl ? dx : du;
+                    zb[r] = q.e.z + my;
                     LPC_SYNC();
-                    T hu[NU];
+                    LPC_FTICK(3);
+#else
+                    if (xl) {   // write-only divergent block
 #pragma unroll
-                    for (int i = 0; i < NU; i++) hu[i] = hub[i];
-                    if (ul) {
-                        T kf = 0;
-#pragma unroll
-                        for (int i = 0; i < NU; i++) kf = fma(-q.kq[i], hu[i], kf);
-                        stU(k, UKFF, kf);
-                    } else {
-                        T s_ = h;
-#pragma unroll
-                        for (int i = 0; i < NU; i++) s_ = fma(q.kq[i], hu[i], s_);
-                        pv = s_;
+                        for (int i = 0; i < NU; i++) part[r * LDU + i] = q.kq[i] * dx;
+                        zb[r] = q.e.z + dx;
                     }
-                    fetchC(k - PD, ring[j]);
+                    LPC_SYNC();
+                    LPC_FTICK(0);
+                    // u-lanes: du_u = kff_u + sum_j K(u, j) dx_j; every lane runs the same straight-line
+                    // code (x-lanes sum column 0 and discard it)
+                    T du;
+                    {
+                        const int uu = ul ? u : 0;
+                        T s0 = q.c0, s1 = 0;
+#pragma unroll
+                        for (int jj = 0; jj + 1 < NX; jj += 2) {
+                            s0 += part[jj * LDU + uu];
+                            s1 += part[(jj + 1) * LDU + uu];
+                        }
+                        if (NX % 2) s0 += part[(NX - 1) * LDU + uu];
+                        du = ul ? s0 + s1 : T(0);
+                    }
+                    if (ul) zb[r] = q.e.z + du;
+                    LPC_SYNC();
+                    LPC_FTICK(3);
+                    const T my = xl ? dx : du;
+#endif
+                    if constexpr (SPARSE) {
+                        const T s = sp_dot(arl, zb, c_r);
+                        xt = xl ? s : xt;
+                    } else {
+                        T s0 = c_r, s1 = 0;
+#pragma unroll
+                        for (int jj = 0; jj + 1 < NZ; jj += 2) {
+                            s0 = fma(arow[jj], zb[jj], s0);
+                            s1 = fma(arow[jj + 1], zb[jj + 1], s1);
+                        }
+                        if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
+                        xt = xl ? s0 + s1 : xt;
+                    }
+                    LPC_FTICK(4);
+                    if constexpr (fin) {
+                        // finish: acceptance tests, next active set; polishing groups only store (a
+                        // finished group's DZ / DZA are its result)
+                        T na;
+                        const T a = fin_flag(q.e, bk, fs0);
+                        s_c += finish_check(my, q.e, bk, a, na);
+                        if (pol) {
+                            if (fref) {
+                                stE(L::DZA, k, my);
+                            } else {
+                                stE(L::DZ, k, my);
+                                stE(L::DZA, k, na);
+                            }
+                        }
+                    } else if (status >= 0) {
+                        stE(dst, k, my);   // groups the finish completed keep their DZ / DZA
+                    }
+#if NMPC_LPC_DEFER
+                    pm = my;
+                    pe = q.e;
+                    pb = bk;
+#else
+                    stats(my, q.e, bk);
+#endif
+                    fetch(k + PD, ring[j]);
+                    LPC_SYNC();
+                    LPC_FTICK(7);
+                }
+            }
+#if NMPC_LPC_DEFER
+            stats(pm, pe, pb);
+#endif
+            if (xl) {
+                El e;
+                e.z = ldE(L::Z, N);
+                e.ll = ldE(L::LL, N);
+                e.lu = ldE(L::LU, N);
+                if (corr || fin) e.dza = (fin && fwarm) ? ldE(L::ACT, N) : ldE(L::DZA, N);
+                if constexpr (fin) {
+                    const T dzp = ldE(L::DZ, N);
+                    e.z = fref ? e.z + dzp : e.z;
+                }
+                const T dx = xt - e.z;
+                if constexpr (fin) {
+                    T na;
+                    const T a = fin_flag(e, bnd(N), fs0);
+                    s_c += finish_check(dx, e, bnd(N), a, na);
+                    if (pol) {
+                        if (fref) {
+                            stE(L::DZA, N, dx);
+                        } else {
+                            stE(L::DZ, N, dx);
+                            stE(L::DZA, N, na);
+                        }
+                    }
+                } else if (status >= 0) {
+                    stE(dst, N, dx);
+                }
+                stats(dx, e, bnd(N));
+            }
+            s_min = corr ? gmin(s_min) : frcp(gmax(s_min));
+            s_a = gsum(s_a);
+            s_b = gsum(s_b);
+            s_c = gsum(s_c);
+        };
+
+        cptr<T> abs_ = (cptr<T>)p.AB;   // [NX][NZ] row-major, wave-uniform SGPR operand
+
+
+        for (int it = 0;; it++) {
+            const bool conv = mu <= p.tol_comp && theta * r0 <= p.tol_res;
+            const bool bad = !isfinite(mu) || !isfinite(theta) || fail;
+            if (active && (conv || bad)) {
+                active = false;
+                status = conv && !bad ? 0 : 4;
+                iters = (fail ? it - 1 : it) + fin_steps;   // a failed factorisation ends the iteration it began
+            }
+            if (active && it >= p.max_iter) {
+                active = false;
+                status = 2;
+                iters = it + fin_steps;
+            }
+            if (!__any(active)) break;
+            LPC_TICK(-1);
+
+            // ============================ A: backward Riccati factorisation (+ lazy step, Sigma, g, re);
+            // the finish pass factors with the finish's penalty terms instead of the barrier
+            bool pfail = false;
+            auto riccati = [&](auto PASS) __attribute__((always_inline)) {
+                constexpr bool FIN = decltype(PASS)::value == 1;
+                T prow[NX], sdiag, pv;
+                T znext;
+                El q, qn;
+                auto fetchA = [&](int k, El &e) {
+                    e.z = ldE(L::Z, k);
+                    e.ll = ldE(L::LL, k);
+                    e.lu = ldE(L::LU, k);
+                    e.g = ldE(L::GC, k);
+                    e.dz = ldE(L::DZ, k);     // unconditional: a divergent load arm costs more than
+                    // the bytes (first iteration: unused stale words; warm finish: the shifted flags)
+                    e.dza = (FIN && fwarm) ? ldE(L::ACT, k < N ? k + 1 : N) : ldE(L::DZA, k);
+                };
+                // terminal stage: P_N = He + Sigma_N, p_N = g_N
+                fetchA(N, q);
+                fetchA(N - 1, qn);
+                lazy(N, q, bnd(N));
+                {
+                    T sg = xl ? sigma(q, bnd(N)) : T(0), gadd = 0;
+                    if constexpr (FIN) {
+                        finish_terms(q, bnd(N), fs0, sg, gadd);
+                        sg = xl ? sg : T(0);
+                    }
+                    zb[r] = xl ? q.z : T(0);
+                    LPC_SYNC();
+                    T g = q.g + gadd;
+                    const int rx = xl ? r : 0;
+                    if (SP::hdiag) {
+                        g = fma(hem[rx * LDX + rx], q.z, g);
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < NX; b++) g = fma(hem[rx * LDX + b], zb[b], g);
+                    }
+                    if (xl && !SP::hdiag) stE(L::GF, N, g);   // diagonal costs: C recomputes g
+#pragma unroll
+                    for (int i = 0; i < NX; i++) prow[i] = SP::hdiag ? T(0) : hem[rx * LDX + i];
+                    sdiag = sg + (SP::hdiag ? hem[rx * LDX + rx] : T(0));
+                    pv = g;
+                    znext = q.z;
                     LPC_SYNC();
                 }
+                for (int k = N - 1; k >= 0; k--) {
+                    LPC_PTICK(1);
+                    q = qn;
+                    if (k > 0) fetchA(k - 1, qn);
+                    SpL<T, RN> arl;
+                    SpL<T, CN> acl;
+                    if constexpr (SPARSE) {
+                        sp_load(arl, slv, sli, row_base);
+                        sp_load(acl, slv, sli, col_base);
+                    }
+                    const Bd bk = bnd(k);
+                    const T hrr = SP::hdiag ? hm[r * LDZ + r] : T(0);   // read once per stage
+#if NMPC_LPC_EARLY_Z
+                    const T zo = lazy_z(q);
+                    zb[r] = q.z;
+                    LPC_SYNC();
+                    lazy_duals(k, q, zo, bk);
+                    T sg = sigma(q, bk), gadd = 0;
+                    if constexpr (FIN) finish_terms(q, bk, fs0, sg, gadd);
+#else
+                    lazy(k, q, bk);
+                    T sg = sigma(q, bk), gadd = 0;
+                    if constexpr (FIN) finish_terms(q, bk, fs0, sg, gadd);
+                    zb[r] = q.z;
+                    LPC_SYNC();
+#endif
+                    // g = H z + G yref (+ the finish's penalty gradient), re = [A B] z_k + c - x_{k+1}
+                    T g = q.g + gadd, re = 0;
+                    if (SP::hdiag) {
+                        g = fma(hrr, q.z, g);
+                    } else {
+                        T g1 = 0;
+#pragma unroll
+                        for (int b = 0; b + 1 < NZ; b += 2) {
+                            g = fma(hm[r * LDZ + b], zb[b], g);
+                            g1 = fma(hm[r * LDZ + b + 1], zb[b + 1], g1);
+                        }
+                        if (NZ % 2) g = fma(hm[r * LDZ + NZ - 1], zb[NZ - 1], g);
+                        g += g1;
+                    }
+                    if (!SP::hdiag) stE(L::GF, k, g);
+                    if constexpr (SPARSE) {
+                        re = sp_dot(arl, zb, c_r - znext);
+                        if (xl) rb[r] = re;
+                    } else if (xl) {
+                        T s0 = c_r - znext, s1 = 0;
+#pragma unroll
+                        for (int j = 0; j + 1 < NZ; j += 2) {
+                            s0 = fma(abr[r * LDZ + j], zb[j], s0);
+                            s1 = fma(abr[r * LDZ + j + 1], zb[j + 1], s1);
+                        }
+                        if (NZ % 2) s0 = fma(abr[r * LDZ + NZ - 1], zb[NZ - 1], s0);
+                        re = s0 + s1;
+                        rb[r] = re;
+                    }
+                    znext = q.z;
+                    LPC_SYNC();
+                    LPC_PTICK(0);
+                    // M = P [A B] (row r per x-lane; [A B] from SGPRs), Pr = P re, v = Pr + p
+                    cptr<T> ab = abs_;
+                    asm volatile("" : "+s"(ab));
+                    if (xl) {
+                        T pr0 = sdiag * re, pr1 = 0;
+#pragma unroll
+                        for (int l = 0; l + 1 < NX; l += 2) {
+                            pr0 = fma(prow[l], rb[l], pr0);
+                            pr1 = fma(prow[l + 1], rb[l + 1], pr1);
+                        }
+                        if (NX % 2) pr0 = fma(prow[NX - 1], rb[NX - 1], pr0);
+                        const T pr = pr0 + pr1;
+                        stX(k, XPR, pr);
+                        vb[r] = pr + pv;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (xl) {
+                        // structured kernels: the diagonal part Sigma_x [A B](r, :) of M's row r
+                        // touches only the <= RN structural nonzeros of row r; it is added to M^T in
+                        // LDS (atomic adds after the plain stores, in order within the wavefront)
+                        // instead of scaling the dense LDS row of [A B] into all NZ accumulators
+                        constexpr bool ADIAG = SPARSE && NMPC_LPC_ATOMIC_DIAG;
+                        SpL<T, RN> arm;
+                        if constexpr (ADIAG) sp_load(arm, slv, sli, row_base);
+                        T mrow[NZ];
+#pragma unroll
+                        for (int c = 0; c < NZ; c++) mrow[c] = ADIAG ? T(0) : sdiag * abr[r * LDZ + c];
+                        sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int l, const T (&row)[NZ]) {
+#pragma unroll
+                            for (int c = 0; c < NZ; c++)
+                                if (SP::ab(l, c)) mrow[c] = fma(prow[l], row[c], mrow[c]);
+                        });
+#pragma unroll
+                        for (int c = 0; c < NZ; c++) mt[c * LDX + r] = mrow[c];
+                        if constexpr (ADIAG) {
+#pragma unroll
+                            for (int j = 0; j < RN; j++)
+                                __hip_atomic_fetch_add((T *)((char *)mt + arm.o[j] * LDX) + r, sdiag * arm.v[j],
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        }
+                    }
+                    LPC_SYNC();
+                    LPC_PTICK(3);
+                    // F = [A B]' M + H (column r per lane; + Sigma on the diagonal, applied by the
+                    // readers), h = [A B]' v + g
+                    T fcol[NZ], h;
+                    if constexpr (SPARSE) {
+                        h = sp_dot(acl, vb, g);
+                    } else {
+                        T h0 = g, h1 = 0;
+#pragma unroll
+                        for (int i = 0; i + 1 < NX; i += 2) {
+                            h0 = fma(abt[r * LDX + i], vb[i], h0);
+                            h1 = fma(abt[r * LDX + i + 1], vb[i + 1], h1);
+                        }
+                        if (NX % 2) h0 = fma(abt[r * LDX + NX - 1], vb[NX - 1], h0);
+                        h = h0 + h1;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    {
+                        T mc[NX];
+#pragma unroll
+                        for (int i = 0; i < NX; i++) mc[i] = mt[r * LDX + i];
+#pragma unroll
+                        for (int a = 0; a < NZ; a++) fcol[a] = SP::hdiag ? T(0) : hm[r * LDZ + a];
+                        asm volatile("" : "+s"(ab));
+                        sgpr_rows<NX, NZ, RPC, SP, T>(ab, [&](int i, const T (&row)[NZ]) {
+#pragma unroll
+                            for (int a = 0; a < NZ; a++)
+                                if (SP::ab(i, a)) fcol[a] = fma(row[a], mc[i], fcol[a]);
+                        });
+                        // materialise F here (IR sinking would otherwise defer the x part to the P
+                        // update and keep every streamed row of [A B] alive in SGPRs until then)
+#pragma unroll
+                        for (int a = 0; a < NZ; a++) asm volatile("" : "+v"(fcol[a]));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (ul) {
+                        T fd = fcol[NX];
+#pragma unroll
+                        for (int a = 0; a < NU; a++) {
+                            fu[a * NU + u] = fcol[NX + a];
+                            fd = (u == a) ? fcol[NX + a] : fd;
+                        }
+                        fu[u * NU + u] = fd + sg + hrr;
+                        hub[u] = h;
+                    }
+                    LPC_SYNC();
+                    LPC_PTICK(4);
+                    // F_uu = L L' (every lane), kff = -F_uu^{-1} h_u
+                    T lf[NUT], hu[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) hu[i] = hub[i];
+#pragma unroll
+                    for (int i = 0; i < NU; i++)
+#pragma unroll
+                        for (int j = 0; j <= i; j++) {
+                            T s_ = fu[i * NU + j];
+#pragma unroll
+                            for (int l = 0; l < j; l++) s_ = fma(-lf[tri(i, l)], lf[tri(j, l)], s_);
+                            if (i == j) {
+                                const bool pd = s_ > T(0);
+                                if constexpr (FIN) pfail |= pol & !pd;
+                                else fail |= active & !pd;
+                                lf[tri(i, i)] = frsq(pd ? s_ : T(1));
+                            } else {
+                                lf[tri(i, j)] = s_ * lf[tri(j, j)];
+                            }
+                        }
+                    // x-lane r: Y(:, r) = L^{-1} F_ux(:, r), K(:, r) = -L^{-T} Y(:, r), p_r = h_r + K(:, r)' h_u;
+                    // u-lane u: F_uu^{-1}(u, :) = L^{-T} L^{-1} e_u, kff_u = -F_uu^{-1}(u, :) h_u — the same
+                    // two triangular solves on different right-hand sides, run by every lane at once
+                    T y[NU], xs[NU], pnew;
+                    {
+                        T f[NU];
+#pragma unroll
+                        for (int i = 0; i < NU; i++) f[i] = xl ? fcol[NX + i] : ((u == i) ? T(1) : T(0));
+#pragma unroll
+                        for (int i = 0; i < NU; i++) {
+                            T s_ = f[i];
+#pragma unroll
+                            for (int l = 0; l < i; l++) s_ = fma(-lf[tri(i, l)], y[l], s_);
+                            y[i] = s_ * lf[tri(i, i)];
+                        }
+#pragma unroll
+                        for (int i = NU - 1; i >= 0; i--) {
+                            T s_ = y[i];
+#pragma unroll
+                            for (int l = i + 1; l < NU; l++) s_ = fma(-lf[tri(l, i)], xs[l], s_);
+                            xs[i] = s_ * lf[tri(i, i)];
+                        }
+                        T d = 0;
+#pragma unroll
+                        for (int i = 0; i < NU; i++) d = fma(xs[i], hu[i], d);
+                        pnew = (xl ? h : T(0)) - d;   // x: p_r; u: kff_u
+                    }
+                    // stage record words 0..NU: x-lane r: K(:, r) = -xs (Pr_r sits in word NU, stored
+                    // above); u-lane u: kff_u, F_uu^{-1}(u, :) = xs
+                    if (xl) {   // write-only divergent block
+#pragma unroll
+                        for (int i = 0; i < NU; i++) ylds[r * LDU + i] = y[i];
+                    }
+                    stX(k, 0, xl ? -xs[0] : pnew);
+#pragma unroll
+                    for (int i = 1; i < NU; i++) stX(k, i, xl ? -xs[i] : xs[i - 1]);
+                    if (ul) stU(k, NU, xs[NU - 1]);
+                    LPC_SYNC();
+                    // P(r, :) = F(r, 0:nx) - Y(:, r)' Y  (+ Sigma_x of stage k on the diagonal); u-lanes
+                    // compute a dummy row (keeps the loop-carried registers dead between stages)
+                    // The rows of Y stream from LDS in chunks of PCH rows, one chunk in flight while
+                    // the previous one is consumed: left to itself the scheduler reused one register
+                    // quad for all 26 reads, i.e. 26 serialised LDS round trips per stage.
+#if NMPC_LPC_PCH == 0
+#pragma unroll
+                    for (int i = 0; i < NX; i++) {
+                        T s_ = fcol[i];
+#pragma unroll
+                        for (int a = 0; a < NU; a++) s_ = fma(-ylds[i * LDU + a], y[a], s_);
+                        prow[i] = s_;
+                    }
+#else
+                    {
+                        constexpr int PCH = NMPC_LPC_PCH, NPC = (NX + PCH - 1) / PCH;
+                        T yb[2][PCH][NU];
+                        auto yload = [&](int ch, T (&dst)[PCH][NU]) {
+#pragma unroll
+                            for (int ii = 0; ii < PCH; ii++) {
+                                const int i = ch * PCH + ii;
+#pragma unroll
+                                for (int a = 0; a < NU; a++) dst[ii][a] = i < NX ? ylds[i * LDU + a] : T(0);
+                            }
+                        };
+                        yload(0, yb[0]);
+#pragma unroll
+                        for (int ch = 0; ch < NPC; ch++) {
+                            if (ch + 1 < NPC) yload(ch + 1, yb[(ch + 1) & 1]);
+                            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                            for (int ii = 0; ii < PCH; ii++) {
+                                const int i = ch * PCH + ii;
+                                if (i < NX) {
+                                    T s_ = fcol[i];
+#pragma unroll
+                                    for (int a = 0; a < NU; a++) s_ = fma(-yb[ch & 1][ii][a], y[a], s_);
+                                    prow[i] = s_;
+                                }
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
+#endif
+                    sdiag = sg + hrr;   // F(r, r) = F_col(r) + H_rr + Sigma
+                    pv = pnew;
+                    LPC_SYNC();
+                    LPC_PTICK(7);
+                }
+            };
+
+            // ============================ exact finish (groups with mu <= polish_at): a primal-dual
+            // active-set run of penalised factorisations + forward sweeps (<= polish_steps set steps,
+            // then the refinement) for the polishing groups; accepted groups are done, the others go
+            // on with this iteration from their untouched IPM iterate
+            pol = active && p.polish_mu > T(0) && mu <= polish_at;
+            if (__any(pol)) {
+                polish_at = pol ? fmin(polish_at, mu) * T(0.01) : polish_at;
+                fref = false;
+                for (int fs = 0; fs <= p.polish_steps; fs++) {
+                    fs0 = fs == 0;
+                    fwarm = warm && fs0 && it == 0;   // first run of the solve: pending is false
+                    pfail = false;
+                    riccati(Pass<1>{});
+                    pending = false;
+                    T d0, d1, d2, nbad;
+                    forward(Pass<2>{}, d0, d1, d2, nbad);
+                    if (pol) {
+                        fin_steps++;
+                        const bool okp = nbad == T(0) && !pfail;
+                        if (fref) {
+                            if (okp) {
+                                active = false;
+                                status = -1;
+                                iters = it + fin_steps;
+                            }
+                            pol = false;
+                        } else if (okp) {
+                            fref = true;
+                        } else if (pfail || fs + 1 >= p.polish_steps) {
+                            pol = false;
+                        }
+                    }
+                    if (!__any(pol)) break;
+                }
+                pol = fref = false;
+                fwarm = false;
+                if (!__any(active)) break;
+            }
+            riccati(Pass<0>{});
+
+            LPC_TICK(1);
+            pending = false;   // the previous step is applied (converged groups stay frozen from here)
+
+            // ============================ B: forward predictor + ratio test / centring sums
+            T a_aff, S0, S2, dummy;
+            forward(Pass<0>{}, a_aff, S0, S2, dummy);
+            LPC_TICK(2);
+            // mu_aff = [(1 - a) S0 - a^2 S2'] / m with S2' = sum lam dz (t + dz) / t (closed form)
+            const T mu_aff = ((T(1) - a_aff) * S0 - a_aff * a_aff * S2) * p.inv_m;
+            const T sgm = mu > T(0) ? fmax(mu_aff, T(0)) * frcp(mu) : T(0);
+            smu = sgm * sgm * sgm * mu;
+
+            // ============================ C: backward corrector vector
+            {
+                // sweep constants: H_rr, interior and stage-0 bounds
+                const T hrr = SP::hdiag ? hm[r * LDZ + r] : T(0);
+                const Bd b0 = bnd(0), bm = bnd(1);
+                auto ghat = [&](int k, const El &e) {
+                    T g = e.g;
+                    if (SP::hdiag) g = fma(k < N ? hrr : hem[(xl ? r : 0) * LDX + (xl ? r : 0)], e.z, g);
+                    const Bd b = k == N ? bnd(N) : (k == 0 ? b0 : bm);
+                    const T tl = e.z - b.lb, tu = b.ub - e.z, itl = frcp(tl), itu = frcp(tu);
+                    const T dll = -e.ll * (T(1) + e.dza * itl), dlu = -e.lu * (T(1) - e.dza * itu);
+                    const T cl = (dll * e.dza - smu) * itl, cu = (dlu * e.dza + smu) * itu;
+                    return g + (e.ll > T(0) ? cl : T(0)) + (e.lu > T(0) ? cu : T(0));
+                };
+                struct RecC {
+                    El e;
+                    T pr, kq[NU];
+                };
+                auto fetchC = [&](int k, RecC &q) {
+                    k = k < 0 ? 0 : k;
+                    q.e.z = ldE(L::Z, k);
+                    q.e.ll = ldE(L::LL, k);
+                    q.e.lu = ldE(L::LU, k);
+                    q.e.dza = ldE(L::DZA, k);
+                    q.e.g = ldE(SP::hdiag ? L::GC : L::GF, k);   // diagonal costs: g = G yref + H_rr z below
+                    const int kk = k < N ? k : N - 1;
+                    // same words for every lane (see fetch of the forward sweeps): x-lane K(:, r) and
+                    // Pr_r in words 0..NU, u-lane F_uu^{-1}(u, :) in words 1..NU
+                    T w[NU + 1];
+#pragma unroll
+                    for (int i = 0; i <= NU; i++) w[i] = ldX(kk, i);
+                    q.pr = w[XPR];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) q.kq[i] = xl ? w[i] : w[UFI + i];
+                };
+                const T *acol = abt + r * LDX;   // column r of [A B] (LDS, read per stage)
+                RecC qN;
+                fetchC(N, qN);
+                T pv = ghat(N, qN.e);
+                RecC ring[PD];
+#pragma unroll
+                for (int j = 0; j < PD; j++) fetchC(N - 1 - j, ring[j]);
+                SpL<T, CN> acl;
+                if constexpr (SPARSE) sp_load(acl, slv, sli, col_base);
+                for (int kb = 0; kb < N; kb += PD) {
+#pragma unroll
+                    for (int j = 0; j < PD; j++) {
+                        const int k = N - 1 - kb - j;
+                        if (k < 0) break;
+                        RecC &q = ring[j];   // read in place, refilled after its last use (see forward)
+#if NMPC_LPC_EARLY_Z
+                        // v first: the corrector right-hand side is only needed after the exchange
+                        if (xl) vb[r] = q.pr + pv;
+                        LPC_SYNC();
+                        const T gh = ghat(k, q.e);
+#else
+                        const T gh = ghat(k, q.e);
+                        if (xl) vb[r] = q.pr + pv;
+                        LPC_SYNC();
+#endif
+                        T h;
+                        if constexpr (SPARSE) {
+                            h = sp_dot(acl, vb, gh);
+                        } else {
+                            T h0 = gh, h1 = 0;
+#pragma unroll
+                            for (int i = 0; i + 1 < NX; i += 2) {
+                                h0 = fma(acol[i], vb[i], h0);
+                                h1 = fma(acol[i + 1], vb[i + 1], h1);
+                            }
+                            if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                            h = h0 + h1;
+                        }
+                        if (ul) hub[u] = h;
+                        LPC_SYNC();
+                        T hu[NU];
+#pragma unroll
+                        for (int i = 0; i < NU; i++) hu[i] = hub[i];
+                        if (ul) {
+                            T kf = 0;
+#pragma unroll
+                            for (int i = 0; i < NU; i++) kf = fma(-q.kq[i], hu[i], kf);
+                            stU(k, UKFF, kf);
+                        } else {
+                            T s_ = h;
+#pragma unroll
+                            for (int i = 0; i < NU; i++) s_ = fma(q.kq[i], hu[i], s_);
+                            pv = s_;
+                        }
+                        fetchC(k - PD, ring[j]);
+                        LPC_SYNC();
+                    }
+                }
+            }
+
+            LPC_TICK(5);
+            // ============================ D: forward corrector + step length / new mu
+            T amax, T0, C1, C2;
+            forward(Pass<1>{}, amax, T0, C1, C2);
+            LPC_TICK(6);
+            const T a = fmin(T(1), T(0.995) * amax);
+            // a failed factorisation (F_uu not positive definite) leaves the iterate as it stood at the
+            // start of this iteration, like the oracle's early exit (oracle/c/riccati_ipm.c:222)
+            if (active && !fail) {
+                // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
+                mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
+                theta *= (T(1) - a);
+                alpha = a;
+                pending = true;
             }
         }
 
-        LPC_TICK(5);
-        // ============================ D: forward corrector + step length / new mu
-        T amax, T0, C1, C2;
-        forward(Pass<1>{}, amax, T0, C1, C2);
-        LPC_TICK(6);
-        const T a = fmin(T(1), T(0.995) * amax);
-        // a failed factorisation (F_uu not positive definite) leaves the iterate as it stood at the
-        // start of this iteration, like the oracle's early exit (oracle/c/riccati_ipm.c:222)
-        if (active && !fail) {
-            // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
-            mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
-            theta *= (T(1) - a);
-            alpha = a;
-            pending = true;
-        }
-    }
-
-    // ------------------------------------------------------------------ apply pending step, outputs
-    if (!inst_ok) return;
-    T *xo = p.xout + (size_t)inst * (N + 1) * NX;
-    T *uo = p.uout + (size_t)inst * N * NU;
-    for (int k = 0; k <= N; k++) {
-        if (k == N && ul) continue;
-        T z = ldE(L::Z, k);
-        if (pending) z += alpha * ldE(L::DZ, k);
-        if (status < 0) {   // completed by the finish: its step, clamped onto the active bounds
-            const T lb = LB(k), ub = UB(k);
-            z += ldE(L::DZ, k);
-            z = has_bound(lb) ? fmax(z, lb) : z;
-            z = has_bound(ub) ? fmin(z, ub) : z;
-        }
-        if (xl) xo[k * NX + r] = z;
-        else uo[k * NU + u] = z;
-    }
-    if (r == 0) {
-        p.status[inst] = status < 0 ? 0 : status;
-        p.iters[inst] = iters;
+        // ------------------------------------------------------------------ apply pending step, outputs
+        if (inst_ok) {
+            T *xo = p.xout + (size_t)inst * (N + 1) * NX;
+            T *uo = p.uout + (size_t)inst * N * NU;
+            T fprev = 0;
+            for (int k = 0; k <= N; k++) {
+                if (k == N && ul) {
+                    if (fused) stE(L::ACT, N, fprev);   // u-lanes: stage N mirrors N - 1 for the shift
+                    continue;
+                }
+                T z = ldE(L::Z, k);
+                if (pending) z += alpha * ldE(L::DZ, k);
+                if (status < 0) {   // completed by the finish: step + refinement, clamped onto the bounds
+                    const T lb = LB(k), ub = UB(k);
+                    z += ldE(L::DZ, k) + ldE(L::DZA, k);
+                    z = has_bound(lb) ? fmax(z, lb) : z;
+                    z = has_bound(ub) ? fmin(z, ub) : z;
+                }
+                if (xl) xo[k * NX + r] = z;
+                else uo[k * NU + u] = z;
+                if (fused) {   // the solution's active flags, the next step's warm start
+                    const T lb = LB(k), ub = UB(k);
+                    const bool onl = has_bound(lb) && z <= lb + T(1e-7) * (T(1) + fabs(lb));
+                    const bool onu = has_bound(ub) && z >= ub - T(1e-7) * (T(1) + fabs(ub));
+                    fprev = onl ? T(-1) : (onu ? T(1) : T(0));
+                    stE(L::ACT, k, fprev);
+                }
+            }
+            if (r == 0) {
+                p.status[inst] = status < 0 ? 0 : status;
+                p.iters[inst] = iters;
 #ifdef NMPC_SWEEP_TIMING
-        if (timed) {
-            unsigned long long *c = p.cycles + (size_t)inst * 9;
-            for (int j = 0; j < 8; j++) c[j] = tcy[j];
-            c[8] = __builtin_amdgcn_s_memtime() - tstart;
-        }
+                if (timed) {
+                    unsigned long long *c = p.cycles + (size_t)inst * 9;
+                    for (int j = 0; j < 8; j++) c[j] = tcy[j];
+                    c[8] = __builtin_amdgcn_s_memtime() - tstart;
+                }
 #endif
+            }
+        }
+        if (fused) {
+            // closed-loop advance of this step by the instance's lanes (its outputs were written by
+            // the lanes of this wavefront just above); the next step's x0 is read by the whole group
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (inst_ok)
+                cl_advance_group<T, NX, NU>(p.cl, inst, p.cl.step + cstep, status < 0 ? 0 : status, r,
+                                            p.cl_noise[(size_t)inst * nsteps + cstep]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
     }
 }
 

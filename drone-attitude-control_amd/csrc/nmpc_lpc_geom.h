@@ -50,7 +50,10 @@ struct Layout {
     static constexpr int LW = (64 / (NX + NU)) * (NX + NU);
     static constexpr int Z = 0, LL = 1, LU = 2, DZA = 3, DZ = 4, GC = 5, GF = HDIAG ? -1 : 6, REC = HDIAG ? 6 : 7;
     static constexpr int RECW = NU + 1;
-    static constexpr int NW = REC + RECW;
+    // ACT: active flag of the last solve's solution (fused closed loop: the next step's finish
+    // starts from it, shifted by one stage)
+    static constexpr int ACT = REC + RECW;
+    static constexpr int NW = ACT + 1;
     __host__ __device__ static size_t wave_elems(int N) { return ((size_t)(N + 1) * NW * LW + 15) & ~size_t(15); }
 };
 

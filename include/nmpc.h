@@ -114,11 +114,15 @@ typedef struct nmpc_ocp_desc {
     double qp_solver_tol_comp; /* <= 0: 1e-15 (fp64) / 1e-7 (fp32); fp32 clamps to >= 1e-7 */
     double qp_solver_tol_res;  /* <= 0: 1e-12 (fp64) / 1e-5 (fp32); fp32 clamps to >= 1e-5 */
     double qp_solver_mu0;      /* <= 0: 1e-2 */
-    /* exact finish (active-set polish): once mu <= qp_solver_polish_mu (retried at
-     * mu / 100 after a rejected attempt) one Newton step with the identified active bounds held
-     * and the others dropped; accepted when it satisfies the QP's KKT sign and bound conditions.
-     * 0: 1e-6 (fp64 handles; fp32 handles never polish); < 0: off */
+    /* exact finish (oracle/c/riccati_ipm.c): once mu <= qp_solver_polish_mu, a
+     * primal-dual active-set run of at most qp_solver_polish_steps Newton steps from the current
+     * iterate (active bounds held by a penalty, the others dropped; the first active set is
+     * where the IPM multiplier exceeds the slack), then one refinement step; accepted when the
+     * QP's KKT sign and bound conditions hold, else the IPM goes on and the next run waits for
+     * mu to drop 100-fold. 0: 1 (first run at the start for the default mu0; fp64 handles only,
+     * fp32 handles never run it); < 0: off */
     double qp_solver_polish_mu;
+    int qp_solver_polish_steps; /* <= 0: 12 */
 } nmpc_ocp_desc;
 
 typedef struct nmpc_solver nmpc_solver;
@@ -218,11 +222,16 @@ typedef struct nmpc_closed_loop_desc {
 
 /* bind the closed loop to a solver handle (allocates the table/state/accumulators on the device) */
 int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d);
-/* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion */
+/* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion. With the
+ * lane-per-component and wavefront kernel families the steps run fused: each solve launch carries
+ * up to 64 steps of every instance (prepare + solve + advance per instance, no step barrier
+ * between instances; env NMPC_CL_FUSED=0 for one prepare / solve / advance launch per step) —
+ * the same results either way */
 int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync);
 /* out[0] sum closed-loop cost, out[1] sum AED numerator, out[2] failed solves, out[3] instance-steps,
- * out[4] total device ms of the solve kernel over the last run (HIP events around each launch),
- * out[5] solve launches in the last run, out[6] mean qp_iter of the last step */
+ * out[4] total device ms of the solve kernel launches of the last run (HIP events around each),
+ * out[5] solve launches in the last run, out[6] mean qp_iter of the last step, out[7] closed-loop
+ * steps of the last run */
 int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n);
 /* per-instance accumulators, batch*4: [cost sum, AED numerator, failed solves, steps] of each
  * instance (the Monte-Carlo distribution behind nmpc_closed_loop_stats' sums) */

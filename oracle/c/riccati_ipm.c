@@ -39,6 +39,7 @@ typedef struct {
     double tol_comp, tol_res, mu0;
     int max_iter;
     double polish_mu;           /* > 0: exact finish (active-set polish) once mu <= polish_mu */
+    int polish_steps;           /* active-set Newton steps per finish attempt */
 } ocp_ref_desc;
 
 static int has(double b) { return fabs(b) < INFB; }
@@ -46,18 +47,23 @@ static int has(double b) { return fabs(b) < INFB; }
 /* per-instance workspace sizes */
 typedef struct {
     double *z, *ll, *lu, *dza, *dz, *gc, *gf, *gh, *re, *Pr, *Luu, *Lxu, *lu_vec, *sg;
+    signed char *act;   /* finish: active bound per element (-1 lower, 1 upper, 0 none) */
 } ws_t;
 
 /* Relative weight of the exact finish's penalty on the identified active bounds: the
- * penalised solution sits lambda / rho from the bound, and rho / |F| costs about
- * eps * rho / |F| in the Schur complements, so sqrt(1/eps) balances the two. */
-#define POLISH_RHO 1e8
+ * penalised solution sits lambda / rho from the bound and rho / |F| costs about eps * rho / |F|
+ * in the Schur complements; the refinement step removes the first to first order, so a moderate
+ * weight keeps the second small (1e5..1e7 give the same 1e-11 answers on the goldens, 1e8
+ * starts to lose accepted solutions to rounding) */
+#define POLISH_RHO 1e6
 /* acceptance of the exact finish, relative to 1 + |bound|: an inactive bound may be violated by
  * POLISH_TOL (the result is clamped onto it); an active bound's multiplier rho * (bound - z)
  * must not fall below -rho * POLISH_TOL_ACTIVE (a few ulps: a wrongly fixed bound shows up as
  * a negative multiplier, i.e. z on the feasible side of the bound) */
 #define POLISH_TOL 1e-9
 #define POLISH_TOL_ACTIVE 1e-15
+/* largest refinement correction accepted, relative to 1 + |z| */
+#define POLISH_TOL_REFINE 1e-3
 
 static void interior(double *v, double l, double u)
 {
@@ -178,7 +184,7 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
 {
     const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ny = d->ny;
     const double *A = d->A, *B = d->B, *c = d->c;
-    double P[NZMAX * NZMAX], M[NZMAX * NZMAX], F[NZMAX * NZMAX], p[NZMAX], v[NZMAX], h[NZMAX];
+    double p[NZMAX], v[NZMAX], h[NZMAX];
     int k, i, j, l, it, status = 2, m = 0;
 
     /* stage widths: stage k<N has nz comps, stage N has nx */
@@ -250,7 +256,7 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
     double theta = 1.0;
     if (m == 0) m = 1;
     double polish_at = d->polish_mu > 0.0 ? d->polish_mu : -1.0, rho = 1.0;
-    int polished = 0;
+    int fin_steps = 0;
     for (i = 0; i < nz * nz; i += nz + 1) rho = fmax(rho, fabs(d->H[i]));
     for (i = 0; i < nx * nx; i += nx + 1) rho = fmax(rho, fabs(d->He[i]));
     rho *= POLISH_RHO;
@@ -299,55 +305,133 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
                 w->re[k * nx + i] = s;
             }
         if (mu <= polish_at) {
-            /* exact finish: a bound is active where its multiplier exceeds its slack; one Newton
-             * step on the QP with those bounds held by a penalty of weight rho (inactive bounds
-             * dropped) lands on the active-set solution. Accepted when every inactive bound
-             * holds and every active one keeps a non-negative multiplier rho * (bound - z);
-             * otherwise the IPM iterate is untouched and the next attempt waits for
-             * mu <= polish_at / 100. */
-            polish_at *= 1e-2;
+            /* exact finish, a primal-dual active-set (PDAS) run of at most polish_steps Newton
+             * steps on the QP from the current iterate: the active bounds (first step: where the
+             * IPM multiplier exceeds the slack) are held by a penalty of weight rho, the others
+             * dropped; one Newton step lands on that active set's solution. Accepted when every
+             * inactive bound holds and every active one keeps a non-negative multiplier
+             * rho * (bound - z) — the QP's KKT conditions; otherwise the violated inactive bounds
+             * join and the negative-multiplier ones leave the active set for the next step. If no
+             * step is accepted the IPM iterate is untouched and the next run waits for mu to
+             * drop 100-fold. */
+            polish_at = (mu < polish_at ? mu : polish_at) * 1e-2;
             for (k = 0; k <= N; k++) {
                 int n = k < N ? nz : nx;
                 for (i = 0; i < n; i++) {
-                    double sgv = 0.0, g = w->gf[k * nz + i];
+                    signed char a = 0;
                     if (!(k == 0 && i < nx)) {
-                        double lbv = LBk(d, k, i), ubv = UBk(d, k, i);
-                        if (LL(k, i) > 0.0 && LL(k, i) > Z(k, i) - lbv) { sgv = rho; g += rho * (Z(k, i) - lbv); }
-                        else if (LU(k, i) > 0.0 && LU(k, i) > ubv - Z(k, i)) { sgv = rho; g += rho * (Z(k, i) - ubv); }
+                        if (LL(k, i) > 0.0 && LL(k, i) > Z(k, i) - LBk(d, k, i)) a = -1;
+                        else if (LU(k, i) > 0.0 && LU(k, i) > UBk(d, k, i) - Z(k, i)) a = 1;
                     }
-                    w->sg[k * nz + i] = sgv;
-                    w->gh[k * nz + i] = g;
+                    w->act[k * nz + i] = a;
                 }
             }
-            if (backward(d, w, w->gh) == 0) {
+            int ok = 0;
+            for (int step = 0; step < d->polish_steps && !ok; step++) {
+                fin_steps++;
+                for (k = 0; k <= N; k++) {
+                    int n = k < N ? nz : nx;
+                    for (i = 0; i < n; i++) {
+                        const signed char a = w->act[k * nz + i];
+                        double g = w->gf[k * nz + i];
+                        if (a) g += rho * (Z(k, i) - (a < 0 ? LBk(d, k, i) : UBk(d, k, i)));
+                        w->sg[k * nz + i] = a ? rho : 0.0;
+                        w->gh[k * nz + i] = g;
+                    }
+                }
+                if (backward(d, w, w->gh) != 0) break;
                 FORWARD(w->dz);
-                int ok = 1;
-                for (k = 0; k <= N && ok; k++) {
+                ok = 1;
+                for (k = 0; k <= N; k++) {
                     int n = k < N ? nz : nx;
                     for (i = (k == 0 ? nx : 0); i < n; i++) {
-                        double zn = Z(k, i) + w->dz[k * nz + i], lbv = LBk(d, k, i), ubv = UBk(d, k, i);
-                        if (w->sg[k * nz + i] > 0.0) {
-                            if (LL(k, i) > 0.0 && LL(k, i) > Z(k, i) - lbv
-                                    ? zn > lbv + POLISH_TOL_ACTIVE * (1.0 + fabs(lbv))
-                                    : zn < ubv - POLISH_TOL_ACTIVE * (1.0 + fabs(ubv))) { ok = 0; break; }
-                        } else if ((has(lbv) && zn < lbv - POLISH_TOL * (1.0 + fabs(lbv))) ||
-                                   (has(ubv) && zn > ubv + POLISH_TOL * (1.0 + fabs(ubv)))) { ok = 0; break; }
+                        const double zn = Z(k, i) + w->dz[k * nz + i], lbv = LBk(d, k, i), ubv = UBk(d, k, i);
+                        signed char *a = &w->act[k * nz + i];
+                        if (*a < 0) {
+                            if (zn > lbv + POLISH_TOL_ACTIVE * (1.0 + fabs(lbv))) { ok = 0; *a = 0; }
+                        } else if (*a > 0) {
+                            if (zn < ubv - POLISH_TOL_ACTIVE * (1.0 + fabs(ubv))) { ok = 0; *a = 0; }
+                        } else if (has(lbv) && zn < lbv - POLISH_TOL * (1.0 + fabs(lbv))) {
+                            ok = 0; *a = -1;
+                        } else if (has(ubv) && zn > ubv + POLISH_TOL * (1.0 + fabs(ubv))) {
+                            ok = 0; *a = 1;
+                        }
+                    }
+                }
+            }
+            if (ok) {
+                /* refinement: the penalised solution z_a sits lambda / rho off its active bounds
+                 * and carries the rounding of a rho-weighted solve; one more Newton step from z_a
+                 * on the same active set with the bounds shifted by that offset (target
+                 * 2 b - z_a, i.e. gradient H z_a + g_c + 2 rho (z_a - b)) removes both to first
+                 * order. Accepted when the refined point holds every bound to POLISH_TOL, sits on
+                 * its active bounds to POLISH_TOL and the correction stayed below POLISH_TOL_REFINE
+                 * (a larger one means the rho-weighted solve was not accurate); otherwise the IPM
+                 * goes on from its own iterate. */
+                for (k = 0; k <= N; k++) {
+                    int n = k < N ? nz : nx;
+                    for (i = 0; i < n; i++) w->dza[k * nz + i] = Z(k, i) + (k == 0 && i < nx ? 0.0 : w->dz[k * nz + i]);
+                }
+                /* gradient and dynamics residual at z_a (w->dza holds z_a) */
+                for (k = 0; k <= N; k++) {
+                    const int n = k < N ? nz : nx;
+                    const double *Hm = k < N ? d->H : d->He;
+                    for (i = 0; i < n; i++) {
+                        double g = w->gc[k * nz + i];
+                        for (j = 0; j < n; j++) g += Hm[i * n + j] * w->dza[k * nz + j];
+                        const signed char a = w->act[k * nz + i];
+                        if (a) g += 2.0 * rho * (w->dza[k * nz + i] - (a < 0 ? LBk(d, k, i) : UBk(d, k, i)));
+                        w->gh[k * nz + i] = g;
+                    }
+                }
+                for (k = 0; k < N; k++)
+                    for (i = 0; i < nx; i++) {
+                        double s = c[i] - w->dza[(k + 1) * nz + i];
+                        for (j = 0; j < nx; j++) s += A[i * nx + j] * w->dza[k * nz + j];
+                        for (j = 0; j < nu; j++) s += B[i * nu + j] * w->dza[k * nz + nx + j];
+                        w->re[k * nx + i] = s;
+                    }
+                fin_steps++;
+                ok = backward(d, w, w->gh) == 0;
+                if (ok) {
+                    FORWARD(w->dz);
+                    for (k = 0; k <= N && ok; k++) {
+                        int n = k < N ? nz : nx;
+                        for (i = (k == 0 ? nx : 0); i < n; i++) {
+                            const double za = w->dza[k * nz + i], zr = za + w->dz[k * nz + i];
+                            const double lbv = LBk(d, k, i), ubv = UBk(d, k, i);
+                            const signed char a = w->act[k * nz + i];
+                            const double tl = POLISH_TOL * (1.0 + fabs(lbv)), tu = POLISH_TOL * (1.0 + fabs(ubv));
+                            if (fabs(w->dz[k * nz + i]) > POLISH_TOL_REFINE * (1.0 + fabs(za)) ||
+                                (a < 0 && fabs(zr - lbv) > tl) || (a > 0 && fabs(zr - ubv) > tu) ||
+                                (!a && has(lbv) && zr < lbv - tl) || (!a && has(ubv) && zr > ubv + tu)) {
+                                ok = 0;
+                                break;
+                            }
+                        }
                     }
                 }
                 if (ok) {
                     for (k = 0; k <= N; k++) {
                         int n = k < N ? nz : nx;
                         for (i = (k == 0 ? nx : 0); i < n; i++) {
-                            double zn = Z(k, i) + w->dz[k * nz + i], lbv = LBk(d, k, i), ubv = UBk(d, k, i);
+                            double zn = w->dza[k * nz + i] + w->dz[k * nz + i], lbv = LBk(d, k, i), ubv = UBk(d, k, i);
                             if (has(lbv) && zn < lbv) zn = lbv;
                             if (has(ubv) && zn > ubv) zn = ubv;
                             Z(k, i) = zn;
                         }
                     }
                     status = 0;
-                    polished = 1;
                     break;
                 }
+                /* the residual at the IPM iterate (overwritten above) for the iteration that follows */
+                for (k = 0; k < N; k++)
+                    for (i = 0; i < nx; i++) {
+                        double s = c[i] - Z(k + 1, i);
+                        for (j = 0; j < nx; j++) s += A[i * nx + j] * Z(k, j);
+                        for (j = 0; j < nu; j++) s += B[i * nu + j] * Z(k, nx + j);
+                        w->re[k * nx + i] = s;
+                    }
             }
         }
         /* ---- backward factorisation (+ predictor vector) ---- */
@@ -487,7 +571,7 @@ done:
         for (i = 0; i < nx; i++) xo[k * nx + i] = Z(k, i);
     for (k = 0; k < N; k++)
         for (j = 0; j < nu; j++) uo[k * nu + j] = Z(k, nx + j);
-    *iters_out = it + polished;
+    *iters_out = it + fin_steps;   /* Newton systems solved: IPM iterations + finish steps */
     return status;
 #undef Z
 #undef LL
@@ -514,13 +598,14 @@ int riccati_ipm_solve_batch(const ocp_ref_desc *d, int batch, const double *x0, 
 #pragma omp parallel num_threads(nthreads) reduction(+ : nfail)
     {
         size_t S = (size_t)(N + 1) * nz;
-        double *buf = (double *)malloc(sizeof(double) * (9 * S + (size_t)N * (2 * nx + nu * nu + nx * nu + nu)));
+        double *buf = (double *)malloc(sizeof(double) * (9 * S + (size_t)N * (2 * nx + nu * nu + nx * nu + nu)) + S);
         ws_t w;
         w.z = buf; w.ll = w.z + S; w.lu = w.ll + S; w.dza = w.lu + S; w.dz = w.dza + S;
         w.gc = w.dz + S; w.gf = w.gc + S; w.gh = w.gf + S;
         w.re = w.gh + S; w.Pr = w.re + (size_t)N * nx; w.Luu = w.Pr + (size_t)N * nx;
         w.Lxu = w.Luu + (size_t)N * nu * nu; w.lu_vec = w.Lxu + (size_t)N * nx * nu;
         w.sg = w.lu_vec + (size_t)N * nu;
+        w.act = (signed char *)(w.sg + S);
 #pragma omp for schedule(dynamic, 16)
         for (int b = 0; b < batch; b++) {
             int st = solve_one(d, x0 + (size_t)b * nx, yref + (size_t)b * ystride,

@@ -36,12 +36,15 @@ class _Desc(ctypes.Structure):
         ("lb", ctypes.c_void_p), ("ub", ctypes.c_void_p),
         ("lbe", ctypes.c_void_p), ("ube", ctypes.c_void_p),
         ("tol_comp", ctypes.c_double), ("tol_res", ctypes.c_double), ("mu0", ctypes.c_double),
-        ("max_iter", ctypes.c_int), ("polish_mu", ctypes.c_double),
+        ("max_iter", ctypes.c_int), ("polish_mu", ctypes.c_double), ("polish_steps", ctypes.c_int),
     ]
 
 
 INF = 1e30
-DEFAULT_POLISH_MU = 1e-6   # include/nmpc.h qp_solver_polish_mu default (fp64 handles)
+# include/nmpc.h defaults of the exact finish (fp64 handles): first attempt once mu <= 1 (at the
+# start for mu0 <= 1), at most 12 active-set steps per attempt
+DEFAULT_POLISH_MU = 1.0
+DEFAULT_POLISH_STEPS = 12
 
 
 def stage_qp_data(spec):
@@ -69,7 +72,8 @@ def stage_qp_data(spec):
 
 
 class RiccatiIpmRef:
-    def __init__(self, spec, tol_comp=1e-15, tol_res=1e-12, mu0=1e-2, max_iter=50, polish_mu=0.0):
+    def __init__(self, spec, tol_comp=1e-15, tol_res=1e-12, mu0=1e-2, max_iter=50, polish_mu=0.0,
+                 polish_steps=None):
         self.lib = ctypes.CDLL(build())
         self.lib.riccati_ipm_solve_batch.restype = ctypes.c_int
         self.lib.riccati_ipm_max_threads.restype = ctypes.c_int
@@ -82,17 +86,19 @@ class RiccatiIpmRef:
         self.desc = _Desc(spec.nx, spec.nu, spec.N, spec.ny, spec.nx,
                           p("A"), p("B"), p("c"), p("H"), p("G"), p("He"), p("Ge"),
                           p("lb0"), p("ub0"), p("lb"), p("ub"), p("lbe"), p("ube"),
-                          tol_comp, tol_res, mu0, max_iter, polish_mu)
+                          tol_comp, tol_res, mu0, max_iter, polish_mu,
+                          DEFAULT_POLISH_STEPS if polish_steps is None else polish_steps)
 
     @classmethod
     def for_options(cls, spec, o, precision="fp64"):
         """The oracle configured like the engine handle of an OCP with solver options `o`
-        (include/nmpc.h defaults: tol_comp 1e-15, tol_res 1e-12, exact finish at mu <= 1e-6 on
-        fp64 handles, none on fp32; a negative polish threshold switches it off)."""
+        (include/nmpc.h defaults: tol_comp 1e-15, tol_res 1e-12, exact finish from mu <= 1 with
+        <= 12 active-set steps on fp64 handles, none on fp32; a negative threshold switches it off)."""
         pm = getattr(o, "qp_solver_polish_mu", None) or 0.0
         pm = 0.0 if pm < 0 or precision != "fp64" else (pm or DEFAULT_POLISH_MU)
+        ps = getattr(o, "qp_solver_polish_steps", None) or DEFAULT_POLISH_STEPS
         return cls(spec, tol_comp=o.qp_solver_tol_comp or 1e-15, tol_res=o.qp_solver_tol_stat or 1e-12,
-                   polish_mu=pm)
+                   polish_mu=pm, polish_steps=ps)
 
     def max_threads(self):
         """Host threads this process may use: the CPU affinity mask, capped by OMP_NUM_THREADS

@@ -171,3 +171,32 @@ def test_solve_after_closed_loop_uses_host_inputs(data):
     assert np.array_equal(s.get_batch("u"), u1)
     o = qp.solve_ocp(models.force_model(20), x0, yref, ye)
     assert np.abs(u1[0] - o["U"]).max() < 1e-6
+
+
+@pytest.mark.parametrize("model,N,B,kernel", [("quad13", 20, 1000, None), ("force", 20, 777, "wave"),
+                                              ("force", 20, 777, "lpc"), ("jerk", 40, 301, None)])
+def test_fused_closed_loop_matches_per_step(model, N, B, kernel):
+    """The fused closed loop (steps inside the solve kernel, nmpc_closed_loop_run's default for the
+    lane-per-component and wavefront families) gives the per-step loop's results (one prepare /
+    solve / advance launch per step, NMPC_CL_FUSED=0): states, per-instance cost / AED sums and
+    failure counts, over 70 steps (two fused launches, 64 + 6 steps), ragged batches."""
+    from drone_attitude_control_amd.batched import ClosedLoop
+
+    def run(fused):
+        if kernel:
+            os.environ["NMPC_KERNEL"] = kernel
+        os.environ["NMPC_CL_FUSED"] = "1" if fused else "0"
+        try:
+            cl = ClosedLoop(model, B, N=N, seed=7)
+            cl.run(70)
+            return cl.state(), cl.instance_stats(), cl.stats()
+        finally:
+            os.environ.pop("NMPC_KERNEL", None)
+            os.environ.pop("NMPC_CL_FUSED", None)
+
+    xs, ins, sts = run(False)
+    xf, inf, stf = run(True)
+    assert sts["solve_launches"] == 70 and stf["solve_launches"] == 2 and stf["steps"] == 70
+    assert np.array_equal(ins[:, 2:], inf[:, 2:])            # failures, steps per instance
+    assert np.allclose(xf, xs, rtol=1e-12, atol=1e-12), np.abs(xf - xs).max()
+    assert np.allclose(inf[:, :2], ins[:, :2], rtol=1e-12, atol=1e-12)
