@@ -257,8 +257,10 @@ def main():
                          "pipe": ("FP64 FMA on the VALU" if args.precision == "fp64" else "FP32 FMA on the VALU")
                          + " (MI355X: FP64 matrix peak = FP64 vector peak; FP32 matrix peak = FP32 vector peak)",
                          "kernel": info["kernel"], "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": pmc.get("hbm_bytes_per_launch"),
-                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per launch from the committed rocprofv3 PMC pass "
+                         "frac": achieved / peak,
+                         "traffic": pmc.get("hbm_bytes_per_step", pmc.get("hbm_bytes_per_launch")),
+                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per closed-loop step (per launch / fused steps per "
+                                         "launch) from the committed rocprofv3 PMC pass "
                                          f"({pmc.get('source', 'none for this config')}); no x2 FETCH_SIZE "
                                          "correction: the kernel's loads are 4/8-B per lane, the guide's x2 is "
                                          "calibrated for 16-B streams; includes Infinity-Cache hits",

@@ -177,9 +177,10 @@ def test_solve_after_closed_loop_uses_host_inputs(data):
                                               ("force", 20, 777, "lpc"), ("jerk", 40, 301, None)])
 def test_fused_closed_loop_matches_per_step(model, N, B, kernel):
     """The fused closed loop (steps inside the solve kernel, nmpc_closed_loop_run's default for the
-    lane-per-component and wavefront families) gives the per-step loop's results (one prepare /
-    solve / advance launch per step, NMPC_CL_FUSED=0): states, per-instance cost / AED sums and
-    failure counts, over 70 steps (two fused launches, 64 + 6 steps), ragged batches."""
+    lane-per-component and wavefront families, with warm-started active sets) gives the per-step
+    loop's results (one prepare / solve / advance launch per step, NMPC_CL_FUSED=0): states,
+    per-instance cost / AED sums and failure counts, over 70 steps (two fused launches, 64 + 6
+    steps), ragged batches."""
     from drone_attitude_control_amd.batched import ClosedLoop
 
     def run(fused):
@@ -198,5 +199,7 @@ def test_fused_closed_loop_matches_per_step(model, N, B, kernel):
     xf, inf, stf = run(True)
     assert sts["solve_launches"] == 70 and stf["solve_launches"] == 2 and stf["steps"] == 70
     assert np.array_equal(ins[:, 2:], inf[:, 2:])            # failures, steps per instance
-    assert np.allclose(xf, xs, rtol=1e-12, atol=1e-12), np.abs(xf - xs).max()
-    assert np.allclose(inf[:, :2], ins[:, :2], rtol=1e-12, atol=1e-12)
+    # certified solutions reached by different paths (warm-started active sets, no finish after a
+    # failed step in the fused loop) agree to rounding, far inside the 1e-6 solve bar
+    assert np.allclose(xf, xs, rtol=1e-9, atol=1e-9), np.abs(xf - xs).max()
+    assert np.allclose(inf[:, :2], ins[:, :2], rtol=1e-9, atol=1e-9)

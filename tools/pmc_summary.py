@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--kernel", default="ipm_kernel")
     ap.add_argument("--out", default=None)
     ap.add_argument("--traffic", default=None, help="model,N,batch,precision")
+    ap.add_argument("--steps-per-launch", type=int, default=1,
+                    help="closed-loop steps per solve launch (fused closed loop: the bench's --steps)")
     a = ap.parse_args()
     means, ndisp, meta = collect(a.tag, a.kernel)
     if not means:
@@ -73,6 +75,8 @@ def main():
         d["entries"] = [e for e in d["entries"] if (e["model"], e["N"], e["batch"], e["precision"]) != key]
         d["entries"].append({"model": model, "N": int(N), "batch": int(batch), "precision": prec,
                              "hbm_bytes_per_launch": res["traffic_bytes_per_launch"],
+                             "steps_per_launch": a.steps_per_launch,
+                             "hbm_bytes_per_step": res["traffic_bytes_per_launch"] / a.steps_per_launch,
                              "source": os.path.relpath(out, ROOT)})
         with open(path, "w") as fh:
             json.dump(d, fh, indent=1)
