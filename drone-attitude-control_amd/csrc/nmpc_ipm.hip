@@ -833,7 +833,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     factor(true);
                     // set steps -> dz, refinement corrections -> sg (dz and the flags in dza stay)
                     forward(Lsg, fref ? 0u : (unsigned)(Ldz - Lsg));
-                    T nbad = 0;
+                    T nbad = 0, nact = 0;
                     for (int e = ll; e < nel; e += G) {
                         const int k = e / NZ, i = e - k * NZ;
                         if ((k == N && i >= NX) || (k == 0 && i < NX)) continue;
@@ -859,16 +859,21 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             bad = rl || ru || al || au;
                             na = (rl || ru) ? T(0) : (al ? T(-1) : (au ? T(1) : a));
                             if (pol) S.st(Ldza, e, na);
+                            nact += na != T(0) ? T(1) : T(0);
                         }
                         nbad += bad ? T(1) : T(0);
                     }
                     nbad = group_sum<G>(nbad);
-                    bool done = false;
+                    nact = group_sum<G>(nact);
+                    bool done = false, done_ref = false;
                     if (pol) {
                         fin_steps++;
                         const bool okp = nbad == T(0) && !pfail;
                         if (fref) {
-                            done = okp;
+                            done = done_ref = okp;
+                            pol = false;
+                        } else if (okp && nact == T(0)) {
+                            done = true;   // no active bound: an unpenalised Newton step, nothing to refine
                             pol = false;
                         } else if (okp) {
                             fref = true;
@@ -886,7 +891,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                                 if (k == N && i >= NX) continue;
                                 const T lb = clb[stype(k) * LDZ + i], ub = cub[stype(k) * LDZ + i];
                                 T z = S.ld(Lz, e);
-                                if (!(k == 0 && i < NX)) z += S.ld(Ldz, e) + S.ld(Lsg, e);
+                                if (!(k == 0 && i < NX)) z += S.ld(Ldz, e) + (done_ref ? S.ld(Lsg, e) : T(0));
                                 z = has_bound(lb) ? fmax(z, lb) : z;
                                 z = has_bound(ub) ? fmin(z, ub) : z;
                                 if (i < NX) p.xout[((size_t)inst * (N + 1) + k) * NX + i] = z;

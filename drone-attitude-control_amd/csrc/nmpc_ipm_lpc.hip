@@ -794,6 +794,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         T na;
                         const T a = fin_flag(q.e, bk, fs0);
                         s_c += finish_check(my, q.e, bk, a, na);
+                        s_a += na != T(0) ? T(1) : T(0);   // active bounds of the next set
                         if (pol) {
                             if (fref) {
                                 stE(L::DZA, k, my);
@@ -835,6 +836,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     T na;
                     const T a = fin_flag(e, bnd(N), fs0);
                     s_c += finish_check(dx, e, bnd(N), a, na);
+                    s_a += na != T(0) ? T(1) : T(0);
                     if (pol) {
                         if (fref) {
                             stE(L::DZA, N, dx);
@@ -1188,8 +1190,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     pfail = false;
                     riccati(Pass<1>{});
                     pending = false;
-                    T d0, d1, d2, nbad;
-                    forward(Pass<2>{}, d0, d1, d2, nbad);
+                    T d0, nact, d2, nbad;
+                    forward(Pass<2>{}, d0, nact, d2, nbad);
                     if (pol) {
                         fin_steps++;
                         const bool okp = nbad == T(0) && !pfail;
@@ -1199,6 +1201,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                                 status = -1;
                                 iters = it + fin_steps;
                             }
+                            pol = false;
+                        } else if (okp && nact == T(0)) {
+                            // no active bound: an unpenalised Newton step, nothing to refine
+                            // (DZA holds the all-zero flags, the output adds nothing)
+                            active = false;
+                            status = -1;
+                            iters = it + fin_steps;
                             pol = false;
                         } else if (okp) {
                             fref = true;

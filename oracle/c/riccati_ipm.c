@@ -359,6 +359,20 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
                     }
                 }
             }
+            int nact = 0;
+            if (ok)
+                for (k = 0; k <= N; k++)
+                    for (i = 0; i < nz; i++) nact += w->act[k * nz + i] != 0;
+            if (ok && nact == 0) {
+                /* no active bound: the step solved the unconstrained Newton system (no penalty),
+                 * nothing to refine */
+                for (k = 0; k <= N; k++) {
+                    int n = k < N ? nz : nx;
+                    for (i = (k == 0 ? nx : 0); i < n; i++) Z(k, i) += w->dz[k * nz + i];
+                }
+                status = 0;
+                break;
+            }
             if (ok) {
                 /* refinement: the penalised solution z_a sits lambda / rho off its active bounds
                  * and carries the rounding of a rho-weighted solve; one more Newton step from z_a
