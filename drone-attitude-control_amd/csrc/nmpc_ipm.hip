@@ -387,6 +387,47 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                               : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
         const int yrow = fused ? p.cl.table_cols : p.ny;
         const T *x0 = (fused ? p.cl.state : p.x0) + (size_t)inst * NX;
+        // ------------------------------------------------------------------ infeasibility certificate
+        // interval reachability (oracle/c/riccati_ipm.c infeasible_stage): lane ll < nx carries the
+        // midpoint / radius of state ll of X_k, lanes nx.. the input box; an empty X_{k+1} (state
+        // box of stage k+1 included) proves the QP infeasible
+        bool infeas = false;
+        {
+            const int cl_ = ll < NZ ? ll : 0;
+            T cm = ll < NX ? x0[cl_] : T(0), cr = 0;
+            if (ll >= NX && ll < NZ) {
+                const T l = clb[cl_], h = cub[cl_];   // stage-0 input bounds
+                const bool bb = has_bound(l) && has_bound(h);
+                cm = bb ? T(0.5) * (l + h) : T(0);
+                cr = bb ? T(0.5) * (h - l) : T(INFINITY);
+            }
+            for (int k = 0; k < N; k++) {
+                if (ll < NZ) {
+                    sv[ll] = cm;
+                    hv[ll] = cr;
+                }
+                WAVE_SYNC();
+                T sm = cc[ll < NX ? ll : 0], sr = 0;
+#pragma unroll
+                for (int j = 0; j < NZ; j++) {
+                    const T a = cab[(ll < NX ? ll : 0) * LDZ + j];
+                    sm = fma(a, sv[j], sm);
+                    sr = a != T(0) ? fma(fabs(a), hv[j], sr) : sr;   // 0 x unbounded radius adds 0
+                }
+                const T l = clb[stype(k + 1) * LDZ + cl_], h = cub[stype(k + 1) * LDZ + cl_];
+                T lo = sm - sr, hi = sm + sr;
+                lo = has_bound(l) ? fmax(lo, l) : lo;
+                hi = has_bound(h) ? fmin(hi, h) : hi;
+                infeas |= ll < NX && lo > hi + T(1e-9) * (T(1) + fabs(hi));
+                const bool fin = isfinite(lo) && isfinite(hi);
+                WAVE_SYNC();
+                if (ll < NX) {
+                    cm = fin ? T(0.5) * (lo + hi) : sm;
+                    cr = fin ? T(0.5) * (hi - lo) : sr;
+                }
+            }
+            infeas = group_max<G>(infeas ? T(1) : T(0)) > T(0);
+        }
         // ------------------------------------------------------------------ initial point
         for (int e = ll; e < nel; e += G) {
             const int k = e / NZ, i = e % NZ;
@@ -452,8 +493,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 
         const T m_bounds = T(1) / p.inv_m;
         T theta = 1;
-        bool active = inst_ok;
-        int status = 2, iters = 0;
+        bool active = inst_ok && !infeas;
+        int status = infeas ? 4 : 2, iters = 0;   // certified infeasible: status 4, the initial point
         bool fail = false, pending = false;
         T alpha = 0, smu = 0;      // step and sigma*mu of the pending (lazily applied) update
         // exact finish (oracle/c/riccati_ipm.c "exact finish"; nmpc_ipm_lpc.hip): a primal-dual
@@ -847,16 +888,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         const bool vl = lam_l > T(0), vu = lam_u > T(0);
                         const T tl = T(1e-9) * (T(1) + fabs(lb)), tu = T(1e-9) * (T(1) + fabs(ub));
                         const bool lo = vl && zn < lb - tl, hi = vu && zn > ub + tu;
-                        bool bad;
+                        bool bad = !isfinite(zn);   // a non-finite step is never accepted
                         T na = a;
                         if (fref) {
-                            bad = fabs(dz) > T(1e-3) * (T(1) + fabs(z)) || (a < T(0) && fabs(zn - lb) > tl) ||
+                            bad |= !(fabs(dz) <= T(1e-3) * (T(1) + fabs(z))) || (a < T(0) && fabs(zn - lb) > tl) ||
                                   (a > T(0) && fabs(zn - ub) > tu) || (a == T(0) && (lo || hi));
                         } else {
                             const bool rl = a < T(0) && zn > fma(T(1e-15), T(1) + fabs(lb), lb);
                             const bool ru = a > T(0) && zn < fma(T(-1e-15), T(1) + fabs(ub), ub);
                             const bool al = a == T(0) && lo, au = a == T(0) && !lo && hi;
-                            bad = rl || ru || al || au;
+                            bad |= rl || ru || al || au;
                             na = (rl || ru) ? T(0) : (al ? T(-1) : (au ? T(1) : a));
                             if (pol) S.st(Ldza, e, na);
                             nact += na != T(0) ? T(1) : T(0);
@@ -1021,6 +1062,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 if (k == N && i >= NX) continue;
                 const T z = S.ld(Lz, e), lam_l = S.ld(Lll, e), lam_u = S.ld(Llu, e);
                 const T dz = S.ld(Ldz, e), dza = S.ld(Ldza, e);
+                C2 += dz * T(0);   // NaN for a non-finite direction (caught at the step below)
                 if (lam_l > T(0)) {
                     const T t = z - clb[stype(k) * LDZ + i], it_ = frcp(t);
                     const T dla = -lam_l * (T(1) + dza * it_);
@@ -1051,10 +1093,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // start of this iteration, like the oracle's early exit (oracle/c/riccati_ipm.c:222)
             if (active && !fail) {
                 // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
-                mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
-                theta *= (T(1) - a);
-                alpha = a;
-                pending = true;
+                const T mu_new = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
+                if (!isfinite(mu_new) || !isfinite(a)) {
+                    fail = true;   // non-finite direction: ends like a failed factorisation (iterate kept)
+                } else {
+                    mu = mu_new;
+                    theta *= (T(1) - a);
+                    alpha = a;
+                    pending = true;
+                }
             }
             NMPC_TICK(7);
         }

@@ -394,6 +394,45 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                               : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
         const int yrow = fused ? p.cl.table_cols : p.ny;
         const T *x0 = (fused ? p.cl.state : p.x0) + (size_t)inst * NX;
+        // ------------------------------------------------------------------ infeasibility certificate
+        // interval reachability (oracle/c/riccati_ipm.c infeasible_stage): x-lane r carries the
+        // midpoint / radius of state r of X_k, u-lanes the input box; X_{k+1} = hull([A B] X_k x U
+        // + c) meets the state box of stage k+1, an empty intersection proves the QP infeasible
+        bool infeas = false;
+        {
+            T cm = xl ? x0[r] : T(0), cr = 0;
+            if (ul) {
+                const T l = LB(0), h = UB(0);
+                const bool bb = has_bound(l) && has_bound(h);
+                cm = bb ? T(0.5) * (l + h) : T(0);
+                cr = bb ? T(0.5) * (h - l) : T(INFINITY);
+            }
+            T *rad = gb + Gm::G_MT;
+            for (int k = 0; k < N; k++) {
+                zb[r] = cm;
+                rad[r] = cr;
+                LPC_SYNC();
+                T sm = c_r, sr = 0;
+#pragma unroll
+                for (int j = 0; j < NZ; j++) {
+                    const T a = abr[(xl ? r : 0) * LDZ + j];
+                    sm = fma(a, zb[j], sm);
+                    sr = a != T(0) ? fma(fabs(a), rad[j], sr) : sr;   // 0 x unbounded radius adds 0
+                }
+                const T l = LB(k + 1), h = UB(k + 1);
+                T lo = sm - sr, hi = sm + sr;
+                lo = has_bound(l) ? fmax(lo, l) : lo;
+                hi = has_bound(h) ? fmin(hi, h) : hi;
+                infeas |= xl && lo > hi + T(1e-9) * (T(1) + fabs(hi));
+                const bool fin = isfinite(lo) && isfinite(hi);
+                LPC_SYNC();
+                if (xl) {
+                    cm = fin ? T(0.5) * (lo + hi) : sm;
+                    cr = fin ? T(0.5) * (hi - lo) : sr;
+                }
+            }
+            infeas = gmax(infeas ? T(1) : T(0)) > T(0);
+        }
         // ------------------------------------------------------------------ initial point
         T r0 = 0, mu = 0, abz = 0;
         for (int k = 0; k <= N; k++) {
@@ -460,8 +499,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 
         const T m_bounds = T(1) / p.inv_m;
         T theta = 1;
-        bool active = inst_ok;
-        int status = 2, iters = 0;
+        bool active = inst_ok && !infeas;
+        int status = infeas ? 4 : 2, iters = 0;   // certified infeasible: status 4, the initial point
         bool fail = false, pending = false;
         T alpha = 0, smu = 0;
         // exact finish (oracle/c/riccati_ipm.c "exact finish"): a primal-dual active-set run of at
@@ -548,16 +587,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             const T zn = q.z + dz;
             const T tl = T(1e-9) * (T(1) + fabs(b.lb)), tu = T(1e-9) * (T(1) + fabs(b.ub));
             const bool lo = vl && zn < b.lb - tl, hi = vu && zn > b.ub + tu;
-            bool bad;
+            bool bad = !isfinite(zn);   // a non-finite step is never accepted
             if (fref) {
-                bad = fabs(dz) > T(1e-3) * (T(1) + fabs(q.z)) || (a < T(0) && fabs(zn - b.lb) > tl) ||
+                bad |= !(fabs(dz) <= T(1e-3) * (T(1) + fabs(q.z))) || (a < T(0) && fabs(zn - b.lb) > tl) ||
                       (a > T(0) && fabs(zn - b.ub) > tu) || (a == T(0) && (lo || hi));
                 na = a;
             } else {
                 const bool rl = a < T(0) && zn > fma(T(1e-15), T(1) + fabs(b.lb), b.lb);
                 const bool ru = a > T(0) && zn < fma(T(-1e-15), T(1) + fabs(b.ub), b.ub);
                 const bool al = a == T(0) && lo, au = a == T(0) && !lo && hi;
-                bad = rl || ru || al || au;
+                bad |= rl || ru || al || au;
                 na = (rl || ru) ? T(0) : (al ? T(-1) : (au ? T(1) : a));
             }
             return bad ? T(1) : T(0);
@@ -661,7 +700,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     c = (vu && dlu < T(0)) ? fmin(c, -q.lu * rcp_raw(dlu)) : c;
                     s_a += (vl ? q.ll * tl : T(0)) + (vu ? q.lu * tu : T(0));
                     s_b += (vl ? dlal * dza : T(0)) - (vu ? dlau * dza : T(0));
-                    s_c += (vl ? dll * dz : T(0)) - (vu ? dlu * dz : T(0));
+                    // + dz * 0: NaN for a non-finite direction (caught at the step below)
+                    s_c += (vl ? dll * dz : T(0)) - (vu ? dlu * dz : T(0)) + dz * T(0);
                 }
                 s_min = corr ? fmin(s_min, c) : fmax(s_min, c);
             };
@@ -1340,10 +1380,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // start of this iteration, like the oracle's early exit (oracle/c/riccati_ipm.c:222)
             if (active && !fail) {
                 // m mu_new = (1 - a) S0 + a (m smu - C1) + a^2 C2
-                mu = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
-                theta *= (T(1) - a);
-                alpha = a;
-                pending = true;
+                const T mu_new = ((T(1) - a) * T0 + a * (smu * m_bounds - C1) + a * a * C2) * p.inv_m;
+                if (!isfinite(mu_new) || !isfinite(a)) {
+                    fail = true;   // non-finite direction: ends like a failed factorisation (iterate kept)
+                } else {
+                    mu = mu_new;
+                    theta *= (T(1) - a);
+                    alpha = a;
+                    pending = true;
+                }
             }
         }
 

@@ -179,6 +179,51 @@ static int backward(const ocp_ref_desc *d, ws_t *w, const double *gr)
     return 0;
 }
 
+/* Infeasibility certificate (interval reachability): X_0 = {x0}; X_{k+1} = hull([A B] (X_k x U_k)
+ * + c) intersected with the state box of stage k+1, in midpoint / radius form. The hull
+ * over-approximates the reachable set, so an empty X_{k+1} proves that no input sequence keeps the
+ * states inside their boxes: the QP is infeasible (typically a closed-loop state pushed past a
+ * position bound with the velocity still pointing out). Returns the first empty stage, 0 if none
+ * (which proves nothing). Tolerance 1e-9 relative on the emptiness test. */
+static int infeasible_stage(const ocp_ref_desc *d, const double *x0)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N;
+    double m[NZMAX], r[NZMAX], mn[NZMAX], rn[NZMAX], mu[NZMAX], ru[NZMAX];
+    for (int j = 0; j < nu; j++) {
+        const double l = d->lb0[nx + j], u = d->ub0[nx + j];   /* input boxes are stage-invariant */
+        mu[j] = has(l) && has(u) ? 0.5 * (l + u) : 0.0;
+        ru[j] = has(l) && has(u) ? 0.5 * (u - l) : INFINITY;
+    }
+    for (int i = 0; i < nx; i++) { m[i] = x0[i]; r[i] = 0.0; }
+    for (int k = 0; k < N; k++) {
+        for (int i = 0; i < nx; i++) {
+            double s = d->c[i], t = 0.0;
+            for (int j = 0; j < nx; j++) {
+                const double a = d->A[i * nx + j];
+                s += a * m[j];
+                if (a != 0.0) t += fabs(a) * r[j];   /* (a zero entry times an unbounded radius adds 0) */
+            }
+            for (int j = 0; j < nu; j++) {
+                const double b = d->B[i * nu + j];
+                s += b * mu[j];
+                if (b != 0.0) t += fabs(b) * ru[j];
+            }
+            mn[i] = s;
+            rn[i] = t;
+        }
+        for (int i = 0; i < nx; i++) {
+            const double lb = k + 1 == N ? d->lbe[i] : d->lb[i], ub = k + 1 == N ? d->ube[i] : d->ub[i];
+            double lo = mn[i] - rn[i], hi = mn[i] + rn[i];
+            if (has(lb) && lb > lo) lo = lb;
+            if (has(ub) && ub < hi) hi = ub;
+            if (lo > hi + 1e-9 * (1.0 + fabs(hi))) return k + 1;
+            if (isfinite(lo) && isfinite(hi)) { m[i] = 0.5 * (lo + hi); r[i] = 0.5 * (hi - lo); }
+            else { m[i] = mn[i]; r[i] = rn[i]; }
+        }
+    }
+    return 0;
+}
+
 static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref,
                      double *xo, double *uo, int *iters_out, ws_t *w)
 {
@@ -260,6 +305,9 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
     for (i = 0; i < nz * nz; i += nz + 1) rho = fmax(rho, fabs(d->H[i]));
     for (i = 0; i < nx * nx; i += nx + 1) rho = fmax(rho, fabs(d->He[i]));
     rho *= POLISH_RHO;
+    it = 0;
+    /* a certified-infeasible QP ends before the first iteration: status 4, the initial point */
+    if (infeasible_stage(d, x0)) { status = 4; goto done; }
 
     /* ---- forward substitution: direction into out[] ---- */
 #define FORWARD(out) do { \
@@ -283,16 +331,18 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
     } while (0)
     for (it = 0; it < d->max_iter; it++) {
         /* complementarity measure */
-        double mu = 0.0;
+        double mu = 0.0, zs = 0.0;
         for (k = 0; k <= N; k++) {
             int n = k < N ? nz : nx;
             for (i = 0; i < n; i++) {
                 if (LL(k, i) > 0.0) mu += LL(k, i) * (Z(k, i) - LBk(d, k, i));
                 if (LU(k, i) > 0.0) mu += LU(k, i) * (UBk(d, k, i) - Z(k, i));
+                zs += Z(k, i) + LL(k, i) + LU(k, i);
             }
         }
         mu /= m;
-        if (!isfinite(mu) || !isfinite(theta)) { status = 4; break; }
+        /* non-finite iterate (a multiplier of a NaN drops out of mu): QP failure */
+        if (!isfinite(mu) || !isfinite(theta) || !isfinite(zs)) { status = 4; break; }
         if (mu <= d->tol_comp && theta * r0 <= d->tol_res) { status = 0; break; }
 
         /* objective gradient gf, dynamics residual re */
@@ -347,6 +397,7 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
                     for (i = (k == 0 ? nx : 0); i < n; i++) {
                         const double zn = Z(k, i) + w->dz[k * nz + i], lbv = LBk(d, k, i), ubv = UBk(d, k, i);
                         signed char *a = &w->act[k * nz + i];
+                        if (!isfinite(zn)) ok = 0;   /* a non-finite step is never accepted */
                         if (*a < 0) {
                             if (zn > lbv + POLISH_TOL_ACTIVE * (1.0 + fabs(lbv))) { ok = 0; *a = 0; }
                         } else if (*a > 0) {
@@ -416,7 +467,7 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
                             const double lbv = LBk(d, k, i), ubv = UBk(d, k, i);
                             const signed char a = w->act[k * nz + i];
                             const double tl = POLISH_TOL * (1.0 + fabs(lbv)), tu = POLISH_TOL * (1.0 + fabs(ubv));
-                            if (fabs(w->dz[k * nz + i]) > POLISH_TOL_REFINE * (1.0 + fabs(za)) ||
+                            if (!(fabs(w->dz[k * nz + i]) <= POLISH_TOL_REFINE * (1.0 + fabs(za))) ||
                                 (a < 0 && fabs(zr - lbv) > tl) || (a > 0 && fabs(zr - ubv) > tu) ||
                                 (!a && has(lbv) && zr < lbv - tl) || (!a && has(ubv) && zr > ubv + tu)) {
                                 ok = 0;
@@ -563,6 +614,13 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
         }
         alpha *= 0.995;
         if (alpha > 1.0) alpha = 1.0;
+        {
+            /* a non-finite direction ends the solve like a failed factorisation (iterate kept) */
+            double nf = 0.0;
+            for (k = 0; k <= N; k++)
+                for (i = 0; i < (k < N ? nz : nx); i++) nf += w->dz[k * nz + i] * 0.0;
+            if (!isfinite(alpha) || !isfinite(nf)) { status = 4; goto done; }
+        }
         for (k = 0; k <= N; k++) {
             int n = k < N ? nz : nx;
             for (i = (k == 0 ? nx : 0); i < n; i++) {

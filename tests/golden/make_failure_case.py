@@ -3,8 +3,10 @@
 Input: gpurun_out/fail.npz from `python tools/fail_diag.py --model jerk --batch 4096` (GPU
 closed loop, seed 42): the first instance whose solve returned status 4. Its x0 (the plant
 state after 18 noisy closed-loop steps, px = 1.1992 against the 1.2 position bound) and yref
-window are stored together with the C oracle's answer (oracle/c/riccati_ipm.c): status 4 when
-F_uu loses positive definiteness, the iterate as it stood at the start of that iteration.
+window are stored together with the C oracle's answer (oracle/c/riccati_ipm.c): status 4 — since
+round 2 from the interval infeasibility certificate before the first iteration (x_1 cannot meet
+the position bound), with the initial point as the iterate; before, F_uu lost positive
+definiteness at iteration 9.
 
     python tests/golden/make_failure_case.py [gpurun_out/fail.npz]
     python tests/golden/make_failure_case.py --refresh   # same inputs, the current oracle's answer

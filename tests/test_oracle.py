@@ -230,7 +230,8 @@ def test_converters_and_plant():
 
 def test_factorisation_failure_fixture(golden_dir):
     """tests/golden/qp_failure.npz: the C oracle still stops with status 4 after the recorded
-    number of iterations and returns the recorded (finite) iterate."""
+    number of iterations (0: the interval certificate proves the QP infeasible before the first
+    iteration) and returns the recorded (finite) iterate."""
     from oracle import cref, models
     f = np.load(os.path.join(golden_dir, "qp_failure.npz"))
     R = cref.RiccatiIpmRef(models.MODELS["jerk"](40))
