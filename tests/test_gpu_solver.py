@@ -381,3 +381,33 @@ def test_factorisation_failure_keeps_last_iterate(kernel, cases, golden_dir):
     assert np.isfinite(X).all() and np.isfinite(U).all()
     assert rel_err(X[:1], U[:1], f[key + "_X"], f[key + "_U"]).max() < TOL64
     assert rel_err(X[1:], U[1:], cases[key + "_X"][:3], cases[key + "_U"][:3]).max() < TOL64
+
+
+@pytest.mark.parametrize("kernel", ["lpc", "wave"])
+@pytest.mark.parametrize("name,N", [("jerk", 40), ("quad13", 20)])
+def test_infeasibility_certificate_on_gpu(kernel, name, N, golden_dir):
+    """Closed-loop QPs past a position bound (tests/golden/qp_infeasible.npz): the kernels' interval
+    certificate ends them before the first iteration — status 4, 0 iterations, the oracle's
+    initial point — next to feasible instances of the same launch that solve normally."""
+    f = np.load(os.path.join(golden_dir, "qp_infeasible.npz"))
+    d = np.load(os.path.join(golden_dir, "qp_cases.npz"))
+    key = f"{name}_N{N}"
+    gkey = key if key + "_x0" in d else f"{name}_N30"
+    n = f[key + "_x0"].shape[0]
+    x0 = np.vstack([f[key + "_x0"], d[gkey + "_x0"][:3]]) if gkey == key else f[key + "_x0"]
+    y = np.vstack([f[key + "_yref"], d[gkey + "_yref"][:3]]) if gkey == key else f[key + "_yref"]
+    os.environ["NMPC_KERNEL"] = kernel
+    try:
+        s = AcadosOcpSolver(OCPS[name](N), batch=x0.shape[0])
+    finally:
+        os.environ.pop("NMPC_KERNEL", None)
+    s.set_batch("x0", x0)
+    s.set_batch("yref", y)
+    s.solve()
+    st, it = s.get_batch_int("status"), s.get_batch_int("qp_iter")
+    assert (st[:n] == 4).all() and (it[:n] == 0).all(), (st, it)
+    X, U = s.get_batch("x"), s.get_batch("u")
+    assert rel_err(X[:n], U[:n], f[key + "_X"], f[key + "_U"]).max() < 1e-12
+    if gkey == key:
+        assert (st[n:] == 0).all()
+        assert rel_err(X[n:], U[n:], d[key + "_X"][:3], d[key + "_U"][:3]).max() < TOL64

@@ -239,3 +239,22 @@ def test_factorisation_failure_fixture(golden_dir):
     assert st[0] == 4 and it[0] == f["jerk_N40_iters"][0]
     assert np.isfinite(X).all() and np.isfinite(U).all()
     assert np.array_equal(X, f["jerk_N40_X"]) and np.array_equal(U, f["jerk_N40_U"])
+
+
+def test_infeasibility_certificate(golden_dir):
+    """The interval-reachability certificate (oracle/c/riccati_ipm.c infeasible_stage): the
+    recorded closed-loop QPs past a position bound end before the first iteration with status 4
+    and the initial point (tests/golden/qp_infeasible.npz); no golden or bench-sample QP (all
+    feasible, certified by the dense oracle) is ever flagged."""
+    f = np.load(os.path.join(golden_dir, "qp_infeasible.npz"))
+    for name, N in [("jerk", 40), ("quad13", 20)]:
+        key = f"{name}_N{N}"
+        X, U, st, it = cref.RiccatiIpmRef(models.MODELS[name](N)).solve(f[key + "_x0"], f[key + "_yref"])
+        assert len(st) > 0 and (st == 4).all() and (it == 0).all()
+        assert np.array_equal(X, f[key + "_X"]) and np.array_equal(U, f[key + "_U"])
+        assert np.isfinite(X).all() and np.isfinite(U).all()
+    d = np.load(os.path.join(golden_dir, "qp_cases.npz"))
+    for key in ("force_N20", "force_N30", "jerk_N30", "jerk_N40", "quad13_N20"):
+        name, N = key.split("_N")
+        _, _, st, it = cref.RiccatiIpmRef(models.MODELS[name](int(N))).solve(d[key + "_x0"], d[key + "_yref"])
+        assert (st == 0).all() and (it > 0).all()
