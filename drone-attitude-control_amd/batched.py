@@ -152,6 +152,17 @@ class ClosedLoop:
             raise NmpcError(f"nmpc_closed_loop_instance_stats: {self.lib.nmpc_last_error(self.solver._h).decode()}")
         return out
 
+    def iter_log(self):
+        """Per-step solve record of the last fused launch (env NMPC_ITER_LOG set before the run):
+        (finish steps, IPM iterations, status), each [steps, batch]."""
+        steps = int(self.stats()["steps"])
+        buf = np.zeros((min(steps, 64), self.batch), dtype=np.int32)
+        rc = self.lib.nmpc_closed_loop_iter_log(self.solver._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                buf.size)
+        if rc < 0:
+            raise NmpcError(f"nmpc_closed_loop_iter_log: {self.lib.nmpc_last_error(self.solver._h).decode()}")
+        return buf & 0xFF, (buf >> 8) & 0xFF, buf >> 16
+
     def state(self):
         out = np.zeros((self.batch, self.solver.nx))
         rc = self.lib.nmpc_closed_loop_get_state(self.solver._h, _lib.dptr(out), out.size)

@@ -195,8 +195,8 @@ struct nmpc_solver {
     int kidx = -1, ipw = 1, wpb = 1, lds = 0, yref_is_z = 0;
     int max_iter = 50;
     double tol_comp = 0, tol_res = 0, mu0 = 0, inv_m = 1, ts = 0, scale_e = 1;
-    double polish_mu = 0, polish_rho = 0;
-    int polish_steps = 12;
+    double polish_mu = 0, polish_rho = 0, polish_drop = 0.01;
+    int polish_steps = 12, polish_first = 12;
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
@@ -222,6 +222,8 @@ struct nmpc_solver {
     double *d_acc = nullptr, *d_noise = nullptr;
     int cl_step = 0, cl_last_launches = 0, cl_last_steps = 0;
     double *d_fnoise = nullptr;   // fused closed loop: noise draws of a launch's steps [B][64]
+    int *d_iter_log = nullptr;    // fused closed loop, env NMPC_ITER_LOG: per-step finish steps | IPM iterations << 8 | status << 16 [64][B]
+    int iter_log_steps = 0;       // steps in the log (the last fused launch)
     std::vector<hipEvent_t> cl_events;
     double cl_last_ms = 0.0;
     double cost_s = 1.0;  // stage cost factor (time step or 1)
@@ -258,7 +260,7 @@ void free_all(nmpc_solver *h)
     for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
                     (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
-                    (void *)h->d_fnoise})
+                    (void *)h->d_fnoise, (void *)h->d_iter_log})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -329,6 +331,8 @@ int launch_cond(nmpc_solver *h, hipEvent_t e0, hipEvent_t e1)
 template <typename T>
 nmpc::ClParams<T> cl_params(nmpc_solver *h);
 
+constexpr int CL_FUSED_CHUNK = 64;   // closed-loop steps per fused solve launch
+
 // cl_steps > 0: fused closed loop of that many steps (lane-per-component / wavefront kernels)
 template <typename T>
 int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0)
@@ -339,6 +343,12 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     if (cl_steps > 0) {
         p.cl = cl_params<T>(h);
         p.cl_noise = h->d_fnoise;
+        static const bool iter_log = std::getenv("NMPC_ITER_LOG") != nullptr;
+        if (iter_log && !h->d_iter_log &&
+            hipMalloc((void **)&h->d_iter_log, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(int)) != hipSuccess)
+            h->d_iter_log = nullptr;
+        p.iter_log = iter_log ? h->d_iter_log : nullptr;
+        h->iter_log_steps = p.iter_log ? cl_steps : 0;
     }
     p.B = h->batch;
     p.N = h->N;
@@ -353,6 +363,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.polish_mu = (T)h->polish_mu;
     p.polish_rho = (T)h->polish_rho;
     p.polish_steps = h->polish_steps;
+    p.polish_first = h->polish_first;
+    p.polish_drop = (T)h->polish_drop;
     const char *m = (const char *)h->d_model;
     p.AB = (const T *)(m + h->off_AB);
     p.ABt = (const T *)(m + h->off_ABt);
@@ -626,6 +638,12 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     // largest cost curvature, as in oracle/c/riccati_ipm.c (POLISH_RHO)
     h->polish_mu = !f64 || d->qp_solver_polish_mu < 0 ? 0.0 : (d->qp_solver_polish_mu > 0 ? d->qp_solver_polish_mu : 1.0);
     h->polish_steps = d->qp_solver_polish_steps > 0 ? d->qp_solver_polish_steps : 12;
+    h->polish_first = h->polish_steps;
+    // tuning overrides (experiments only): set steps of later / first finish runs, mu drop between runs
+    if (const char *e = std::getenv("NMPC_POLISH_STEPS")) h->polish_steps = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("NMPC_POLISH_FIRST")) h->polish_first = std::max(1, std::atoi(e));
+    else h->polish_first = h->polish_steps;
+    if (const char *e = std::getenv("NMPC_POLISH_DROP")) h->polish_drop = std::atof(e);
     {
         double hmax = 1.0;
         for (int i = 0; i < nz; i++) hmax = std::max(hmax, std::fabs(h->H[i * nz + i]));
@@ -1149,8 +1167,6 @@ bool cl_fused(nmpc_solver *h)
     return kind == 0 || kind == 1;
 }
 
-constexpr int CL_FUSED_CHUNK = 64;
-
 template <typename T>
 int cl_fused_enqueue(nmpc_solver *h, int launch_idx, int n)
 {
@@ -1318,6 +1334,20 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
     v[7] = h->cl_last_steps;
     for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
     return 0;
+}
+
+int nmpc_closed_loop_iter_log(nmpc_solver *h, int32_t *out, size_t count)
+{
+    if (!h || !out) return NMPC_EINVAL;
+    if (!h->d_iter_log || h->iter_log_steps <= 0)
+        return h->fail(NMPC_ESTATE, "nmpc_closed_loop_iter_log: no log (set NMPC_ITER_LOG and run a fused closed loop)");
+    const size_t n = (size_t)h->iter_log_steps * h->batch;
+    if (count != n) return h->fail(NMPC_EINVAL, "nmpc_closed_loop_iter_log: needs steps*batch values");
+    hipSetDevice(h->device);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, h->d_iter_log, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_iter_log");
+    return (int)h->iter_log_steps;
 }
 
 int nmpc_closed_loop_instance_stats(nmpc_solver *h, double *out, size_t count)

@@ -47,6 +47,8 @@ struct IpmParams {
     T polish_mu;    // exact finish threshold (0: off)
     T polish_rho;   // penalty on the identified active bounds in the finish
     int polish_steps;   // active-set Newton steps per finish run
+    int polish_first;   // ... in the first run of a solve (the warm-started one in the closed loop)
+    T polish_drop;      // after a rejected run the next one waits for mu <= polish_drop * mu
     const T *AB;    // [nx][nx+nu]   discrete [A B], row-major
     const T *ABt;   // [nx+nu][nx]   its transpose
     const T *c;     // [nx]
@@ -72,6 +74,7 @@ struct IpmParams {
     int cl_steps;
     ClParams<T> cl;
     const double *cl_noise;   // [B][cl_steps] noise draws of the launch's steps (cl_noise_launch)
+    int *iter_log;            // optional [cl_steps][B]: finish steps | IPM iterations << 8 | status << 16 per fused step
 };
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);

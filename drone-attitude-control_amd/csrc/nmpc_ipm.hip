@@ -73,6 +73,13 @@ namespace nmpc {
         __builtin_amdgcn_wave_barrier();                         \
     } while (0)
 
+// LDS maximum of a non-negative value (its bit pattern orders like an unsigned integer)
+__device__ __forceinline__ void lds_max(double *p, double v)
+{
+    atomicMax((unsigned long long *)p, (unsigned long long)__double_as_longlong(v));
+}
+__device__ __forceinline__ void lds_max(float *p, float v) { atomicMax((unsigned int *)p, __float_as_uint(v)); }
+
 template <int G, typename T>
 __device__ __forceinline__ T group_sum(T v)
 {
@@ -245,7 +252,9 @@ struct Geometry {
     // the elementwise phase E_A (ZW elements)
     static constexpr int I_FP = 0, I_MT = I_FP + NZ * LDZ, I_RV = I_MT + NZ * LDX, I_SV = I_RV + LDX,
                          I_VV = I_SV + LDZ, I_HV = I_VV + LDX, I_PV = I_HV + LDZ, I_GV = I_PV + LDX,
-                         I_DX = I_GV + LDZ, I_DU = I_DX + 2 * LDX, I_TOT = I_DU + LDU;
+                         I_DX = I_GV + LDZ, I_DU = I_DX + 2 * LDX, I_CM = I_DU + LDU, I_TOT = I_CM + 2 * LDX;
+    // I_CM: exact finish, largest violation of each state component's add candidates (two buffers:
+    // the previous set step's, read by this step's flags, and this step's)
     // symmetric stage matrices are computed as lower triangles: column c owns rows c..n-1 in
     // chunks of E consecutive rows, one chunk per lane, E the smallest that fits G lanes
     static constexpr int tri_lanes(int n, int E)
@@ -503,13 +512,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // During a run dz holds the set step, dza the active flags (-1 lower, 1 upper, 0) and sg the
         // refinement's correction; a group the finish completes writes its outputs at once (status -1)
         T polish_at = p.polish_mu;
-        int fin_steps = 0;
+        int fin_steps = 0, fin_runs = 0;
         bool pol = false, fref = false, fs0 = false;
         // fused closed loop after its first step: the first finish run of a solve starts from the
         // previous step's active set shifted by one stage (act array; a warm start, the acceptance
         // tests are unchanged)
         const bool warm = fused && (cstep > 0 || p.cl.step > 0);
         bool fwarm = false;
+        // PDAS update (oracle/c/riccati_ipm.c pdas_update): a violated inactive state bound is an add
+        // candidate (flag +-(2 + violation)); it joins in the next step if it is its component's most
+        // violated one (cmax buffer cmb) and the step that found it was the run's first or had no removals
+        int cmb = 0;
+        bool addok = false;
         // the solution's active flag of an element (z on a bound to 1e-7): the warm start's input
         auto act_flag = [&](T z, T lb, T ub) {
             const bool onl = has_bound(lb) && z <= lb + T(1e-7) * (T(1) + fabs(lb));
@@ -624,7 +638,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     const T a = S.ld(Lact, (unsigned)(ks * NZ + i));
                     return (a < T(-0.5) && lam_l > T(0)) ? T(-1) : ((a > T(0.5) && lam_u > T(0)) ? T(1) : T(0));
                 }
-                if (!fs0) return S.ld(Ldza, e);
+                if (!fs0) {
+                    const T f = S.ld(Ldza, e);
+                    if (!(fabs(f) > T(1.5))) return f;
+                    const T *cmo = w + Gm::I_CM + cmb * Gm::LDX;
+                    return (addok && fabs(f) - T(2) == cmo[i]) ? (f < T(0) ? T(-1) : T(1)) : T(0);
+                }
                 const bool al = lam_l > T(0) && lam_l > z - lb, au = !al && lam_u > T(0) && lam_u > ub - z;
                 return al ? T(-1) : (au ? T(1) : T(0));
             };
@@ -865,16 +884,21 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // with this iteration from their untouched IPM iterate
             pol = active && p.polish_mu > T(0) && mu <= polish_at && !prev_failed;
             if (__any(pol)) {
-                polish_at = pol ? fmin(polish_at, mu) * T(0.01) : polish_at;
+                polish_at = pol ? fmin(polish_at, mu) * p.polish_drop : polish_at;
+                const int plim = fin_runs == 0 ? p.polish_first : p.polish_steps;   // set steps of this run
+                fin_runs += pol ? 1 : 0;
                 fref = false;
-                for (int fs = 0; fs <= p.polish_steps; fs++) {
+                for (int fs = 0; fs <= (p.polish_first > p.polish_steps ? p.polish_first : p.polish_steps); fs++) {
                     fs0 = fs == 0;
                     fwarm = warm && fs0 && it == 0;
                     pfail = false;
                     factor(true);
                     // set steps -> dz, refinement corrections -> sg (dz and the flags in dza stay)
                     forward(Lsg, fref ? 0u : (unsigned)(Ldz - Lsg));
-                    T nbad = 0, nact = 0;
+                    T nbad = 0, nact = 0, nrem = 0;
+                    T *cmn = w + Gm::I_CM + (1 - cmb) * Gm::LDX;   // this step's candidate maxima
+                    if (ll < NX) cmn[ll] = T(0);
+                    WAVE_SYNC();
                     for (int e = ll; e < nel; e += G) {
                         const int k = e / NZ, i = e - k * NZ;
                         if ((k == N && i >= NX) || (k == 0 && i < NX)) continue;
@@ -898,14 +922,22 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             const bool ru = a > T(0) && zn < fma(T(-1e-15), T(1) + fabs(ub), ub);
                             const bool al = a == T(0) && lo, au = a == T(0) && !lo && hi;
                             bad |= rl || ru || al || au;
-                            na = (rl || ru) ? T(0) : (al ? T(-1) : (au ? T(1) : a));
+                            // inputs join at once, states as candidates +-(2 + violation)
+                            const T cv = i < NX ? T(2) + (al ? lb - zn : zn - ub) : T(1);
+                            na = (rl || ru) ? T(0) : (al ? -cv : (au ? cv : a));
+                            if (i < NX && (al || au)) lds_max(&cmn[i], cv - T(2));
                             if (pol) S.st(Ldza, e, na);
                             nact += na != T(0) ? T(1) : T(0);
+                            nrem += (rl || ru) ? T(1) : T(0);
                         }
                         nbad += bad ? T(1) : T(0);
                     }
                     nbad = group_sum<G>(nbad);
                     nact = group_sum<G>(nact);
+                    nrem = group_sum<G>(nrem);
+                    addok = fs0 || nrem == T(0);
+                    cmb = 1 - cmb;
+                    WAVE_SYNC();
                     bool done = false, done_ref = false;
                     if (pol) {
                         fin_steps++;
@@ -918,7 +950,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             pol = false;
                         } else if (okp) {
                             fref = true;
-                        } else if (pfail || fs + 1 >= p.polish_steps) {
+                        } else if (pfail || fs + 1 >= plim) {
                             pol = false;
                         }
                     }
@@ -1123,6 +1155,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             if (ll == 0) {
                 p.status[inst] = status < 0 ? 0 : status;
                 p.iters[inst] = iters;
+                if (fused && p.iter_log)   // finish steps | IPM iterations << 8 | status << 16
+                    p.iter_log[(size_t)cstep * p.B + inst] = fin_steps | ((iters - fin_steps) << 8) | ((status < 0 ? 0 : status) << 16);
 #ifdef NMPC_SWEEP_TIMING
                 if (timed) {
                     unsigned long long *c = p.cycles + (size_t)inst * 9;

@@ -511,7 +511,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // its correction. status -1: completed by the finish, outputs = Z + DZ + DZA (B and D skip
         // the group's DZA / DZ)
         T polish_at = p.polish_mu;
-        int fin_steps = 0;
+        int fin_steps = 0, fin_runs = 0;
         bool pol = false, fref = false;
         bool fs0 = false;   // wave-uniform: the current finish pass is the first step of its runs
     // fused closed loop after its first step: the first finish run of a solve starts from the
@@ -565,12 +565,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // Branch-free; q.z becomes the step's base point.
         // active flag of a finish step from the dza slot (flags of the run, or the warm-start flags,
         // kept to bounds the element has), or from the multipliers at the first step of a cold run
-        auto fin_flag = [&](const El &q, const Bd &b, bool first) {
+        // an add candidate (flag +-2, a violated inactive state bound of the previous set step) joins
+        // only if it is its component's most violated stage (addk) — see the PDAS update in forward()
+        int addk = -1;
+        auto fin_flag = [&](const El &q, const Bd &b, bool first, int k) {
             if (first && !fwarm) return finish_rule(q, b);
-            return (q.dza < T(-0.5) && q.ll > T(0)) ? T(-1) : ((q.dza > T(0.5) && q.lu > T(0)) ? T(1) : T(0));
+            const bool cand = fabs(q.dza) > T(1.5);
+            const T f = cand && k != addk ? T(0) : q.dza;
+            return (f < T(-0.5) && q.ll > T(0)) ? T(-1) : ((f > T(0.5) && q.lu > T(0)) ? T(1) : T(0));
         };
-        auto finish_terms = [&](El &q, const Bd &b, bool fs0, T &sg, T &gadd) {
-            const T a = fin_flag(q, b, fs0);
+        auto finish_terms = [&](El &q, const Bd &b, bool fs0, int k, T &sg, T &gadd) {
+            const T a = fin_flag(q, b, fs0, k);
             q.z = fref ? q.z + q.dz : q.z;
             const T rho = p.polish_rho;
             sg = a != T(0) ? rho : T(0);
@@ -579,10 +584,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // acceptance tests of a finish step at element (k, r) (the oracle's POLISH_TOL_*): q.z is the
         // step's base, dz the step, a the active flag it used. A set step: active bounds keep a
         // non-negative multiplier rho (bound - z_new) (to a few ulps), inactive ones hold (to 1e-9);
-        // the next active set (na) drops the first and adds the second kind of violation. The
-        // refinement: the correction stays below 1e-3 (1 + |z|) and the refined point sits on its
-        // active bounds and inside the others to 1e-9. Returns 1 for a violated test.
-        auto finish_check = [&](T dz, const El &q, const Bd &b, T a, T &na) {
+        // the next active set (na) drops the first kind (rem) and marks the second as add candidates
+        // (flag +-2, violation viol). The refinement: the correction stays below 1e-3 (1 + |z|) and
+        // the refined point sits on its active bounds and inside the others to 1e-9. Returns 1 for a
+        // violated test.
+        auto finish_check = [&](T dz, const El &q, const Bd &b, T a, T &na, T &viol, bool &rem) {
             const bool vl = q.ll > T(0), vu = q.lu > T(0);
             const T zn = q.z + dz;
             const T tl = T(1e-9) * (T(1) + fabs(b.lb)), tu = T(1e-9) * (T(1) + fabs(b.ub));
@@ -592,12 +598,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 bad |= !(fabs(dz) <= T(1e-3) * (T(1) + fabs(q.z))) || (a < T(0) && fabs(zn - b.lb) > tl) ||
                       (a > T(0) && fabs(zn - b.ub) > tu) || (a == T(0) && (lo || hi));
                 na = a;
+                viol = 0;
+                rem = false;
             } else {
                 const bool rl = a < T(0) && zn > fma(T(1e-15), T(1) + fabs(b.lb), b.lb);
                 const bool ru = a > T(0) && zn < fma(T(-1e-15), T(1) + fabs(b.ub), b.ub);
                 const bool al = a == T(0) && lo, au = a == T(0) && !lo && hi;
                 bad |= rl || ru || al || au;
-                na = (rl || ru) ? T(0) : (al ? T(-1) : (au ? T(1) : a));
+                // inputs join at once, states as candidates (+-2, PDAS update in forward())
+                const T add = xl ? T(2) : T(1);
+                na = (rl || ru) ? T(0) : (al ? -add : (au ? add : a));
+                viol = !xl ? T(0) : (al ? b.lb - zn : (au ? zn - b.ub : T(0)));
+                rem = rl || ru;
             }
             return bad ? T(1) : T(0);
         };
@@ -727,6 +739,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 q.c0 = q.kq[UKFF];
             };
             const int dst = (corr || fin) ? L::DZ : L::DZA;   // the finish's step goes to DZ
+            T cviol = 0;   // finish: this lane's most violated add candidate and its stage
+            int ck = -1;
             T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) dx_j
             // dx_{k+1}(r) = c_r + [A B](r, :) (z_k + dz_k) - z_{k+1}(r): the dynamics residual is
             // folded in, so the sweep carries xt = dx_{k+1} + z_{k+1} and subtracts z_{k+1} when
@@ -831,10 +845,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if constexpr (fin) {
                         // finish: acceptance tests, next active set; polishing groups only store (a
                         // finished group's DZ / DZA are its result)
-                        T na;
-                        const T a = fin_flag(q.e, bk, fs0);
-                        s_c += finish_check(my, q.e, bk, a, na);
+                        T na, viol;
+                        bool rem;
+                        const T a = fin_flag(q.e, bk, fs0, k);
+                        s_c += finish_check(my, q.e, bk, a, na, viol, rem);
                         s_a += na != T(0) ? T(1) : T(0);   // active bounds of the next set
+                        s_b += rem ? T(1) : T(0);           // removals
+                        ck = viol > cviol ? k : ck;
+                        cviol = fmax(cviol, viol);
                         if (pol) {
                             if (fref) {
                                 stE(L::DZA, k, my);
@@ -873,10 +891,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 const T dx = xt - e.z;
                 if constexpr (fin) {
-                    T na;
-                    const T a = fin_flag(e, bnd(N), fs0);
-                    s_c += finish_check(dx, e, bnd(N), a, na);
+                    T na, viol;
+                    bool rem;
+                    const T a = fin_flag(e, bnd(N), fs0, N);
+                    s_c += finish_check(dx, e, bnd(N), a, na, viol, rem);
                     s_a += na != T(0) ? T(1) : T(0);
+                    s_b += rem ? T(1) : T(0);
+                    ck = viol > cviol ? N : ck;
+                    cviol = fmax(cviol, viol);
                     if (pol) {
                         if (fref) {
                             stE(L::DZA, N, dx);
@@ -894,6 +916,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             s_a = gsum(s_a);
             s_b = gsum(s_b);
             s_c = gsum(s_c);
+            if constexpr (fin) {
+                // PDAS update (oracle/c/riccati_ipm.c pdas_update): bounds with a negative multiplier
+                // leave the set, violated input bounds join; of the violated state bounds only each
+                // component's most violated one joins, and only in the run's first step or a step
+                // without removals
+                addk = (fs0 || s_b == T(0)) ? ck : -1;
+            }
         };
 
         cptr<T> abs_ = (cptr<T>)p.AB;   // [NX][NZ] row-major, wave-uniform SGPR operand
@@ -939,7 +968,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 {
                     T sg = xl ? sigma(q, bnd(N)) : T(0), gadd = 0;
                     if constexpr (FIN) {
-                        finish_terms(q, bnd(N), fs0, sg, gadd);
+                        finish_terms(q, bnd(N), fs0, N, sg, gadd);
                         sg = xl ? sg : T(0);
                     }
                     zb[r] = xl ? q.z : T(0);
@@ -978,11 +1007,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     LPC_SYNC();
                     lazy_duals(k, q, zo, bk);
                     T sg = sigma(q, bk), gadd = 0;
-                    if constexpr (FIN) finish_terms(q, bk, fs0, sg, gadd);
+                    if constexpr (FIN) finish_terms(q, bk, fs0, k, sg, gadd);
 #else
                     lazy(k, q, bk);
                     T sg = sigma(q, bk), gadd = 0;
-                    if constexpr (FIN) finish_terms(q, bk, fs0, sg, gadd);
+                    if constexpr (FIN) finish_terms(q, bk, fs0, k, sg, gadd);
                     zb[r] = q.z;
                     LPC_SYNC();
 #endif
@@ -1222,9 +1251,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // on with this iteration from their untouched IPM iterate
             pol = active && p.polish_mu > T(0) && mu <= polish_at && !prev_failed;
             if (__any(pol)) {
-                polish_at = pol ? fmin(polish_at, mu) * T(0.01) : polish_at;
+                polish_at = pol ? fmin(polish_at, mu) * p.polish_drop : polish_at;
+                const int plim = fin_runs == 0 ? p.polish_first : p.polish_steps;   // set steps of this run
+                fin_runs += pol ? 1 : 0;
                 fref = false;
-                for (int fs = 0; fs <= p.polish_steps; fs++) {
+                for (int fs = 0; fs <= (p.polish_first > p.polish_steps ? p.polish_first : p.polish_steps); fs++) {
                     fs0 = fs == 0;
                     fwarm = warm && fs0 && it == 0;   // first run of the solve: pending is false
                     pfail = false;
@@ -1251,7 +1282,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             pol = false;
                         } else if (okp) {
                             fref = true;
-                        } else if (pfail || fs + 1 >= p.polish_steps) {
+                        } else if (pfail || fs + 1 >= plim) {
                             pol = false;
                         }
                     }
@@ -1423,6 +1454,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             if (r == 0) {
                 p.status[inst] = status < 0 ? 0 : status;
                 p.iters[inst] = iters;
+                if (fused && p.iter_log)   // finish steps | IPM iterations << 8 | status << 16
+                    p.iter_log[(size_t)cstep * p.B + inst] = fin_steps | ((iters - fin_steps) << 8) | ((status < 0 ? 0 : status) << 16);
 #ifdef NMPC_SWEEP_TIMING
                 if (timed) {
                     unsigned long long *c = p.cycles + (size_t)inst * 9;
