@@ -192,7 +192,7 @@ struct nmpc_solver {
     std::string name, err;
     int device = 0, precision = NMPC_FP64, batch = 0;
     int nx = 0, nu = 0, N = 0, ny = 0, ny_e = 0;
-    int kidx = -1, ipw = 1, wpb = 1, lds = 0, yref_is_z = 0;
+    int kidx = -1, ipw = 1, wpb = 1, lds = 0, yref_is_z = 0, g_diag = 0;
     int max_iter = 50;
     double tol_comp = 0, tol_res = 0, mu0 = 0, inv_m = 1, ts = 0, scale_e = 1;
     double polish_mu = 0, polish_rho = 0, polish_drop = 0.01;
@@ -355,6 +355,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.ny = h->ny;
     p.ny_e = h->ny_e;
     p.yref_is_z = h->yref_is_z;
+    p.g_diag = h->g_diag;
     p.max_iter = h->max_iter;
     p.tol_comp = (T)h->tol_comp;
     p.tol_res = (T)h->tol_res;
@@ -404,9 +405,14 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
         double s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int b = 0; b < h->batch; b++)
             for (int j = 0; j < 9; j++) s[j] += (double)c[(size_t)b * 9 + j] / h->batch;
-        std::fprintf(stderr, "[nmpc cycles] B=%d mean per instance: E_A %.0f A %.0f B %.0f E_B %.0f E_C %.0f C %.0f"
-                     " D %.0f E_D %.0f total %.0f\n",
-                     h->batch, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8]);
+        if (std::strcmp(std::getenv("NMPC_SWEEP_CYCLES"), "step") == 0)   // NMPC_STEP_TIMING builds
+            std::fprintf(stderr, "[nmpc step cycles] B=%d steps=%d mean per instance: cert %.0f init %.0f finA %.0f"
+                         " finB %.0f ipmA %.0f ipmBCD %.0f out %.0f adv %.0f total %.0f\n",
+                         h->batch, cl_steps, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8]);
+        else
+            std::fprintf(stderr, "[nmpc cycles] B=%d mean per instance: E_A %.0f A %.0f B %.0f E_B %.0f E_C %.0f C %.0f"
+                         " D %.0f E_D %.0f total %.0f\n",
+                         h->batch, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8]);
     }
     return 0;
 }
@@ -579,6 +585,15 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         for (int q = 0; sel && q < nx; q++)
             if (d->Vx_e[r * nx + q] != (r == q ? 1.0 : 0.0)) sel = false;
     h->yref_is_z = sel ? 1 : 0;
+    // diagonal gradient maps (diagonal W): the kernels form g_c = G_rr y_r
+    bool gdiag = sel;
+    for (int i = 0; gdiag && i < nz; i++)
+        for (int j = 0; j < ny; j++)
+            if (i != j && h->G[i * ny + j] != 0.0) gdiag = false;
+    for (int i = 0; gdiag && i < nx; i++)
+        for (int j = 0; j < ny_e; j++)
+            if (i != j && h->Ge[i * ny_e + j] != 0.0) gdiag = false;
+    h->g_diag = gdiag ? 1 : 0;
     // ---- bounds [3][nz]
     h->lbnd.assign(3 * nz, -kInf);
     h->ubnd.assign(3 * nz, kInf);

@@ -42,6 +42,7 @@ struct IpmParams {
     int N;          // horizon
     int ny, ny_e;   // LINEAR_LS residual sizes
     int yref_is_z;  // y = [x; u] (selection Vx, Vu): use yref as the initial guess
+    int g_diag;     // yref_is_z and G, Ge diagonal (diagonal W): g_c = G_rr y_r
     int max_iter;
     T tol_comp, tol_res, mu0, inv_m;
     T polish_mu;    // exact finish threshold (0: off)

@@ -386,7 +386,24 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // bounds, an infeasible QP) skips the finish in the next step — its active-set runs cannot be
     // accepted and would only lengthen its wavefront's step chain
     bool prev_failed = false;
+#ifdef NMPC_STEP_TIMING
+    // experiment builds only (build_experiment(..., ["NMPC_STEP_TIMING"]), env NMPC_SWEEP_CYCLES): clock
+    // cycles of each phase of a closed-loop step, summed over the launch's steps: 0 certificate, 1
+    // initial point, 2 finish Riccati, 3 finish forward, 4 IPM Riccati, 5 IPM B/C/D, 6 outputs, 7 advance
+    unsigned long long st_cy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     for (int cstep = 0; cstep < nsteps; cstep++) {
+#ifdef NMPC_STEP_TIMING
+        unsigned long long st_mark = __builtin_amdgcn_s_memtime();
+        auto stick = [&](int slot) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            st_cy[slot] += t - st_mark;
+            st_mark = t;
+        };
+#define LPC_STICK(slot) stick(slot)
+#else
+#define LPC_STICK(slot) ((void)0)
+#endif
         // fused closed loop: the yref window straight from the reference table rows (offset + step) %
         // period (cl_prepare_kernel's gather), x0 from the closed-loop state
         const int t_ref = fused ? (p.cl.offset[inst] + p.cl.step + cstep) % p.cl.period : 0;
@@ -394,11 +411,20 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                               : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
         const int yrow = fused ? p.cl.table_cols : p.ny;
         const T *x0 = (fused ? p.cl.state : p.x0) + (size_t)inst * NX;
+        // the bounds of element (k, r) are read once per stage, ahead of their use (B)
+        struct Bd {
+            T lb, ub;
+        };
+        auto bnd = [&](int k) { return Bd{LB(k), UB(k)}; };
         // ------------------------------------------------------------------ infeasibility certificate
         // interval reachability (oracle/c/riccati_ipm.c infeasible_stage): x-lane r carries the
         // midpoint / radius of state r of X_k, u-lanes the input box; X_{k+1} = hull([A B] X_k x U
         // + c) meets the state box of stage k+1, an empty intersection proves the QP infeasible
         bool infeas = false;
+        // row r of [A B] as a compact list (structured kernels) for the certificate and the residual
+        // of the initial point
+        SpL<T, RN> arl0;
+        if constexpr (SPARSE) sp_load(arl0, slv, sli, row_base);
         {
             T cm = xl ? x0[r] : T(0), cr = 0;
             if (ul) {
@@ -407,25 +433,36 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 cm = bb ? T(0.5) * (l + h) : T(0);
                 cr = bb ? T(0.5) * (h - l) : T(INFINITY);
             }
-            T *rad = gb + Gm::G_MT;
+            const Bd bm = bnd(1);
+            // one LDS exchange per stage: midpoints and radii alternate between two buffers
             for (int k = 0; k < N; k++) {
-                zb[r] = cm;
+                T *cmb = gb + Gm::G_MT + (k & 1) * 2 * LDZ, *rad = cmb + LDZ;
+                cmb[r] = cm;
                 rad[r] = cr;
                 LPC_SYNC();
                 T sm = c_r, sr = 0;
+                if constexpr (SPARSE) {
 #pragma unroll
-                for (int j = 0; j < NZ; j++) {
-                    const T a = abr[(xl ? r : 0) * LDZ + j];
-                    sm = fma(a, zb[j], sm);
-                    sr = a != T(0) ? fma(fabs(a), rad[j], sr) : sr;   // 0 x unbounded radius adds 0
+                    for (int j = 0; j < RN; j++) {
+                        const T a = arl0.v[j];
+                        sm = fma(a, *(const T *)((const char *)cmb + arl0.o[j]), sm);
+                        // 0 x unbounded radius adds 0 (padding entries are (0, 0))
+                        sr = a != T(0) ? fma(fabs(a), *(const T *)((const char *)rad + arl0.o[j]), sr) : sr;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NZ; j++) {
+                        const T a = abr[(xl ? r : 0) * LDZ + j];
+                        sm = fma(a, cmb[j], sm);
+                        sr = a != T(0) ? fma(fabs(a), rad[j], sr) : sr;
+                    }
                 }
-                const T l = LB(k + 1), h = UB(k + 1);
+                const Bd b1 = k + 1 == N ? bnd(N) : bm;
                 T lo = sm - sr, hi = sm + sr;
-                lo = has_bound(l) ? fmax(lo, l) : lo;
-                hi = has_bound(h) ? fmin(hi, h) : hi;
+                lo = has_bound(b1.lb) ? fmax(lo, b1.lb) : lo;
+                hi = has_bound(b1.ub) ? fmin(hi, b1.ub) : hi;
                 infeas |= xl && lo > hi + T(1e-9) * (T(1) + fabs(hi));
                 const bool fin = isfinite(lo) && isfinite(hi);
-                LPC_SYNC();
                 if (xl) {
                     cm = fin ? T(0.5) * (lo + hi) : sm;
                     cr = fin ? T(0.5) * (hi - lo) : sr;
@@ -433,69 +470,105 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             }
             infeas = gmax(infeas ? T(1) : T(0)) > T(0);
         }
+        LPC_STICK(0);
         // ------------------------------------------------------------------ initial point
+        // y = z with diagonal W (p.g_diag, every reference model): g_c = G_rr y_r from the lane's own
+        // y component; stage rows are loaded YC stages at a time (one memory latency per chunk)
+        constexpr int YC = 4;
+        const bool gd = p.g_diag != 0;
+        const T gdr = gd ? p.G[r * p.ny + r] : T(0), gde = (gd && xl) ? p.Ge[r * p.ny_e + r] : T(0);
+        const T hrr0 = SP::hdiag ? hm[r * LDZ + r] : T(0), hre0 = SP::hdiag ? hem[(xl ? r : 0) * LDX + (xl ? r : 0)] : T(0);
         T r0 = 0, mu = 0, abz = 0;
-        for (int k = 0; k <= N; k++) {
-            const bool ex = k < N || xl;
-            const T *yk = yref + (size_t)k * yrow;
-            T z = 0, lam_l = 0, lam_u = 0, gc = 0;
-            const T lb = LB(k), ub = UB(k);
-            if (ex) {
-                if (k < N) {
-                    for (int j = 0; j < p.ny; j++) gc += p.G[r * p.ny + j] * yk[j];
-                } else {
-                    for (int j = 0; j < p.ny_e; j++) gc += p.Ge[r * p.ny_e + j] * yk[j];
-                }
-                if (k == 0 && xl) {
-                    z = x0[r];
-                } else {
-                    z = p.yref_is_z ? yk[r] : T(0);
-                    const bool hl = has_bound(lb), hu = has_bound(ub);
-                    if (hl && hu) {
-                        const T d = T(0.01) * (ub - lb);
-                        z = ul ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
-                        z = fmin(fmax(z, lb + d), ub - d);
-                    } else if (hl) {
-                        z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
-                    } else if (hu) {
-                        z = fmin(z, ub - T(0.01) * fmax(fabs(ub), T(1)));
+        const Bd b0i = bnd(0), bmi = bnd(1);
+        LPC_SYNC();   // the certificate's last exchange buffers are read before they are rewritten
+        for (int kc = 0; kc <= N; kc += YC) {
+            T ych[YC];
+#pragma unroll
+            for (int j = 0; j < YC; j++) {
+                const int k = kc + j <= N ? kc + j : N;
+                const bool yv = k < N ? r < p.ny : r < p.ny_e;   // row N holds ny_e entries
+                ych[j] = yref[(size_t)k * yrow + (yv ? r : 0)];
+                ych[j] = yv ? ych[j] : T(0);
+            }
+#pragma unroll
+            for (int j = 0; j < YC; j++) {
+                const int k = kc + j;
+                if (k > N) break;
+                const bool ex = k < N || xl;
+                const T yr = ych[j];
+                T z = 0, lam_l = 0, lam_u = 0, gc = 0;
+                const Bd bk = k == 0 ? b0i : (k == N ? bnd(N) : bmi);
+                const T lb = bk.lb, ub = bk.ub;
+                if (ex) {
+                    if (gd) {
+                        gc = (k < N ? gdr : gde) * yr;
+                    } else {
+                        const T *yk = yref + (size_t)k * yrow;
+                        if (k < N) {
+                            for (int jj = 0; jj < p.ny; jj++) gc += p.G[r * p.ny + jj] * yk[jj];
+                        } else {
+                            for (int jj = 0; jj < p.ny_e; jj++) gc += p.Ge[r * p.ny_e + jj] * yk[jj];
+                        }
                     }
-                    if (hl) lam_l = p.mu0 / (z - lb);
-                    if (hu) lam_u = p.mu0 / (ub - z);
+                    if (k == 0 && xl) {
+                        z = x0[r];
+                    } else {
+                        z = p.yref_is_z ? yr : T(0);
+                        const bool hl = has_bound(lb), hu = has_bound(ub);
+                        if (hl && hu) {
+                            const T d = T(0.01) * (ub - lb);
+                            z = ul ? T(0.5) * (lb + ub) : z;   // boxed inputs start mid-box (oracle/c/riccati_ipm.c)
+                            z = fmin(fmax(z, lb + d), ub - d);
+                        } else if (hl) {
+                            z = fmax(z, lb + T(0.01) * fmax(fabs(lb), T(1)));
+                        } else if (hu) {
+                            z = fmin(z, ub - T(0.01) * fmax(fabs(ub), T(1)));
+                        }
+                        if (hl) lam_l = p.mu0 / (z - lb);
+                        if (hu) lam_u = p.mu0 / (ub - z);
+                    }
+                }
+                stE(L::Z, k, z);
+                stE(L::LL, k, lam_l);
+                stE(L::LU, k, lam_u);
+                stE(L::GC, k, gc);
+                // one LDS exchange per stage (two alternating buffers)
+                T *zx = gb + Gm::G_MT + (k & 1) * LDZ;
+                zx[r] = z;
+                LPC_SYNC();
+                if (ex) {
+                    T g = gc;
+                    if (SP::hdiag) {
+                        g = fma(k < N ? hrr0 : hre0, z, g);
+                    } else if (k < N) {
+#pragma unroll
+                        for (int b = 0; b < NZ; b++) g = fma(hm[r * LDZ + b], zx[b], g);
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < NX; b++) g = fma(hem[r * LDX + b], zx[b], g);
+                    }
+                    if (!(k == 0 && xl)) {
+                        r0 = fmax(r0, fabs(g - lam_l + lam_u));
+                        if (lam_l > T(0)) mu += lam_l * (z - lb);
+                        if (lam_u > T(0)) mu += lam_u * (ub - z);
+                    }
+                    if (xl && k > 0) r0 = fmax(r0, fabs(abz - z));
+                    if (xl && k < N) {
+                        if constexpr (SPARSE) {
+                            abz = sp_dot(arl0, zx, c_r);
+                        } else {
+                            T s_ = c_r;
+#pragma unroll
+                            for (int jj = 0; jj < NZ; jj++) s_ = fma(abr[r * LDZ + jj], zx[jj], s_);
+                            abz = s_;
+                        }
+                    }
                 }
             }
-            stE(L::Z, k, z);
-            stE(L::LL, k, lam_l);
-            stE(L::LU, k, lam_u);
-            stE(L::GC, k, gc);
-            zb[r] = z;
-            LPC_SYNC();
-            if (ex) {
-                T g = gc;
-                if (k < N) {
-#pragma unroll
-                    for (int b = 0; b < NZ; b++) g = fma(hm[r * LDZ + b], zb[b], g);
-                } else {
-#pragma unroll
-                    for (int b = 0; b < NX; b++) g = fma(hem[r * LDX + b], zb[b], g);
-                }
-                if (!(k == 0 && xl)) {
-                    r0 = fmax(r0, fabs(g - lam_l + lam_u));
-                    if (lam_l > T(0)) mu += lam_l * (z - lb);
-                    if (lam_u > T(0)) mu += lam_u * (ub - z);
-                }
-                if (xl && k > 0) r0 = fmax(r0, fabs(abz - z));
-                if (xl && k < N) {
-                    T s = c_r;
-#pragma unroll
-                    for (int j = 0; j < NZ; j++) s = fma(abr[r * LDZ + j], zb[j], s);
-                    abz = s;
-                }
-            }
-            LPC_SYNC();
         }
         r0 = gmax(r0);
         mu = gsum(mu) * p.inv_m;
+        LPC_STICK(1);
 
         const T m_bounds = T(1) / p.inv_m;
         T theta = 1;
@@ -527,11 +600,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // lazily apply the pending step of the previous iteration to element (k, r)
         // lazily apply the pending step of the previous iteration to element (k, r); the arithmetic
         // is branch-free (selects), the write-back a write-only divergent block
-        // the bounds of element (k, r) are read once per stage, ahead of their use (B)
-        struct Bd {
-            T lb, ub;
-        };
-        auto bnd = [&](int k) { return Bd{LB(k), UB(k)}; };
         auto lazy = [&](int k, El &q, const Bd &b) {
             const bool upd = pending && (k < N || xl);
             const T lb = b.lb, ub = b.ub;
@@ -1260,9 +1328,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     fwarm = warm && fs0 && it == 0;   // first run of the solve: pending is false
                     pfail = false;
                     riccati(Pass<1>{});
+                    LPC_STICK(2);
                     pending = false;
                     T d0, nact, d2, nbad;
                     forward(Pass<2>{}, d0, nact, d2, nbad);
+                    LPC_STICK(3);
                     if (pol) {
                         fin_steps++;
                         const bool okp = nbad == T(0) && !pfail;
@@ -1293,6 +1363,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 if (!__any(active)) break;
             }
             riccati(Pass<0>{});
+            LPC_STICK(4);
 
             LPC_TICK(1);
             pending = false;   // the previous step is applied (converged groups stay frozen from here)
@@ -1421,6 +1492,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     pending = true;
                 }
             }
+            LPC_STICK(5);
         }
 
         // ------------------------------------------------------------------ apply pending step, outputs
@@ -1428,27 +1500,41 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             T *xo = p.xout + (size_t)inst * (N + 1) * NX;
             T *uo = p.uout + (size_t)inst * N * NU;
             T fprev = 0;
-            for (int k = 0; k <= N; k++) {
-                if (k == N && ul) {
-                    if (fused) stE(L::ACT, N, fprev);   // u-lanes: stage N mirrors N - 1 for the shift
-                    continue;
+            // the iterate words of OC stages are loaded together (one memory latency per chunk)
+            constexpr int OC = 4;
+            for (int kc = 0; kc <= N; kc += OC) {
+                T zc[OC], dc[OC], ac[OC];
+#pragma unroll
+                for (int j = 0; j < OC; j++) {
+                    const int k = kc + j <= N ? kc + j : N;
+                    zc[j] = ldE(L::Z, k);
+                    dc[j] = ldE(L::DZ, k);
+                    ac[j] = ldE(L::DZA, k);
                 }
-                T z = ldE(L::Z, k);
-                if (pending) z += alpha * ldE(L::DZ, k);
-                if (status < 0) {   // completed by the finish: step + refinement, clamped onto the bounds
-                    const T lb = LB(k), ub = UB(k);
-                    z += ldE(L::DZ, k) + ldE(L::DZA, k);
-                    z = has_bound(lb) ? fmax(z, lb) : z;
-                    z = has_bound(ub) ? fmin(z, ub) : z;
-                }
-                if (xl) xo[k * NX + r] = z;
-                else uo[k * NU + u] = z;
-                if (fused) {   // the solution's active flags, the next step's warm start
-                    const T lb = LB(k), ub = UB(k);
-                    const bool onl = has_bound(lb) && z <= lb + T(1e-7) * (T(1) + fabs(lb));
-                    const bool onu = has_bound(ub) && z >= ub - T(1e-7) * (T(1) + fabs(ub));
-                    fprev = onl ? T(-1) : (onu ? T(1) : T(0));
-                    stE(L::ACT, k, fprev);
+#pragma unroll
+                for (int j = 0; j < OC; j++) {
+                    const int k = kc + j;
+                    if (k > N) break;
+                    if (k == N && ul) {
+                        if (fused) stE(L::ACT, N, fprev);   // u-lanes: stage N mirrors N - 1 for the shift
+                        continue;
+                    }
+                    const Bd bk = bnd(k);
+                    T z = zc[j];
+                    if (pending) z += alpha * dc[j];
+                    if (status < 0) {   // completed by the finish: step + refinement, clamped onto the bounds
+                        z += dc[j] + ac[j];
+                        z = has_bound(bk.lb) ? fmax(z, bk.lb) : z;
+                        z = has_bound(bk.ub) ? fmin(z, bk.ub) : z;
+                    }
+                    if (xl) xo[k * NX + r] = z;
+                    else uo[k * NU + u] = z;
+                    if (fused) {   // the solution's active flags, the next step's warm start
+                        const bool onl = has_bound(bk.lb) && z <= bk.lb + T(1e-7) * (T(1) + fabs(bk.lb));
+                        const bool onu = has_bound(bk.ub) && z >= bk.ub - T(1e-7) * (T(1) + fabs(bk.ub));
+                        fprev = onl ? T(-1) : (onu ? T(1) : T(0));
+                        stE(L::ACT, k, fprev);
+                    }
                 }
             }
             if (r == 0) {
@@ -1466,6 +1552,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             }
         }
         prev_failed = status > 0;
+        LPC_STICK(6);
         if (fused) {
             // closed-loop advance of this step by the instance's lanes (its outputs were written by
             // the lanes of this wavefront just above); the next step's x0 is read by the whole group
@@ -1479,7 +1566,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
+        LPC_STICK(7);
     }
+#ifdef NMPC_STEP_TIMING
+    if (p.cycles && inst_ok && r == 0) {
+        unsigned long long *c = p.cycles + (size_t)inst * 9, tot = 0;
+        for (int j = 0; j < 8; j++) {
+            c[j] = st_cy[j];
+            tot += st_cy[j];
+        }
+        c[8] = tot;
+    }
+#endif
+#undef LPC_STICK
 }
 
 }  // namespace lpc

@@ -22,9 +22,10 @@ struct Geom {
     static constexpr int C_ABR = 0, C_ABT = C_ABR + NX * LDZ, C_H = C_ABT + NZ * LDX, C_HE = C_H + NZ * LDZ,
                          C_LB = C_HE + NX * LDX, C_UB = C_LB + 3 * LDZ, C_TOT = C_UB + 3 * LDZ;
     // per lane group: stage z / dx broadcast, re, v, h_u, F_uu, M^T (aliased by the rows of
-    // Y = L^{-1} F_ux in the factorisation and by the partial products K(u, j) dx_j in the forward sweeps)
+    // Y = L^{-1} F_ux in the factorisation, by the partial products K(u, j) dx_j in the forward sweeps
+    // and by the double-buffered stage exchanges of the certificate and the initial point)
     static constexpr int G_ZB = 0, G_RB = G_ZB + LDZ, G_VB = G_RB + LDX, G_HU = G_VB + LDX, G_FU = G_HU + LDU,
-                         G_MT = G_FU + rup(NU * NU), MTW = cmax(NZ * LDX, NX * LDU), G_RAW = G_MT + MTW;
+                         G_MT = G_FU + rup(NU * NU), MTW = cmax(cmax(NZ * LDX, NX * LDU), 4 * LDZ), G_RAW = G_MT + MTW;
     // lane groups start 16 banks apart (mod 64 dword banks): with a 32-bank stride the first and
     // third instance of a wavefront collided on every per-instance LDS access (PMC: bank
     // conflicts were ~3/4 of LDS-active cycles)

@@ -18,7 +18,7 @@ os.environ.setdefault("NMPC_ITER_LOG", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from drone_attitude_control_amd.batched import ClosedLoop, DEFAULT_N  # noqa: E402
+from drone_attitude_control_amd.batched import ClosedLoop, DEFAULT_N, workload  # noqa: E402
 
 
 def main():
@@ -32,9 +32,18 @@ def main():
     ap.add_argument("--ipw", type=int, default=None, help="instances per wavefront (default: 64 // nz)")
     ap.add_argument("--ipm-cost", type=float, default=1.6)
     ap.add_argument("--worst", type=int, default=4, help="print the step records of the longest chains")
+    ap.add_argument("--uniform", type=int, default=-1,
+                    help="every instance a copy of this one, no noise: the kernel time without a tail")
     args = ap.parse_args()
     N = args.N or DEFAULT_N[args.model]
-    cl = ClosedLoop(args.model, args.batch, N=N, precision=args.precision)
+    if args.uniform >= 0:
+        table, off, x = workload(args.model, N, args.batch, seed=42)
+        u = args.uniform
+        cl = ClosedLoop(args.model, args.batch, N=N, precision=args.precision, table=table,
+                        offsets=np.full(args.batch, off[u], dtype=np.int32), x_init=np.repeat(x[u:u + 1], args.batch, 0),
+                        noise_std=0.0)
+    else:
+        cl = ClosedLoop(args.model, args.batch, N=N, precision=args.precision)
     if args.skip:
         cl.run(args.skip)
     cl.run(args.steps)
