@@ -1267,11 +1267,11 @@ static const IpmEntry<T> *table(int *n)
         entry<T, 13, 4, 1, 4, 3>(), entry<T, 13, 4, 1, 2, 4>(),
         // lane-per-component kernels (the default family); the first listed per (nx, nu) is
         // the default variant
-        entry_lpc<T, 13, 4, 4, 3>(), entry_lpc<T, 13, 4, 1, 3>(), entry_lpc<T, 13, 4, 2, 2>(),
+        entry_lpc<T, 13, 4, 2, 2>(), entry_lpc<T, 13, 4, 4, 3>(), entry_lpc<T, 13, 4, 1, 3>(),
         entry_lpc<T, 4, 2, 4, 2>(), entry_lpc<T, 6, 2, 4, 2>(),
         // their structure-specialised twins (chosen by ipm_refine when the model fits)
-        entry_lpc<T, 13, 4, 4, 3, lpc::Quad13Structure>(), entry_lpc<T, 13, 4, 1, 3, lpc::Quad13Structure>(),
-        entry_lpc<T, 13, 4, 2, 2, lpc::Quad13Structure>(), entry_lpc<T, 4, 2, 4, 2, lpc::ForceStructure>(),
+        entry_lpc<T, 13, 4, 2, 2, lpc::Quad13Structure>(), entry_lpc<T, 13, 4, 4, 3, lpc::Quad13Structure>(),
+        entry_lpc<T, 13, 4, 1, 3, lpc::Quad13Structure>(), entry_lpc<T, 4, 2, 4, 2, lpc::ForceStructure>(),
         entry_lpc<T, 6, 2, 4, 2, lpc::JerkStructure>(),
         // lane-per-instance kernels for the small models, dense and structure-specialised
         entry_lpi<T, 4, 2>(), entry_lpi<T, 6, 2>(),

@@ -386,6 +386,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // bounds, an infeasible QP) skips the finish in the next step — its active-set runs cannot be
     // accepted and would only lengthen its wavefront's step chain
     bool prev_failed = false;
+    // fused closed loop with the controller-model plant (quad13), fp64, cost at x_0: the state stays in
+    // the group's LDS for the whole launch (G_CL: state, this step's output z_0, yref row 0, sums),
+    // the plant step is one LDS exchange and a row of the solver's own [A B] (the same data
+    // nmpc_closed_loop_init uploads as the plant), and the cost / AED / failure sums of
+    // cl_advance_group are accumulated in LDS and added to the global sums once at the end
+    const bool fastpl = sizeof(T) == 8 && fused && p.cl.plant == 0 && p.cl.cost_stage == 0;
+    T *const clx = lds + Gm::C_TOT + (wave * VS + grp) * Gm::G_TOT + Gm::G_CL, *const clz = clx + LDZ,
+            *const cly = clz + LDZ, *const cls = cly + LDZ;
+    if (fastpl) {
+        clx[r] = (xl && inst_ok) ? p.cl.state[(size_t)inst * NX + r] : T(0);
+        if (r < 4) cls[r] = T(0);
+    }
 #ifdef NMPC_STEP_TIMING
     // experiment builds only (build_experiment(..., ["NMPC_STEP_TIMING"]), env NMPC_SWEEP_CYCLES): clock
     // cycles of each phase of a closed-loop step, summed over the launch's steps: 0 certificate, 1
@@ -411,6 +423,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                               : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
         const int yrow = fused ? p.cl.table_cols : p.ny;
         const T *x0 = (fused ? p.cl.state : p.x0) + (size_t)inst * NX;
+        const T x0r = fastpl ? clx[r] : (xl ? x0[r] : T(0));
         T *const xo = p.xout + (size_t)inst * (N + 1) * NX, *const uo = p.uout + (size_t)inst * N * NU;
         // the bounds of element (k, r) are read once per stage, ahead of their use (B)
         struct Bd {
@@ -427,7 +440,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         SpL<T, RN> arl0;
         if constexpr (SPARSE) sp_load(arl0, slv, sli, row_base);
         {
-            T cm = xl ? x0[r] : T(0), cr = 0;
+            T cm = xl ? x0r : T(0), cr = 0;
             if (ul) {
                 const T l = LB(0), h = UB(0);
                 const bool bb = has_bound(l) && has_bound(h);
@@ -497,6 +510,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 if (k > N) break;
                 const bool ex = k < N || xl;
                 const T yr = ych[j];
+                if (fastpl && k == 0) cly[r] = yr;
                 T z = 0, lam_l = 0, lam_u = 0, gc = 0;
                 const Bd bk = k == 0 ? b0i : (k == N ? bnd(N) : bmi);
                 const T lb = bk.lb, ub = bk.ub;
@@ -512,7 +526,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         }
                     }
                     if (k == 0 && xl) {
-                        z = x0[r];
+                        z = x0r;
                     } else {
                         z = p.yref_is_z ? yr : T(0);
                         const bool hl = has_bound(lb), hu = has_bound(ub);
@@ -691,6 +705,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             z = has_bound(b.ub) ? fmin(z, b.ub) : z;
             if (xl) xo[k * NX + r] = z;
             else uo[k * NU + u] = z;
+            if (fastpl && k == 0) clz[r] = z;
             if (fused) {
                 const bool onl = has_bound(b.lb) && z <= b.lb + T(1e-7) * (T(1) + fabs(b.lb));
                 const bool onu = has_bound(b.ub) && z >= b.ub - T(1e-7) * (T(1) + fabs(b.ub));
@@ -1630,6 +1645,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     const Bd bk = bnd(k);
                     T z = zc[j];
                     if (pending) z += alpha * dc[j];
+                    if (fastpl && k == 0) clz[r] = z;
                     if (xl) xo[k * NX + r] = z;
                     else uo[k * NU + u] = z;
                     if (fused) {   // the solution's active flags, the next step's warm start
@@ -1664,14 +1680,54 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (inst_ok)
+            if (fastpl) {
+                // cl_advance_group for the controller-model plant: cost sum_i w_i (x_0 - xref)_i^2 and
+                // AED numerator sum_i |xref - x|_i at the current state (x_0 is pinned to it; xref =
+                // yref row 0), then x <- [A B] [x; u_0] + c + noise
+                const int nc = p.cl.ncl, na_ = p.cl.aed_dims;
+                const T xs = clx[r];
+                const double e_ = (double)xs - (double)cly[r];
+                double ce = (xl && r < nc) ? (double)p.cl.wcl[r] * e_ * e_ : 0.0;
+                double ae = (xl && r < na_) ? fabs(e_) : 0.0;
+                ce = gsum(ce);
+                ae = gsum(ae);
+                T *zx = gb + Gm::G_MT;
+                zx[r] = xl ? xs : clz[r];
+                LPC_SYNC();
+                T sx;
+                if constexpr (SPARSE) {
+                    sx = sp_dot(arl0, zx, c_r);
+                } else {
+                    T s0 = c_r, s1 = 0;
+#pragma unroll
+                    for (int jj = 0; jj + 1 < NZ; jj += 2) {
+                        s0 = fma(abr[(xl ? r : 0) * LDZ + jj], zx[jj], s0);
+                        s1 = fma(abr[(xl ? r : 0) * LDZ + jj + 1], zx[jj + 1], s1);
+                    }
+                    if (NZ % 2) s0 = fma(abr[(xl ? r : 0) * LDZ + NZ - 1], zx[NZ - 1], s0);
+                    sx = s0 + s1;
+                }
+                const double w_ = p.cl_noise[(size_t)inst * nsteps + cstep];
+                if (xl) clx[r] = (T)((double)sx + (r < p.cl.noise_dims ? w_ : 0.0));
+                if (r == 0) {
+                    cls[0] += (T)ce;
+                    cls[1] += (T)ae;
+                    cls[2] += (status > 0) ? T(1) : T(0);
+                    cls[3] += T(1);
+                }
+            } else if (inst_ok) {
                 cl_advance_group<T, NX, NU>(p.cl, inst, p.cl.step + cstep, status < 0 ? 0 : status, r,
                                             p.cl_noise[(size_t)inst * nsteps + cstep]);
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         LPC_STICK(7);
+    }
+    if (fastpl && inst_ok) {   // the launch's final state and its closed-loop sums
+        if (xl) p.cl.state[(size_t)inst * NX + r] = clx[r];
+        if (r < 4) p.cl.acc[(size_t)inst * 4 + r] += (double)cls[r];
     }
 #ifdef NMPC_STEP_TIMING
     if (p.cycles && inst_ok && r == 0) {

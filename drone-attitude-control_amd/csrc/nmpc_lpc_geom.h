@@ -23,9 +23,11 @@ struct Geom {
                          C_LB = C_HE + NX * LDX, C_UB = C_LB + 3 * LDZ, C_TOT = C_UB + 3 * LDZ;
     // per lane group: stage z / dx broadcast, re, v, h_u, F_uu, M^T (aliased by the rows of
     // Y = L^{-1} F_ux in the factorisation, by the partial products K(u, j) dx_j in the forward sweeps
-    // and by the double-buffered stage exchanges of the certificate and the initial point)
+    // and by the double-buffered stage exchanges of the certificate and the initial point); G_CL: fused
+    // closed loop with the model plant — state, output z_0, yref row 0 (LDZ each) and 4 sums
     static constexpr int G_ZB = 0, G_RB = G_ZB + LDZ, G_VB = G_RB + LDX, G_HU = G_VB + LDX, G_FU = G_HU + LDU,
-                         G_MT = G_FU + rup(NU * NU), MTW = cmax(cmax(NZ * LDX, NX * LDU), 4 * LDZ), G_RAW = G_MT + MTW;
+                         G_MT = G_FU + rup(NU * NU), MTW = cmax(cmax(NZ * LDX, NX * LDU), 4 * LDZ),
+                         G_CL = G_MT + MTW, G_RAW = G_CL + 3 * LDZ + rup(4);
     // lane groups start 16 banks apart (mod 64 dword banks): with a 32-bank stride the first and
     // third instance of a wavefront collided on every per-instance LDS access (PMC: bank
     // conflicts were ~3/4 of LDS-active cycles)
