@@ -366,6 +366,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.polish_steps = h->polish_steps;
     p.polish_first = h->polish_first;
     p.polish_drop = (T)h->polish_drop;
+    static const int warm_shift = std::getenv("NMPC_WARM_SHIFT") ? std::atoi(std::getenv("NMPC_WARM_SHIFT")) : 1;
+    p.warm_shift = warm_shift;
     const char *m = (const char *)h->d_model;
     p.AB = (const T *)(m + h->off_AB);
     p.ABt = (const T *)(m + h->off_ABt);

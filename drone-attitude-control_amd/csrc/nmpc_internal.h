@@ -50,6 +50,7 @@ struct IpmParams {
     int polish_steps;   // active-set Newton steps per finish run
     int polish_first;   // ... in the first run of a solve (the warm-started one in the closed loop)
     T polish_drop;      // after a rejected run the next one waits for mu <= polish_drop * mu
+    int warm_shift;     // fused closed loop: warm-start flags shifted by one stage (1) or as solved (0)
     const T *AB;    // [nx][nx+nu]   discrete [A B], row-major
     const T *ABt;   // [nx+nu][nx]   its transpose
     const T *c;     // [nx]

@@ -634,7 +634,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             auto fin_flag = [&](int k, int i, int e, T z, T lam_l, T lam_u, T lb, T ub) {
                 if (k == 0 && i < NX) return T(0);
                 if (fs0 && fwarm) {
-                    const int ks = (k < N - 1 || (k == N - 1 && i < NX)) ? k + 1 : k;
+                    const int ks = !p.warm_shift ? k : ((k < N - 1 || (k == N - 1 && i < NX)) ? k + 1 : k);
                     const T a = S.ld(Lact, (unsigned)(ks * NZ + i));
                     return (a < T(-0.5) && lam_l > T(0)) ? T(-1) : ((a > T(0.5) && lam_u > T(0)) ? T(1) : T(0));
                 }

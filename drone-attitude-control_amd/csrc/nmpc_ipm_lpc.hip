@@ -828,7 +828,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 q.e.z = ldE(L::Z, k);
                 q.e.ll = ldE(L::LL, k);
                 q.e.lu = ldE(L::LU, k);
-                if (corr || fin) q.e.dza = (fin && fwarm) ? ldE(L::ACT, k < N ? k + 1 : N) : ldE(L::DZA, k);
+                if (corr || fin) q.e.dza = (fin && fwarm) ? ldE(L::ACT, (p.warm_shift && k < N) ? k + 1 : k) : ldE(L::DZA, k);
                 if constexpr (fin) {   // finish: the step's base point (refinement: z_a = z + dz)
                     const T dzp = ldE(L::DZ, k);
                     q.e.z = fref ? q.e.z + dzp : q.e.z;
@@ -1062,7 +1062,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     e.g = ldE(L::GC, k);
                     e.dz = ldE(L::DZ, k);     // unconditional: a divergent load arm costs more than
                     // the bytes (first iteration: unused stale words; warm finish: the shifted flags)
-                    e.dza = (FIN && fwarm) ? ldE(L::ACT, k < N ? k + 1 : N) : ldE(L::DZA, k);
+                    e.dza = (FIN && fwarm) ? ldE(L::ACT, (p.warm_shift && k < N) ? k + 1 : k) : ldE(L::DZA, k);
                 };
                 // terminal stage: P_N = He + Sigma_N, p_N = g_N
                 fetchA(N, q);
