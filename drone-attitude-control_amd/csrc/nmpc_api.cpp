@@ -213,6 +213,7 @@ struct nmpc_solver {
     int *d_status = nullptr, *d_iters = nullptr;
     unsigned long long *d_cycles = nullptr;
     size_t off_AB = 0, off_ABt = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
+    size_t off_lqr = 0;   // unconstrained Riccati records per stage (lqr_table)
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
     bool cl_ready = false;
@@ -248,6 +249,77 @@ struct nmpc_solver {
 };
 
 namespace {
+
+// The Newton system of an exact-finish step whose active set is empty (no penalty, no barrier) is
+// the unconstrained LQ problem: its Riccati factorisation is the same for every instance and step.
+// Per stage k < N and lane r of the lane-per-component kernels, nz words: x-lane r holds row r of
+// P_{k+1} (nx words) and column r of the gain K_k = -F_uu^{-1} F_ux (nu words); u-lane u holds row u
+// of F_uu^{-1} (nu words). P_N = He; F = [A B]' P_{k+1} [A B] + H; P_k = F_xx + F_xu K_k.
+void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::vector<double> &B,
+               const std::vector<double> &H, const std::vector<double> &He, std::vector<double> &tab)
+{
+    const int nz = nx + nu;
+    tab.assign((size_t)N * nz * nz, 0.0);
+    std::vector<double> P(He), M((size_t)nx * nz), F((size_t)nz * nz), L((size_t)nu * nu), Fi((size_t)nu * nu),
+        K((size_t)nu * nx);
+    auto ab = [&](int l, int c) { return c < nx ? A[l * nx + c] : B[l * nu + (c - nx)]; };
+    for (int k = N - 1; k >= 0; k--) {
+        double *t = &tab[(size_t)k * nz * nz];
+        for (int r = 0; r < nx; r++)
+            for (int j = 0; j < nx; j++) t[r * nz + j] = P[r * nx + j];
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < nz; j++) {
+                double s_ = 0.0;
+                for (int l = 0; l < nx; l++) s_ += P[i * nx + l] * ab(l, j);
+                M[i * nz + j] = s_;
+            }
+        for (int i = 0; i < nz; i++)
+            for (int j = 0; j < nz; j++) {
+                double s_ = H[i * nz + j];
+                for (int l = 0; l < nx; l++) s_ += ab(l, i) * M[l * nz + j];
+                F[i * nz + j] = s_;
+            }
+        // F_uu^{-1} by Cholesky (F_uu is positive definite for the reference models' costs)
+        for (int i = 0; i < nu; i++)
+            for (int j = 0; j <= i; j++) {
+                double s_ = F[(nx + i) * nz + nx + j];
+                for (int l = 0; l < j; l++) s_ -= L[i * nu + l] * L[j * nu + l];
+                L[i * nu + j] = i == j ? std::sqrt(std::max(s_, 1e-300)) : s_ / L[j * nu + j];
+            }
+        for (int c = 0; c < nu; c++) {   // column c of F_uu^{-1}: L L' x = e_c
+            double y[64];
+            for (int i = 0; i < nu; i++) {
+                double s_ = i == c ? 1.0 : 0.0;
+                for (int l = 0; l < i; l++) s_ -= L[i * nu + l] * y[l];
+                y[i] = s_ / L[i * nu + i];
+            }
+            for (int i = nu - 1; i >= 0; i--) {
+                double s_ = y[i];
+                for (int l = i + 1; l < nu; l++) s_ -= L[l * nu + i] * y[l];
+                y[i] = s_ / L[i * nu + i];
+            }
+            for (int i = 0; i < nu; i++) Fi[i * nu + c] = y[i];
+        }
+        for (int i = 0; i < nu; i++)
+            for (int j = 0; j < nx; j++) {
+                double s_ = 0.0;
+                for (int l = 0; l < nu; l++) s_ -= Fi[i * nu + l] * F[(nx + l) * nz + j];
+                K[i * nx + j] = s_;
+            }
+        for (int r = 0; r < nx; r++)
+            for (int i = 0; i < nu; i++) t[r * nz + nx + i] = K[i * nx + r];
+        for (int u = 0; u < nu; u++)
+            for (int i = 0; i < nu; i++) t[(nx + u) * nz + i] = Fi[u * nu + i];
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < nx; j++) {
+                double s_ = F[i * nz + j];
+                for (int l = 0; l < nu; l++) s_ += F[i * nz + nx + l] * K[l * nx + j];
+                P[i * nx + j] = s_;
+            }
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < i; j++) P[i * nx + j] = P[j * nx + i] = 0.5 * (P[i * nx + j] + P[j * nx + i]);
+    }
+}
 
 int hip_fail(nmpc_solver *h, hipError_t e, const char *what)
 {
@@ -378,6 +450,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.Ge = (const T *)(m + h->off_Ge);
     p.lbnd = (const T *)(m + h->off_lb);
     p.ubnd = (const T *)(m + h->off_ub);
+    static const bool no_lqr = std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0';
+    p.lqr = no_lqr ? nullptr : (const T *)(m + h->off_lqr);
     p.x0 = (const T *)h->d_x0;
     p.yref = (const T *)h->d_yref;
     p.xout = (T *)h->d_x;
@@ -717,6 +791,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_Ge = carve((size_t)nx * std::max(ny_e, 1));
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
+    h->off_lqr = carve((size_t)N * nz * nz);
     const size_t model_bytes = off;
     if (h->cond) {
         if (!nmpc::cond_build(nx, nu, N, ny, ny_e, h->A, h->B, h->c, h->H, h->G, h->He, h->Ge, h->lbnd, h->ubnd, h->ch)) {
@@ -796,6 +871,11 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     put(h->off_Ge, h->Ge);
     put(h->off_lb, h->lbnd);
     put(h->off_ub, h->ubnd);
+    {
+        std::vector<double> lqr;
+        lqr_table(nx, nu, N, h->A, h->B, h->H, h->He, lqr);
+        put(h->off_lqr, lqr);
+    }
     if (h->cond) {
         const nmpc::CondHost &c = h->ch;
         const std::vector<double> *parts[15] = {&c.Gx, &c.H0, &c.H0t, &c.Fx, &c.Fy, &c.fc, &c.Phx, &c.dx, &c.lox,

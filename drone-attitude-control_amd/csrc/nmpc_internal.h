@@ -60,6 +60,7 @@ struct IpmParams {
     const T *Ge;    // [nx][ny_e]
     const T *lbnd;  // [3][nz]       bounds: stage 0 (x entries absent), 1..N-1, N
     const T *ubnd;  // [3][nz]
+    const T *lqr;   // [N][nz][nz]   unconstrained Riccati records (nmpc_api.cpp lqr_table), or null
     const T *x0;    // [B][nx]
     const T *yref;  // [B][N*ny + ny_e]
     T *xout;        // [B][N+1][nx]

@@ -493,6 +493,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         const T gdr = gd ? p.G[r * p.ny + r] : T(0), gde = (gd && xl) ? p.Ge[r * p.ny_e + r] : T(0);
         const T hrr0 = SP::hdiag ? hm[r * LDZ + r] : T(0), hre0 = SP::hdiag ? hem[(xl ? r : 0) * LDX + (xl ? r : 0)] : T(0);
         T r0 = 0, mu = 0, abz = 0;
+        T cold_act = 0;   // bounds the finish's first-set rule marks at the initial point (lqr_back)
         const Bd b0i = bnd(0), bmi = bnd(1);
         LPC_SYNC();   // the certificate's last exchange buffers are read before they are rewritten
         for (int kc = 0; kc <= N; kc += YC) {
@@ -541,6 +542,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         }
                         if (hl) lam_l = p.mu0 / (z - lb);
                         if (hu) lam_u = p.mu0 / (ub - z);
+                        cold_act += ((hl && lam_l > z - lb) || (hu && lam_u > ub - z)) ? T(1) : T(0);
                     }
                 }
                 stE(L::Z, k, z);
@@ -583,6 +585,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         }
         r0 = gmax(r0);
         mu = gsum(mu) * p.inv_m;
+        cold_act = gsum(cold_act);
         LPC_STICK(1);
 
         const T m_bounds = T(1) / p.inv_m;
@@ -607,6 +610,27 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // are unchanged), read into the dza slots, which the first iteration does not use otherwise
     const bool warm = fused && (cstep > 0 || p.cl.step > 0);
     bool fwarm = false;   // wave-uniform: the current finish pass reads the warm flags
+    // active bounds of the warm-start set (lqr_back needs an empty first set): the previous solution's
+    // flags as the first finish step will read them (shifted by one stage)
+    T warm_act = 0;
+    if (warm && p.lqr) {
+        constexpr int AC = 4;
+        for (int kc = 0; kc <= N; kc += AC) {
+            T a_[AC];
+#pragma unroll
+            for (int j = 0; j < AC; j++) {
+                const int k = kc + j <= N ? kc + j : N;
+                a_[j] = ldE(L::ACT, (p.warm_shift && k < N) ? k + 1 : k);
+            }
+#pragma unroll
+            for (int j = 0; j < AC; j++) {
+                const int k = kc + j;
+                const bool valid = k <= N && !(k == 0 && xl) && (k < N || xl);
+                warm_act += (valid && a_[j] != T(0)) ? T(1) : T(0);
+            }
+        }
+        warm_act = gsum(warm_act);
+    }
 
         // elementwise state of element (k, r) fetched one stage ahead in the sweeps
         struct El {
@@ -1348,6 +1372,98 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
             };
 
+            // ============================ exact finish step on an empty active set (structured kernels):
+            // no penalty and no barrier, so the Newton system is the unconstrained LQ problem, whose
+            // Riccati factorisation is the same for every instance (p.lqr, computed once per handle on
+            // the host: P_{k+1}, K_k, F_uu^{-1}). What remains per instance is the vector recursion
+            // p_k = h_x + K' h_u, h = g_k + [A B]' (P_{k+1} re_k + p_{k+1}), kff = -F_uu^{-1} h_u with
+            // g = H z + G yref and re the dynamics residual at z; K and kff go to the stage records for
+            // the forward sweep, as the full factorisation would write them
+            auto lqr_back = [&]() __attribute__((always_inline)) {
+                const T hrr = hm[r * LDZ + r], hre = hem[(xl ? r : 0) * LDX + (xl ? r : 0)];
+                T znext = ldE(L::Z, N), pv = fma(hre, znext, ldE(L::GC, N));
+                T rowc[NZ], rown[NZ];
+                auto rowld = [&](int k, T (&d_)[NZ]) {
+                    const T *t_ = p.lqr + ((size_t)(k < 0 ? 0 : k) * NZ + r) * NZ;
+#pragma unroll
+                    for (int j = 0; j < NZ; j++) d_[j] = t_[j];
+                };
+                rowld(N - 1, rowc);
+                SpL<T, RN> arl;
+                SpL<T, CN> acl;
+                if constexpr (SPARSE) {
+                    sp_load(arl, slv, sli, row_base);
+                    sp_load(acl, slv, sli, col_base);
+                }
+                const T *arow = abr + (xl ? r : 0) * LDZ, *acol = abt + r * LDX;
+                for (int k = N - 1; k >= 0; k--) {
+                    const T z = ldE(L::Z, k), gc = ldE(L::GC, k);
+                    rowld(k - 1, rown);   // next stage's table row, in flight during this stage
+                    zb[r] = z;
+                    LPC_SYNC();
+                    T re;
+                    if constexpr (SPARSE) {
+                        re = sp_dot(arl, zb, c_r) - znext;
+                    } else {
+                        T s0 = c_r, s1 = 0;
+#pragma unroll
+                        for (int jj = 0; jj + 1 < NZ; jj += 2) {
+                            s0 = fma(arow[jj], zb[jj], s0);
+                            s1 = fma(arow[jj + 1], zb[jj + 1], s1);
+                        }
+                        if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
+                        re = s0 + s1 - znext;
+                    }
+                    if (xl) rb[r] = re;
+                    LPC_SYNC();
+                    T v0 = pv, v1 = 0;
+#pragma unroll
+                    for (int j = 0; j + 1 < NX; j += 2) {
+                        v0 = fma(rowc[j], rb[j], v0);
+                        v1 = fma(rowc[j + 1], rb[j + 1], v1);
+                    }
+                    if (NX % 2) v0 = fma(rowc[NX - 1], rb[NX - 1], v0);
+                    if (xl) vb[r] = v0 + v1;
+                    LPC_SYNC();
+                    const T g = fma(hrr, z, gc);
+                    T h;
+                    if constexpr (SPARSE) {
+                        h = sp_dot(acl, vb, g);
+                    } else {
+                        T h0 = g, h1 = 0;
+#pragma unroll
+                        for (int i = 0; i + 1 < NX; i += 2) {
+                            h0 = fma(acol[i], vb[i], h0);
+                            h1 = fma(acol[i + 1], vb[i + 1], h1);
+                        }
+                        if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                        h = h0 + h1;
+                    }
+                    if (ul) hub[u] = h;
+                    LPC_SYNC();
+                    T hu[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) hu[i] = hub[i];
+                    if (ul) {
+                        T kf = 0;
+#pragma unroll
+                        for (int i = 0; i < NU; i++) kf = fma(-rowc[i], hu[i], kf);
+                        stU(k, UKFF, kf);
+                    } else {
+                        T s_ = h;
+#pragma unroll
+                        for (int i = 0; i < NU; i++) {
+                            s_ = fma(rowc[NX + i], hu[i], s_);
+                            stX(k, i, rowc[NX + i]);
+                        }
+                        pv = s_;
+                    }
+                    znext = z;
+#pragma unroll
+                    for (int j = 0; j < NZ; j++) rowc[j] = rown[j];
+                }
+            };
+
             // ============================ refinement of the exact finish, vector pass (structured kernels):
             // the refinement solves the set step's Newton system again — same active set, same penalty,
             // so the same factorisation, whose records (K, F_uu^{-1}) are still in scratch — with the
@@ -1451,7 +1567,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     pfail = false;
                     // the refinement reuses the set step's factorisation when every polishing group of
                     // the wavefront is refining (structured kernels: diagonal costs)
+                    // and an empty first set (warm: the previous solution had no active bound; cold: the
+                    // first-set rule marks none) runs lqr_back
+                    const bool sempty = fs0 && it == 0 && (fwarm ? warm_act == T(0) : cold_act == T(0));
                     if (SP::hdiag && __all(!pol || fref)) refine_back();
+                    else if (SP::hdiag && p.lqr && __all(!pol || sempty)) lqr_back();
                     else riccati(Pass<1>{});
                     LPC_STICK(2);
                     pending = false;
