@@ -252,27 +252,30 @@ namespace {
 
 // The Newton system of an exact-finish step whose active set is empty (no penalty, no barrier) is
 // the unconstrained LQ problem: its Riccati factorisation is the same for every instance and step.
-// Per stage k < N and lane r of the lane-per-component kernels, nz words: x-lane r holds row r of
-// P_{k+1} (nx words) and column r of the gain K_k = -F_uu^{-1} F_ux (nu words); u-lane u holds row u
-// of F_uu^{-1} (nu words). P_N = He; F = [A B]' P_{k+1} [A B] + H; P_k = F_xx + F_xu K_k.
+// Per stage k < N and lane r of the lane-per-component kernels, lqr_words(nx, nu) = nz words: x-lane
+// r holds row r of P_{k+1} (nx words) and column r of the gain K_k = -F_uu^{-1} F_ux (nu); u-lane u
+// holds row u of F_uu^{-1} (nu words). P_N = He; F = [A B]' P_{k+1} [A B] + H; P_k = F_xx + F_xu K_k.
+int lqr_words(int nx, int nu) { return nx + nu; }
 void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::vector<double> &B,
-               const std::vector<double> &H, const std::vector<double> &He, std::vector<double> &tab)
+               const std::vector<double> &c, const std::vector<double> &H, const std::vector<double> &He,
+               std::vector<double> &tab)
 {
-    const int nz = nx + nu;
-    tab.assign((size_t)N * nz * nz, 0.0);
+    const int nz = nx + nu, W = lqr_words(nx, nu);
+    tab.assign((size_t)N * nz * W, 0.0);
     std::vector<double> P(He), M((size_t)nx * nz), F((size_t)nz * nz), L((size_t)nu * nu), Fi((size_t)nu * nu),
         K((size_t)nu * nx);
     auto ab = [&](int l, int c) { return c < nx ? A[l * nx + c] : B[l * nu + (c - nx)]; };
     for (int k = N - 1; k >= 0; k--) {
-        double *t = &tab[(size_t)k * nz * nz];
-        for (int r = 0; r < nx; r++)
-            for (int j = 0; j < nx; j++) t[r * nz + j] = P[r * nx + j];
+        double *t = &tab[(size_t)k * nz * W];
         for (int i = 0; i < nx; i++)
             for (int j = 0; j < nz; j++) {
                 double s_ = 0.0;
                 for (int l = 0; l < nx; l++) s_ += P[i * nx + l] * ab(l, j);
                 M[i * nz + j] = s_;
             }
+        (void)c;
+        for (int r = 0; r < nx; r++)
+            for (int j = 0; j < nx; j++) t[r * W + j] = P[r * nx + j];
         for (int i = 0; i < nz; i++)
             for (int j = 0; j < nz; j++) {
                 double s_ = H[i * nz + j];
@@ -307,9 +310,9 @@ void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::v
                 K[i * nx + j] = s_;
             }
         for (int r = 0; r < nx; r++)
-            for (int i = 0; i < nu; i++) t[r * nz + nx + i] = K[i * nx + r];
+            for (int i = 0; i < nu; i++) t[r * W + nx + i] = K[i * nx + r];
         for (int u = 0; u < nu; u++)
-            for (int i = 0; i < nu; i++) t[(nx + u) * nz + i] = Fi[u * nu + i];
+            for (int i = 0; i < nu; i++) t[(nx + u) * W + i] = Fi[u * nu + i];
         for (int i = 0; i < nx; i++)
             for (int j = 0; j < nx; j++) {
                 double s_ = F[i * nz + j];
@@ -791,7 +794,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_Ge = carve((size_t)nx * std::max(ny_e, 1));
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
-    h->off_lqr = carve((size_t)N * nz * nz);
+    h->off_lqr = carve((size_t)N * nz * lqr_words(nx, nu));
     const size_t model_bytes = off;
     if (h->cond) {
         if (!nmpc::cond_build(nx, nu, N, ny, ny_e, h->A, h->B, h->c, h->H, h->G, h->He, h->Ge, h->lbnd, h->ubnd, h->ch)) {
@@ -873,7 +876,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     put(h->off_ub, h->ubnd);
     {
         std::vector<double> lqr;
-        lqr_table(nx, nu, N, h->A, h->B, h->H, h->He, lqr);
+        lqr_table(nx, nu, N, h->A, h->B, h->c, h->H, h->He, lqr);
         put(h->off_lqr, lqr);
     }
     if (h->cond) {

@@ -1380,15 +1380,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // g = H z + G yref and re the dynamics residual at z; K and kff go to the stage records for
             // the forward sweep, as the full factorisation would write them
             auto lqr_back = [&]() __attribute__((always_inline)) {
+                // three LDS exchanges per stage: [z_k; g_k], the residual re_k, v = p_{k+1} + P_{k+1} re_k;
+                // every lane forms h_u = g_u + B' v itself (no fourth exchange), x-lanes h_x = g_x + A' v
+                constexpr int OK = NX;
                 const T hrr = hm[r * LDZ + r], hre = hem[(xl ? r : 0) * LDX + (xl ? r : 0)];
-                T znext = ldE(L::Z, N), pv = fma(hre, znext, ldE(L::GC, N));
-                T rowc[NZ], rown[NZ];
+                T *const zk = gb + Gm::G_MT, *const gk = zk + LDZ;
+                T rowc[NZ];
                 auto rowld = [&](int k, T (&d_)[NZ]) {
                     const T *t_ = p.lqr + ((size_t)(k < 0 ? 0 : k) * NZ + r) * NZ;
 #pragma unroll
                     for (int j = 0; j < NZ; j++) d_[j] = t_[j];
                 };
-                rowld(N - 1, rowc);
                 SpL<T, RN> arl;
                 SpL<T, CN> acl;
                 if constexpr (SPARSE) {
@@ -1396,22 +1398,24 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     sp_load(acl, slv, sli, col_base);
                 }
                 const T *arow = abr + (xl ? r : 0) * LDZ, *acol = abt + r * LDX;
+                T znext = ldE(L::Z, N), pv = fma(hre, znext, ldE(L::GC, N));   // p_N = g_N (x-lanes)
                 for (int k = N - 1; k >= 0; k--) {
                     const T z = ldE(L::Z, k), gc = ldE(L::GC, k);
-                    rowld(k - 1, rown);   // next stage's table row, in flight during this stage
-                    zb[r] = z;
+                    rowld(k, rowc);   // the table row (L2-resident), in flight during the first exchanges
+                    zk[r] = z;
+                    gk[r] = fma(hrr, z, gc);
                     LPC_SYNC();
                     T re;
                     if constexpr (SPARSE) {
-                        re = sp_dot(arl, zb, c_r) - znext;
+                        re = sp_dot(arl, zk, c_r) - znext;
                     } else {
                         T s0 = c_r, s1 = 0;
 #pragma unroll
                         for (int jj = 0; jj + 1 < NZ; jj += 2) {
-                            s0 = fma(arow[jj], zb[jj], s0);
-                            s1 = fma(arow[jj + 1], zb[jj + 1], s1);
+                            s0 = fma(arow[jj], zk[jj], s0);
+                            s1 = fma(arow[jj + 1], zk[jj + 1], s1);
                         }
-                        if (NZ % 2) s0 = fma(arow[NZ - 1], zb[NZ - 1], s0);
+                        if (NZ % 2) s0 = fma(arow[NZ - 1], zk[NZ - 1], s0);
                         re = s0 + s1 - znext;
                     }
                     if (xl) rb[r] = re;
@@ -1425,42 +1429,47 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if (NX % 2) v0 = fma(rowc[NX - 1], rb[NX - 1], v0);
                     if (xl) vb[r] = v0 + v1;
                     LPC_SYNC();
-                    const T g = fma(hrr, z, gc);
-                    T h;
-                    if constexpr (SPARSE) {
-                        h = sp_dot(acl, vb, g);
-                    } else {
-                        T h0 = g, h1 = 0;
-#pragma unroll
-                        for (int i = 0; i + 1 < NX; i += 2) {
-                            h0 = fma(acol[i], vb[i], h0);
-                            h1 = fma(acol[i + 1], vb[i + 1], h1);
-                        }
-                        if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
-                        h = h0 + h1;
-                    }
-                    if (ul) hub[u] = h;
-                    LPC_SYNC();
                     T hu[NU];
 #pragma unroll
-                    for (int i = 0; i < NU; i++) hu[i] = hub[i];
+                    for (int i = 0; i < NU; i++) {
+                        if constexpr (SPARSE) {
+                            SpL<T, CN> bc;
+                            sp_load(bc, slv, sli, NX * RN + (NX + i) * CN);
+                            hu[i] = sp_dot(bc, vb, gk[NX + i]);
+                        } else {
+                            T s0 = gk[NX + i];
+#pragma unroll
+                            for (int l = 0; l < NX; l++) s0 = fma(abt[(NX + i) * LDX + l], vb[l], s0);
+                            hu[i] = s0;
+                        }
+                    }
                     if (ul) {
                         T kf = 0;
 #pragma unroll
                         for (int i = 0; i < NU; i++) kf = fma(-rowc[i], hu[i], kf);
                         stU(k, UKFF, kf);
                     } else {
-                        T s_ = h;
+                        T h;
+                        if constexpr (SPARSE) {
+                            h = sp_dot(acl, vb, gk[r]);
+                        } else {
+                            T h0 = gk[r], h1 = 0;
+#pragma unroll
+                            for (int i = 0; i + 1 < NX; i += 2) {
+                                h0 = fma(acol[i], vb[i], h0);
+                                h1 = fma(acol[i + 1], vb[i + 1], h1);
+                            }
+                            if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                            h = h0 + h1;
+                        }
 #pragma unroll
                         for (int i = 0; i < NU; i++) {
-                            s_ = fma(rowc[NX + i], hu[i], s_);
-                            stX(k, i, rowc[NX + i]);
+                            h = fma(rowc[OK + i], hu[i], h);
+                            stX(k, i, rowc[OK + i]);
                         }
-                        pv = s_;
+                        pv = h;
                     }
                     znext = z;
-#pragma unroll
-                    for (int j = 0; j < NZ; j++) rowc[j] = rown[j];
                 }
             };
 
