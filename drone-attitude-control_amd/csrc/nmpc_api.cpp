@@ -252,10 +252,11 @@ namespace {
 
 // The Newton system of an exact-finish step whose active set is empty (no penalty, no barrier) is
 // the unconstrained LQ problem: its Riccati factorisation is the same for every instance and step.
-// Per stage k < N and lane r of the lane-per-component kernels, lqr_words(nx, nu) = nz words: x-lane
-// r holds row r of P_{k+1} (nx words) and column r of the gain K_k = -F_uu^{-1} F_ux (nu); u-lane u
-// holds row u of F_uu^{-1} (nu words). P_N = He; F = [A B]' P_{k+1} [A B] + H; P_k = F_xx + F_xu K_k.
-int lqr_words(int nx, int nu) { return nx + nu; }
+// Per stage k < N and lane r of the lane-per-component kernels, lqr_words(nx, nu) = nz + 1 words:
+// x-lane r holds row r of P_{k+1} (nx words), column r of the gain K_k = -F_uu^{-1} F_ux (nu) and
+// (P_{k+1} c)_r (1); u-lane u holds row u of F_uu^{-1} (nu words). P_N = He;
+// F = [A B]' P_{k+1} [A B] + H; P_k = F_xx + F_xu K_k.
+int lqr_words(int nx, int nu) { return nx + nu + 1; }
 void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::vector<double> &B,
                const std::vector<double> &c, const std::vector<double> &H, const std::vector<double> &He,
                std::vector<double> &tab)
@@ -273,9 +274,14 @@ void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::v
                 for (int l = 0; l < nx; l++) s_ += P[i * nx + l] * ab(l, j);
                 M[i * nz + j] = s_;
             }
-        (void)c;
-        for (int r = 0; r < nx; r++)
-            for (int j = 0; j < nx; j++) t[r * W + j] = P[r * nx + j];
+        for (int r = 0; r < nx; r++) {
+            double q = 0.0;
+            for (int j = 0; j < nx; j++) {
+                t[r * W + j] = P[r * nx + j];
+                q += P[r * nx + j] * c[j];
+            }
+            t[r * W + nz] = q;
+        }
         for (int i = 0; i < nz; i++)
             for (int j = 0; j < nz; j++) {
                 double s_ = H[i * nz + j];
@@ -443,6 +449,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.polish_drop = (T)h->polish_drop;
     static const int warm_shift = std::getenv("NMPC_WARM_SHIFT") ? std::atoi(std::getenv("NMPC_WARM_SHIFT")) : 1;
     p.warm_shift = warm_shift;
+    static const int fast_mode = std::getenv("NMPC_FAST") ? std::atoi(std::getenv("NMPC_FAST")) : 1;
+    p.fast_mode = fast_mode;
     const char *m = (const char *)h->d_model;
     p.AB = (const T *)(m + h->off_AB);
     p.ABt = (const T *)(m + h->off_ABt);

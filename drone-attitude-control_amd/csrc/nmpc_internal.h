@@ -51,6 +51,7 @@ struct IpmParams {
     int polish_first;   // ... in the first run of a solve (the warm-started one in the closed loop)
     T polish_drop;      // after a rejected run the next one waits for mu <= polish_drop * mu
     int warm_shift;     // fused closed loop: warm-start flags shifted by one stage (1) or as solved (0)
+    int fast_mode;      // fused closed loop: fast exact finish on an empty warm set (1; 0 off, 2 not at a launch's first step)
     const T *AB;    // [nx][nx+nu]   discrete [A B], row-major
     const T *ABt;   // [nx+nu][nx]   its transpose
     const T *c;     // [nx]
@@ -60,7 +61,7 @@ struct IpmParams {
     const T *Ge;    // [nx][ny_e]
     const T *lbnd;  // [3][nz]       bounds: stage 0 (x entries absent), 1..N-1, N
     const T *ubnd;  // [3][nz]
-    const T *lqr;   // [N][nz][nz]   unconstrained Riccati records (nmpc_api.cpp lqr_table), or null
+    const T *lqr;   // [N][nz][nz+1] unconstrained Riccati records (nmpc_api.cpp lqr_table), or null
     const T *x0;    // [B][nx]
     const T *yref;  // [B][N*ny + ny_e]
     T *xout;        // [B][N+1][nx]

@@ -348,7 +348,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     __syncthreads();
     if (!__any(inst_ok)) return;
 
-    T *gb = lds + Gm::C_TOT + (wave * VS + grp) * Gm::G_TOT;
+    T *gb = lds + Gm::C_TOT + Gm::group_area(wave, grp) * Gm::G_TOT;
     T *zb = gb + Gm::G_ZB, *rb = gb + Gm::G_RB, *vb = gb + Gm::G_VB, *hub = gb + Gm::G_HU, *fu = gb + Gm::G_FU;
     T *mt = gb + Gm::G_MT, *ylds = gb + Gm::G_MT;
 
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // nmpc_closed_loop_init uploads as the plant), and the cost / AED / failure sums of
     // cl_advance_group are accumulated in LDS and added to the global sums once at the end
     const bool fastpl = sizeof(T) == 8 && fused && p.cl.plant == 0 && p.cl.cost_stage == 0;
-    T *const clx = lds + Gm::C_TOT + (wave * VS + grp) * Gm::G_TOT + Gm::G_CL, *const clz = clx + LDZ,
+    T *const clx = lds + Gm::C_TOT + Gm::group_area(wave, grp) * Gm::G_TOT + Gm::G_CL, *const clz = clx + LDZ,
             *const cly = clz + LDZ, *const cls = cly + LDZ;
     if (fastpl) {
         clx[r] = (xl && inst_ok) ? p.cl.state[(size_t)inst * NX + r] : T(0);
@@ -430,6 +430,200 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             T lb, ub;
         };
         auto bnd = [&](int k) { return Bd{LB(k), UB(k)}; };
+        // outputs of a finish step, written by its forward sweep (status -1 skips the output pass):
+        // z_new clamped onto the bounds and, in the fused closed loop, its active flags (the next
+        // step's warm start; u-lanes also write stage N, a mirror of N - 1). A step that is not
+        // accepted is overwritten by a later one or by the output pass of an IPM-ended solve.
+        auto fin_out = [&](int k, T z, const Bd &b) {
+            z = has_bound(b.lb) ? fmax(z, b.lb) : z;
+            z = has_bound(b.ub) ? fmin(z, b.ub) : z;
+            if (xl) xo[k * NX + r] = z;
+            else uo[k * NU + u] = z;
+            if (fastpl && k == 0) clz[r] = z;
+            if (fused) {
+                const bool onl = has_bound(b.lb) && z <= b.lb + T(1e-7) * (T(1) + fabs(b.lb));
+                const bool onu = has_bound(b.ub) && z >= b.ub - T(1e-7) * (T(1) + fabs(b.ub));
+                const T f = onl ? T(-1) : (onu ? T(1) : T(0));
+                stE(L::ACT, k, f);
+                if (ul && k == N - 1) stE(L::ACT, N, f);
+            }
+        };
+        // row r of [A B] as a compact list (structured kernels): certificate, initial point, plant step
+        SpL<T, RN> arl0;
+        if constexpr (SPARSE) sp_load(arl0, slv, sli, row_base);
+    // fused closed loop after its first step: the first finish run of a solve starts from the
+    // previous step's active set shifted by one stage (ACT word; warm start, the acceptance tests
+    // are unchanged), read into the dza slots, which the first iteration does not use otherwise
+    const bool warm = fused && (cstep > 0 || p.cl.step > 0);
+    bool fwarm = false;   // wave-uniform: the current finish pass reads the warm flags
+    // the warm-start set: the previous solution's flags (ACT), shifted by one stage, copied into the
+    // DZA words the first finish step reads its flags from (so ACT is free for this solve's outputs),
+    // and counted (an empty set takes the fast finish / lqr_back)
+    T warm_act = 0;
+    if (warm) {
+        constexpr int AC = 4;
+        for (int kc = 0; kc <= N; kc += AC) {
+            T a_[AC];
+#pragma unroll
+            for (int j = 0; j < AC; j++) {
+                const int k = kc + j <= N ? kc + j : N;
+                a_[j] = ldE(L::ACT, (p.warm_shift && k < N) ? k + 1 : k);
+            }
+#pragma unroll
+            for (int j = 0; j < AC; j++) {
+                const int k = kc + j;
+                const bool valid = k <= N && !(k == 0 && xl) && (k < N || xl);
+                warm_act += (valid && a_[j] != T(0)) ? T(1) : T(0);
+                if (k <= N) stE(L::DZA, k, valid ? a_[j] : T(0));
+            }
+        }
+        warm_act = gsum(warm_act);
+    }
+
+
+        // ------------------------------------------------------------------ fast exact finish
+        // (fused closed loop, structured kernels with diagonal gradient maps): when the warm-start set
+        // is empty, the first finish step is the unconstrained LQ solution, taken here from the base
+        // point z = 0 (a Newton step on the QP lands on the same point from any base): backward
+        // p_N = g_N, v = p_{k+1} + P_{k+1} c, h = g_k + [A B]' v, kff_k = -F_uu^{-1} h_u,
+        // p_k = h_x + K_k' h_u with g = G yref (one LDS exchange per stage, the factorisation from
+        // p.lqr), then the forward rollout x_0 = x0, u_k = kff_k + K_k x_k, x_{k+1} = [A B] z_k + c.
+        // If every bound holds (the finish's acceptance test for an empty set) the solve is complete
+        // (status 0, one Newton system) and the group skips the certificate, the initial point and
+        // the IPM; otherwise it runs the full solve below.
+        bool fast_ok = false;
+        {
+            constexpr int W = NZ + 1, OQ = NZ;
+            constexpr double FAST_TOL = 1e-13;
+            const bool try_fast = SP::hdiag && p.lqr != nullptr && p.g_diag && p.polish_mu > T(0) && warm && inst_ok &&
+                                  !prev_failed && warm_act == T(0) && p.fast_mode != 0 && (p.fast_mode == 1 || cstep > 0);
+            if (__any(try_fast)) {
+                const T gdr = p.G[r * p.ny + r], gde = xl ? p.Ge[r * p.ny_e + r] : T(0);
+                T gdu[NU];
+#pragma unroll
+                for (int i = 0; i < NU; i++) gdu[i] = p.G[(NX + i) * p.ny + NX + i];
+                SpL<T, CN> acl;
+                if constexpr (SPARSE) sp_load(acl, slv, sli, col_base);
+                const T *acol = abt + r * LDX;
+                auto trow = [&](int k) { return p.lqr + ((size_t)k * NZ + r) * W; };
+                T pv = gde * yref[(size_t)N * yrow + (xl ? r : 0)];   // p_N = g_N (x-lanes)
+                for (int k = N - 1; k >= 0; k--) {
+                    const T *yk = yref + (size_t)k * yrow, *t_ = trow(k);
+                    const T gc = gdr * yk[r];
+                    T gu[NU], tr[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        gu[i] = gdu[i] * yk[NX + i];
+                        tr[i] = t_[(xl ? NX : 0) + i];   // x-lane: K(i, r); u-lane: F_uu^{-1}(u, i)
+                    }
+                    if (xl) vb[r] = pv + t_[OQ];
+                    LPC_SYNC();
+                    T hu[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        if constexpr (SPARSE) {
+                            SpL<T, CN> bc;
+                            sp_load(bc, slv, sli, NX * RN + (NX + i) * CN);
+                            hu[i] = sp_dot(bc, vb, gu[i]);
+                        } else {
+                            T s0 = gu[i];
+#pragma unroll
+                            for (int l = 0; l < NX; l++) s0 = fma(abt[(NX + i) * LDX + l], vb[l], s0);
+                            hu[i] = s0;
+                        }
+                    }
+                    if (ul) {
+                        T kf = 0;
+#pragma unroll
+                        for (int i = 0; i < NU; i++) kf = fma(-tr[i], hu[i], kf);
+                        stU(k, UKFF, kf);
+                    } else {
+                        T h;
+                        if constexpr (SPARSE) {
+                            h = sp_dot(acl, vb, gc);
+                        } else {
+                            T h0 = gc, h1 = 0;
+#pragma unroll
+                            for (int i = 0; i + 1 < NX; i += 2) {
+                                h0 = fma(acol[i], vb[i], h0);
+                                h1 = fma(acol[i + 1], vb[i + 1], h1);
+                            }
+                            if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                            h = h0 + h1;
+                        }
+#pragma unroll
+                        for (int i = 0; i < NU; i++) h = fma(tr[i], hu[i], h);
+                        pv = h;
+                    }
+                    LPC_SYNC();   // vb is rewritten by the next stage
+                }
+                // forward rollout with the acceptance test and the outputs
+                T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) x_j
+                T xk = x0r, nbad = 0;
+                T kq[NU], kfn = ldU(0, UKFF);
+#pragma unroll
+                for (int i = 0; i < NU; i++) kq[i] = trow(0)[NX + i];
+                const Bd b0 = bnd(0), bm = bnd(1);
+                for (int k = 0; k < N; k++) {
+                    const T kf = kfn;
+                    T kqn[NU];
+                    const int kn = k + 1 < N ? k + 1 : k;
+                    kfn = ldU(kn, UKFF);
+#pragma unroll
+                    for (int i = 0; i < NU; i++) kqn[i] = trow(kn)[NX + i];
+                    {
+                        const int pr_ = xl ? r : NX;   // u-lanes write the spare row
+#pragma unroll
+                        for (int i = 0; i < NU; i++) part[pr_ * LDU + i] = kq[i] * xk;
+                    }
+                    LPC_SYNC();
+                    T uk = kf;
+                    {
+                        const int uu = ul ? u : 0;
+#pragma unroll
+                        for (int jj = 0; jj < NX; jj++) uk += part[jj * LDU + uu];
+                    }
+                    const T z = xl ? xk : uk;
+                    zb[r] = z;
+                    LPC_SYNC();
+                    const Bd bk = k == 0 ? b0 : bm;
+                    // stricter than the finish's 1e-9: a bound violated inside that band goes through the
+                    // full solve, whose rounding decides it exactly as without the fast path
+                    const T tl = T(FAST_TOL) * (T(1) + fabs(bk.lb)), tu = T(FAST_TOL) * (T(1) + fabs(bk.ub));
+                    nbad += (!isfinite(z) || (has_bound(bk.lb) && z < bk.lb - tl) || (has_bound(bk.ub) && z > bk.ub + tu))
+                                ? T(1) : T(0);
+                    if (try_fast) fin_out(k, z, bk);
+                    T xn;
+                    if constexpr (SPARSE) {
+                        xn = sp_dot(arl0, zb, c_r);
+                    } else {
+                        T s0 = c_r, s1 = 0;
+#pragma unroll
+                        for (int jj = 0; jj + 1 < NZ; jj += 2) {
+                            s0 = fma(abr[(xl ? r : 0) * LDZ + jj], zb[jj], s0);
+                            s1 = fma(abr[(xl ? r : 0) * LDZ + jj + 1], zb[jj + 1], s1);
+                        }
+                        if (NZ % 2) s0 = fma(abr[(xl ? r : 0) * LDZ + NZ - 1], zb[NZ - 1], s0);
+                        xn = s0 + s1;
+                    }
+                    xk = xn;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) kq[i] = kqn[i];
+                    LPC_SYNC();   // zb / part are rewritten by the next stage
+                }
+                if (xl) {
+                    const Bd bN = bnd(N);
+                    const T tl = T(FAST_TOL) * (T(1) + fabs(bN.lb)), tu = T(FAST_TOL) * (T(1) + fabs(bN.ub));
+                    nbad += (!isfinite(xk) || (has_bound(bN.lb) && xk < bN.lb - tl) || (has_bound(bN.ub) && xk > bN.ub + tu))
+                                ? T(1) : T(0);
+                    if (try_fast) fin_out(N, xk, bN);
+                }
+                nbad = gsum(nbad);
+                fast_ok = try_fast && nbad == T(0);
+                if (fastpl) cly[r] = yref[xl || r < p.ny ? r : 0];   // yref row 0 (cost / AED reference)
+            }
+        }
+        const bool need_full = __any(inst_ok && !fast_ok);
         // ------------------------------------------------------------------ infeasibility certificate
         // interval reachability (oracle/c/riccati_ipm.c infeasible_stage): x-lane r carries the
         // midpoint / radius of state r of X_k, u-lanes the input box; X_{k+1} = hull([A B] X_k x U
@@ -437,9 +631,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         bool infeas = false;
         // row r of [A B] as a compact list (structured kernels) for the certificate and the residual
         // of the initial point
-        SpL<T, RN> arl0;
-        if constexpr (SPARSE) sp_load(arl0, slv, sli, row_base);
-        {
+        if (need_full) {
             T cm = xl ? x0r : T(0), cr = 0;
             if (ul) {
                 const T l = LB(0), h = UB(0);
@@ -496,7 +688,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         T cold_act = 0;   // bounds the finish's first-set rule marks at the initial point (lqr_back)
         const Bd b0i = bnd(0), bmi = bnd(1);
         LPC_SYNC();   // the certificate's last exchange buffers are read before they are rewritten
-        for (int kc = 0; kc <= N; kc += YC) {
+        for (int kc = 0; need_full && kc <= N; kc += YC) {
             T ych[YC];
 #pragma unroll
             for (int j = 0; j < YC; j++) {
@@ -590,8 +782,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 
         const T m_bounds = T(1) / p.inv_m;
         T theta = 1;
-        bool active = inst_ok && !infeas;
-        int status = infeas ? 4 : 2, iters = 0;   // certified infeasible: status 4, the initial point
+        bool active = inst_ok && !infeas && !fast_ok;
+        // certified infeasible: status 4, the initial point; completed by the fast finish: status -1
+        int status = fast_ok ? -1 : (infeas ? 4 : 2), iters = fast_ok ? 1 : 0;
         bool fail = false, pending = false;
         T alpha = 0, smu = 0;
         // exact finish (oracle/c/riccati_ipm.c "exact finish"): a primal-dual active-set run of at
@@ -602,35 +795,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // its correction. status -1: completed by the finish, outputs = Z + DZ + DZA (B and D skip
         // the group's DZA / DZ)
         T polish_at = p.polish_mu;
-        int fin_steps = 0, fin_runs = 0;
+        int fin_steps = fast_ok ? 1 : 0, fin_runs = 0;
         bool pol = false, fref = false;
         bool fs0 = false;   // wave-uniform: the current finish pass is the first step of its runs
-    // fused closed loop after its first step: the first finish run of a solve starts from the
-    // previous step's active set shifted by one stage (ACT word; warm start, the acceptance tests
-    // are unchanged), read into the dza slots, which the first iteration does not use otherwise
-    const bool warm = fused && (cstep > 0 || p.cl.step > 0);
-    bool fwarm = false;   // wave-uniform: the current finish pass reads the warm flags
-    // active bounds of the warm-start set (lqr_back needs an empty first set): the previous solution's
-    // flags as the first finish step will read them (shifted by one stage)
-    T warm_act = 0;
-    if (warm && p.lqr) {
-        constexpr int AC = 4;
-        for (int kc = 0; kc <= N; kc += AC) {
-            T a_[AC];
-#pragma unroll
-            for (int j = 0; j < AC; j++) {
-                const int k = kc + j <= N ? kc + j : N;
-                a_[j] = ldE(L::ACT, (p.warm_shift && k < N) ? k + 1 : k);
-            }
-#pragma unroll
-            for (int j = 0; j < AC; j++) {
-                const int k = kc + j;
-                const bool valid = k <= N && !(k == 0 && xl) && (k < N || xl);
-                warm_act += (valid && a_[j] != T(0)) ? T(1) : T(0);
-            }
-        }
-        warm_act = gsum(warm_act);
-    }
 
         // elementwise state of element (k, r) fetched one stage ahead in the sweeps
         struct El {
@@ -719,24 +886,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 rem = rl || ru;
             }
             return bad ? T(1) : T(0);
-        };
-        // outputs of a finish step, written by its forward sweep (status -1 skips the output pass):
-        // z_new clamped onto the bounds and, in the fused closed loop, its active flags (the next
-        // step's warm start; u-lanes also write stage N, a mirror of N - 1). A step that is not
-        // accepted is overwritten by a later one or by the output pass of an IPM-ended solve.
-        auto fin_out = [&](int k, T z, const Bd &b) {
-            z = has_bound(b.lb) ? fmax(z, b.lb) : z;
-            z = has_bound(b.ub) ? fmin(z, b.ub) : z;
-            if (xl) xo[k * NX + r] = z;
-            else uo[k * NU + u] = z;
-            if (fastpl && k == 0) clz[r] = z;
-            if (fused) {
-                const bool onl = has_bound(b.lb) && z <= b.lb + T(1e-7) * (T(1) + fabs(b.lb));
-                const bool onu = has_bound(b.ub) && z >= b.ub - T(1e-7) * (T(1) + fabs(b.ub));
-                const T f = onl ? T(-1) : (onu ? T(1) : T(0));
-                stE(L::ACT, k, f);
-                if (ul && k == N - 1) stE(L::ACT, N, f);
-            }
         };
         // the same lazy step split in two for the Riccati stages k < N: the primal update first (it
         // is all the stage's first LDS exchange needs), the dual update after that exchange, where
@@ -852,7 +1001,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 q.e.z = ldE(L::Z, k);
                 q.e.ll = ldE(L::LL, k);
                 q.e.lu = ldE(L::LU, k);
-                if (corr || fin) q.e.dza = (fin && fwarm) ? ldE(L::ACT, (p.warm_shift && k < N) ? k + 1 : k) : ldE(L::DZA, k);
+                if (corr || fin) q.e.dza = ldE(L::DZA, k);   // warm flags: copied into DZA at the step start
                 if constexpr (fin) {   // finish: the step's base point (refinement: z_a = z + dz)
                     const T dzp = ldE(L::DZ, k);
                     q.e.z = fref ? q.e.z + dzp : q.e.z;
@@ -1010,7 +1159,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 e.z = ldE(L::Z, N);
                 e.ll = ldE(L::LL, N);
                 e.lu = ldE(L::LU, N);
-                if (corr || fin) e.dza = (fin && fwarm) ? ldE(L::ACT, N) : ldE(L::DZA, N);
+                if (corr || fin) e.dza = ldE(L::DZA, N);
                 if constexpr (fin) {
                     const T dzp = ldE(L::DZ, N);
                     e.z = fref ? e.z + dzp : e.z;
@@ -1086,7 +1235,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     e.g = ldE(L::GC, k);
                     e.dz = ldE(L::DZ, k);     // unconditional: a divergent load arm costs more than
                     // the bytes (first iteration: unused stale words; warm finish: the shifted flags)
-                    e.dza = (FIN && fwarm) ? ldE(L::ACT, (p.warm_shift && k < N) ? k + 1 : k) : ldE(L::DZA, k);
+                    e.dza = ldE(L::DZA, k);   // (warm flags: copied into DZA at the step start)
                 };
                 // terminal stage: P_N = He + Sigma_N, p_N = g_N
                 fetchA(N, q);
@@ -1387,7 +1536,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 T *const zk = gb + Gm::G_MT, *const gk = zk + LDZ;
                 T rowc[NZ];
                 auto rowld = [&](int k, T (&d_)[NZ]) {
-                    const T *t_ = p.lqr + ((size_t)(k < 0 ? 0 : k) * NZ + r) * NZ;
+                    const T *t_ = p.lqr + ((size_t)(k < 0 ? 0 : k) * NZ + r) * (NZ + 1);   // lqr_table rows
 #pragma unroll
                     for (int j = 0; j < NZ; j++) d_[j] = t_[j];
                 };

@@ -33,7 +33,11 @@ struct Geom {
     // conflicts were ~3/4 of LDS-active cycles)
     static constexpr int DW = (int)sizeof(T) / 4, GSTEP = 64 / DW;
     static constexpr int G_TOT = G_RAW + ((16 / DW - G_RAW % GSTEP) % GSTEP + GSTEP) % GSTEP;
-    static constexpr int LDS_ELEMS = C_TOT + WPB * VS * G_TOT;
+    // the partial lane group of a wavefront (VS > IPW: lanes that carry no instance) works in one
+    // dummy area shared by the whole workgroup (its results are never used)
+    static constexpr int NGA = WPB * IPW + (VS > IPW ? 1 : 0);
+    static constexpr int LDS_ELEMS = C_TOT + NGA * G_TOT;
+    __host__ __device__ static constexpr int group_area(int wave, int grp) { return grp < IPW ? wave * IPW + grp : WPB * IPW; }
     static constexpr int XPR = NU;        // x record: K(:, r) in words 0..NU-1, Pr_r in word NU
     static constexpr int UKFF = 0, UFI = 1;   // u record: kff_u, F_uu^{-1}(u, :) in words 1..NU
     static_assert(IPW >= 1, "stage wider than a wavefront");
