@@ -265,6 +265,14 @@ def main():
                                          "correction: the kernel's loads are 4/8-B per lane, the guide's x2 is "
                                          "calibrated for 16-B streams; includes Infinity-Cache hits",
                          "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
+                         "executed_fp64_flops_per_step": pmc.get("fp64_flops_per_step"),
+                         "flops_note": "achieved credits SURVEY 8d's F_iter (one Riccati factorisation) per Newton "
+                                       "system (n_ipm: the CPU baseline's count on the same first-step QPs); the "
+                                       "GPU's empty-active-set finish steps (fast finish, lqr_back) run a vector "
+                                       "recursion on the handle's shared factorisation instead, so the FP64 work "
+                                       "the kernel executes (executed_fp64_flops_per_step, SQ_INSTS_VALU_FLOPS_FP64 "
+                                       "from the committed PMC pass) is below the credit; the path is bound by "
+                                       "LDS-exchange and dependency latency, not by the FP64 pipe or HBM",
                          "flops_per_launch": fl_launch, "kernel_ms": kernel_ms,
                          "n_ipm": n_ipm, "n_ipm_cpu": n_ipm_cpu, "gpu_mean_qp_iter": st["mean_qp_iter"]},
             "solve_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "QP solves/s",

@@ -447,9 +447,9 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.polish_steps = h->polish_steps;
     p.polish_first = h->polish_first;
     p.polish_drop = (T)h->polish_drop;
-    static const int warm_shift = std::getenv("NMPC_WARM_SHIFT") ? std::atoi(std::getenv("NMPC_WARM_SHIFT")) : 1;
+    const int warm_shift = std::getenv("NMPC_WARM_SHIFT") ? std::atoi(std::getenv("NMPC_WARM_SHIFT")) : 1;
     p.warm_shift = warm_shift;
-    static const int fast_mode = std::getenv("NMPC_FAST") ? std::atoi(std::getenv("NMPC_FAST")) : 1;
+    const int fast_mode = std::getenv("NMPC_FAST") ? std::atoi(std::getenv("NMPC_FAST")) : 1;
     p.fast_mode = fast_mode;
     const char *m = (const char *)h->d_model;
     p.AB = (const T *)(m + h->off_AB);
@@ -461,7 +461,10 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.Ge = (const T *)(m + h->off_Ge);
     p.lbnd = (const T *)(m + h->off_lb);
     p.ubnd = (const T *)(m + h->off_ub);
-    static const bool no_lqr = std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0';
+    // tuning / test switches, read per launch: NMPC_LQR=0 drops the shared factorisation (every finish
+    // step factors), NMPC_FAST=0 / 2 the fast finish (2: not at a launch's first step),
+    // NMPC_WARM_SHIFT=0 the warm-start shift
+    const bool no_lqr = std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0';
     p.lqr = no_lqr ? nullptr : (const T *)(m + h->off_lqr);
     p.x0 = (const T *)h->d_x0;
     p.yref = (const T *)h->d_yref;
