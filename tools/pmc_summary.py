@@ -72,8 +72,8 @@ def main():
         d["note"] = ("memory-side bytes per solve-kernel launch = (FETCH_SIZE + WRITE_SIZE) x 1024 from "
                      "rocprofv3 PMC passes (tools/pmc.sh, tools/pmc_summary.py); includes Infinity-Cache hits; "
                      "per step = per launch / fused closed-loop steps per launch; mfma_insts_per_launch = "
-                     "SQ_INSTS_MFMA; fp64_flops_per_step = SQ_INSTS_VALU_FLOPS_FP64 per step (executed FP64 "
-                     "flops as the hardware counts them)")
+                     "SQ_INSTS_MFMA; fp64_flops_per_step = 64 x SQ_INSTS_VALU_FLOPS_FP64 per step (executed FP64 "
+                     "flops as the hardware counts them, idle lanes included)")
         key = (model, int(N), int(batch), prec)
         d["entries"] = [e for e in d["entries"] if (e["model"], e["N"], e["batch"], e["precision"]) != key]
         d["entries"].append({"model": model, "N": int(N), "batch": int(batch), "precision": prec,
@@ -82,7 +82,9 @@ def main():
                              "hbm_bytes_per_step": res["traffic_bytes_per_launch"] / a.steps_per_launch,
                              # SQ_INSTS_* count wave-level instructions (x 64 lanes for flops); MFMA: 0
                              "mfma_insts_per_launch": means.get("SQ_INSTS_MFMA"),
-                             "fp64_flops_per_step": (means["SQ_INSTS_VALU_FLOPS_FP64"] / a.steps_per_launch
+                             # SQ_INSTS_VALU_FLOPS_FP64 counts per wave instruction (2 per FMA): x 64 lanes
+                             # (the idle lanes of a wavefront included)
+                             "fp64_flops_per_step": (64.0 * means["SQ_INSTS_VALU_FLOPS_FP64"] / a.steps_per_launch
                                                      if "SQ_INSTS_VALU_FLOPS_FP64" in means else None),
                              "source": os.path.relpath(out, ROOT)})
         with open(path, "w") as fh:
