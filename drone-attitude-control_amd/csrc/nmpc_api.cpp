@@ -213,7 +213,7 @@ struct nmpc_solver {
     int *d_status = nullptr, *d_iters = nullptr;
     unsigned long long *d_cycles = nullptr;
     size_t off_AB = 0, off_ABt = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
-    size_t off_lqr = 0;   // unconstrained Riccati records per stage (lqr_table)
+    size_t off_lqr = 0, off_lqrf = 0;   // unconstrained Riccati records per stage (lqr_table)
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
     bool cl_ready = false;
@@ -257,12 +257,18 @@ namespace {
 // (P_{k+1} c)_r (1); u-lane u holds row u of F_uu^{-1} (nu words). P_N = He;
 // F = [A B]' P_{k+1} [A B] + H; P_k = F_xx + F_xu K_k.
 int lqr_words(int nx, int nu) { return nx + nu + 1; }
+//
+// The fast finish's rollout table (lqrf_words = 1 + 2 nu + nx words per stage and lane): x-lane r
+// holds (P_{k+1} c)_r, column r of K_k, row r of B F_uu^{-1} and row r of the closed-loop matrix
+// A + B K_k; u-lane u holds 0, nu zeros, row u of F_uu^{-1} and row u of K_k.
+int lqrf_words(int nx, int nu) { return 1 + 2 * nu + nx; }
 void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::vector<double> &B,
                const std::vector<double> &c, const std::vector<double> &H, const std::vector<double> &He,
-               std::vector<double> &tab)
+               std::vector<double> &tab, std::vector<double> &ftab)
 {
-    const int nz = nx + nu, W = lqr_words(nx, nu);
+    const int nz = nx + nu, W = lqr_words(nx, nu), WF = lqrf_words(nx, nu);
     tab.assign((size_t)N * nz * W, 0.0);
+    ftab.assign((size_t)N * nz * WF, 0.0);
     std::vector<double> P(He), M((size_t)nx * nz), F((size_t)nz * nz), L((size_t)nu * nu), Fi((size_t)nu * nu),
         K((size_t)nu * nx);
     auto ab = [&](int l, int c) { return c < nx ? A[l * nx + c] : B[l * nu + (c - nx)]; };
@@ -319,6 +325,25 @@ void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::v
             for (int i = 0; i < nu; i++) t[r * W + nx + i] = K[i * nx + r];
         for (int u = 0; u < nu; u++)
             for (int i = 0; i < nu; i++) t[(nx + u) * W + i] = Fi[u * nu + i];
+        double *f = &ftab[(size_t)k * nz * WF];
+        for (int r = 0; r < nx; r++) {
+            f[r * WF] = t[r * W + nz];
+            for (int i = 0; i < nu; i++) {
+                f[r * WF + 1 + i] = K[i * nx + r];
+                double s_ = 0.0;
+                for (int l = 0; l < nu; l++) s_ += B[r * nu + l] * Fi[l * nu + i];
+                f[r * WF + 1 + nu + i] = s_;
+            }
+            for (int j = 0; j < nx; j++) {
+                double s_ = A[r * nx + j];
+                for (int i = 0; i < nu; i++) s_ += B[r * nu + i] * K[i * nx + j];
+                f[r * WF + 1 + 2 * nu + j] = s_;
+            }
+        }
+        for (int u = 0; u < nu; u++) {
+            for (int i = 0; i < nu; i++) f[(nx + u) * WF + 1 + nu + i] = Fi[u * nu + i];
+            for (int j = 0; j < nx; j++) f[(nx + u) * WF + 1 + 2 * nu + j] = K[u * nx + j];
+        }
         for (int i = 0; i < nx; i++)
             for (int j = 0; j < nx; j++) {
                 double s_ = F[i * nz + j];
@@ -466,6 +491,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     // NMPC_WARM_SHIFT=0 the warm-start shift
     const bool no_lqr = std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0';
     p.lqr = no_lqr ? nullptr : (const T *)(m + h->off_lqr);
+    p.lqrf = no_lqr ? nullptr : (const T *)(m + h->off_lqrf);
     p.x0 = (const T *)h->d_x0;
     p.yref = (const T *)h->d_yref;
     p.xout = (T *)h->d_x;
@@ -496,7 +522,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
         for (int b = 0; b < h->batch; b++)
             for (int j = 0; j < 9; j++) s[j] += (double)c[(size_t)b * 9 + j] / h->batch;
         if (std::strcmp(std::getenv("NMPC_SWEEP_CYCLES"), "step") == 0)   // NMPC_STEP_TIMING builds
-            std::fprintf(stderr, "[nmpc step cycles] B=%d steps=%d mean per instance: cert %.0f init %.0f finA %.0f"
+            std::fprintf(stderr, "[nmpc step cycles] B=%d steps=%d mean per instance: warm+fast %.0f cert+init %.0f finA %.0f"
                          " finB %.0f ipmA %.0f ipmBCD %.0f out %.0f adv %.0f total %.0f\n",
                          h->batch, cl_steps, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8]);
         else
@@ -806,6 +832,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
     h->off_lqr = carve((size_t)N * nz * lqr_words(nx, nu));
+    h->off_lqrf = carve((size_t)N * nz * lqrf_words(nx, nu));
     const size_t model_bytes = off;
     if (h->cond) {
         if (!nmpc::cond_build(nx, nu, N, ny, ny_e, h->A, h->B, h->c, h->H, h->G, h->He, h->Ge, h->lbnd, h->ubnd, h->ch)) {
@@ -886,9 +913,10 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     put(h->off_lb, h->lbnd);
     put(h->off_ub, h->ubnd);
     {
-        std::vector<double> lqr;
-        lqr_table(nx, nu, N, h->A, h->B, h->c, h->H, h->He, lqr);
+        std::vector<double> lqr, lqrf;
+        lqr_table(nx, nu, N, h->A, h->B, h->c, h->H, h->He, lqr, lqrf);
         put(h->off_lqr, lqr);
+        put(h->off_lqrf, lqrf);
     }
     if (h->cond) {
         const nmpc::CondHost &c = h->ch;

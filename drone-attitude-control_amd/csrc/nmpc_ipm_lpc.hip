@@ -402,6 +402,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // experiment builds only (build_experiment(..., ["NMPC_STEP_TIMING"]), env NMPC_SWEEP_CYCLES): clock
     // cycles of each phase of a closed-loop step, summed over the launch's steps: 0 certificate, 1
     // initial point, 2 finish Riccati, 3 finish forward, 4 IPM Riccati, 5 IPM B/C/D, 6 outputs, 7 advance
+    // (slot 0: the warm-flag copy and the fast finish; slot 1: certificate + initial point)
     unsigned long long st_cy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     for (int cstep = 0; cstep < nsteps; cstep++) {
@@ -493,9 +494,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // the IPM; otherwise it runs the full solve below.
         bool fast_ok = false;
         {
-            constexpr int W = NZ + 1, OQ = NZ;
+            // rollout records (p.lqrf, lqr_table): x-lane [q_r | K(:, r) | (B F_uu^{-1})(r, :) |
+            // (A + B K)(r, :)], u-lane [0 | 0 | F_uu^{-1}(u, :) | K(u, :)]
+            constexpr int WF = 1 + 2 * NU + NX, OM = 1, OW = 1 + NU, OR = 1 + 2 * NU;
             constexpr double FAST_TOL = 1e-13;
-            const bool try_fast = SP::hdiag && p.lqr != nullptr && p.g_diag && p.polish_mu > T(0) && warm && inst_ok &&
+            const bool try_fast = SP::hdiag && p.lqrf != nullptr && p.g_diag && p.polish_mu > T(0) && warm && inst_ok &&
                                   !prev_failed && warm_act == T(0) && p.fast_mode != 0 && (p.fast_mode == 1 || cstep > 0);
             if (__any(try_fast)) {
                 const T gdr = p.G[r * p.ny + r], gde = xl ? p.Ge[r * p.ny_e + r] : T(0);
@@ -505,87 +508,98 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 SpL<T, CN> acl;
                 if constexpr (SPARSE) sp_load(acl, slv, sli, col_base);
                 const T *acol = abt + r * LDX;
-                auto trow = [&](int k) { return p.lqr + ((size_t)k * NZ + r) * W; };
-                T pv = gde * yref[(size_t)N * yrow + (xl ? r : 0)];   // p_N = g_N (x-lanes)
-                for (int k = N - 1; k >= 0; k--) {
-                    const T *yk = yref + (size_t)k * yrow, *t_ = trow(k);
-                    const T gc = gdr * yk[r];
-                    T gu[NU], tr[NU];
+                auto frow = [&](int k, int lane) { return p.lqrf + ((size_t)k * NZ + lane) * WF; };
+                // backward, one LDS exchange per stage: v = p_{k+1} + q_k; every lane forms h_u; u-lanes
+                // kff_k = -F_uu^{-1} h_u, x-lanes d_k = B kff_k = -(B F_uu^{-1}) h_u (their rollout
+                // offset), both into the lane's DZ word; x-lanes p_k = h_x + K_k' h_u
+                struct Bk {
+                    T y, yu[NU], m[NU], w[NU], q;
+                };
+                auto bload = [&](int k, Bk &b) {
+                    const T *yk = yref + (size_t)k * yrow, *t_ = frow(k, r);
+                    b.y = yk[r];
+                    b.q = t_[0];
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
-                        gu[i] = gdu[i] * yk[NX + i];
-                        tr[i] = t_[(xl ? NX : 0) + i];   // x-lane: K(i, r); u-lane: F_uu^{-1}(u, i)
+                        b.yu[i] = yk[NX + i];
+                        b.m[i] = t_[OM + i];
+                        b.w[i] = t_[OW + i];
                     }
-                    if (xl) vb[r] = pv + t_[OQ];
+                };
+                T pv = gde * yref[(size_t)N * yrow + (xl ? r : 0)];   // p_N = g_N (x-lanes)
+                Bk bc;
+                bload(N - 1, bc);
+                for (int k = N - 1; k >= 0; k--) {
+                    Bk bn;
+                    bload(k > 0 ? k - 1 : 0, bn);   // next stage's inputs, in flight during this stage
+                    if (xl) vb[r] = pv + bc.q;
                     LPC_SYNC();
                     T hu[NU];
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
+                        const T gu = gdu[i] * bc.yu[i];
                         if constexpr (SPARSE) {
-                            SpL<T, CN> bc;
-                            sp_load(bc, slv, sli, NX * RN + (NX + i) * CN);
-                            hu[i] = sp_dot(bc, vb, gu[i]);
+                            SpL<T, CN> bcl;
+                            sp_load(bcl, slv, sli, NX * RN + (NX + i) * CN);
+                            hu[i] = sp_dot(bcl, vb, gu);
                         } else {
-                            T s0 = gu[i];
+                            T s0 = gu;
 #pragma unroll
                             for (int l = 0; l < NX; l++) s0 = fma(abt[(NX + i) * LDX + l], vb[l], s0);
                             hu[i] = s0;
                         }
                     }
-                    if (ul) {
-                        T kf = 0;
+                    T dk = 0;   // u-lane: kff_k(u); x-lane: (B kff_k)(r)
 #pragma unroll
-                        for (int i = 0; i < NU; i++) kf = fma(-tr[i], hu[i], kf);
-                        stU(k, UKFF, kf);
+                    for (int j = 0; j < NU; j++) dk = fma(-bc.w[j], hu[j], dk);
+                    T h;
+                    if constexpr (SPARSE) {
+                        h = sp_dot(acl, vb, gdr * bc.y);
                     } else {
-                        T h;
-                        if constexpr (SPARSE) {
-                            h = sp_dot(acl, vb, gc);
-                        } else {
-                            T h0 = gc, h1 = 0;
+                        T h0 = gdr * bc.y, h1 = 0;
 #pragma unroll
-                            for (int i = 0; i + 1 < NX; i += 2) {
-                                h0 = fma(acol[i], vb[i], h0);
-                                h1 = fma(acol[i + 1], vb[i + 1], h1);
-                            }
-                            if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
-                            h = h0 + h1;
+                        for (int i = 0; i + 1 < NX; i += 2) {
+                            h0 = fma(acol[i], vb[i], h0);
+                            h1 = fma(acol[i + 1], vb[i + 1], h1);
                         }
-#pragma unroll
-                        for (int i = 0; i < NU; i++) h = fma(tr[i], hu[i], h);
-                        pv = h;
+                        if (NX % 2) h0 = fma(acol[NX - 1], vb[NX - 1], h0);
+                        h = h0 + h1;
                     }
-                    LPC_SYNC();   // vb is rewritten by the next stage
-                }
-                // forward rollout with the acceptance test and the outputs
-                T *part = gb + Gm::G_MT;   // [NX][LDU] partial products K(u, j) x_j
-                T xk = x0r, nbad = 0;
-                T kq[NU], kfn = ldU(0, UKFF);
 #pragma unroll
-                for (int i = 0; i < NU; i++) kq[i] = trow(0)[NX + i];
+                    for (int i = 0; i < NU; i++) h = fma(bc.m[i], hu[i], h);
+                    pv = h;
+                    stE(L::DZ, k, dk);
+                    bc = bn;
+                }
+                // forward rollout, one LDS exchange per stage (x_k, two alternating buffers):
+                // x_{k+1} = (A + B K_k) x_k + B kff_k + c, u_k = kff_k + K_k x_k; bound test, outputs
+                T xk = x0r, nbad = 0;
+                T fr[NX], frn[NX], dd = ldE(L::DZ, 0), ddn;
+                {
+                    const T *t_ = frow(0, r);
+#pragma unroll
+                    for (int j = 0; j < NX; j++) fr[j] = t_[OR + j];
+                }
                 const Bd b0 = bnd(0), bm = bnd(1);
                 for (int k = 0; k < N; k++) {
-                    const T kf = kfn;
-                    T kqn[NU];
                     const int kn = k + 1 < N ? k + 1 : k;
-                    kfn = ldU(kn, UKFF);
-#pragma unroll
-                    for (int i = 0; i < NU; i++) kqn[i] = trow(kn)[NX + i];
                     {
-                        const int pr_ = xl ? r : NX;   // u-lanes write the spare row
+                        const T *t_ = frow(kn, r);
 #pragma unroll
-                        for (int i = 0; i < NU; i++) part[pr_ * LDU + i] = kq[i] * xk;
+                        for (int j = 0; j < NX; j++) frn[j] = t_[OR + j];
+                        ddn = ldE(L::DZ, kn);
                     }
+                    T *xb = gb + Gm::G_MT + (k & 1) * LDZ;
+                    if (xl) xb[r] = xk;
                     LPC_SYNC();
-                    T uk = kf;
-                    {
-                        const int uu = ul ? u : 0;
+                    T s0 = dd, s1 = 0;
 #pragma unroll
-                        for (int jj = 0; jj < NX; jj++) uk += part[jj * LDU + uu];
+                    for (int j = 0; j + 1 < NX; j += 2) {
+                        s0 = fma(fr[j], xb[j], s0);
+                        s1 = fma(fr[j + 1], xb[j + 1], s1);
                     }
-                    const T z = xl ? xk : uk;
-                    zb[r] = z;
-                    LPC_SYNC();
+                    if (NX % 2) s0 = fma(fr[NX - 1], xb[NX - 1], s0);
+                    const T z = xl ? xk : s0 + s1;   // u-lane: u_k = kff + K(u, :) x_k
                     const Bd bk = k == 0 ? b0 : bm;
                     // stricter than the finish's 1e-9: a bound violated inside that band goes through the
                     // full solve, whose rounding decides it exactly as without the fast path
@@ -593,23 +607,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     nbad += (!isfinite(z) || (has_bound(bk.lb) && z < bk.lb - tl) || (has_bound(bk.ub) && z > bk.ub + tu))
                                 ? T(1) : T(0);
                     if (try_fast) fin_out(k, z, bk);
-                    T xn;
-                    if constexpr (SPARSE) {
-                        xn = sp_dot(arl0, zb, c_r);
-                    } else {
-                        T s0 = c_r, s1 = 0;
+                    xk = xl ? s0 + s1 + c_r : xk;   // x-lane: x_{k+1} = (A + B K) x_k + d_k + c
 #pragma unroll
-                        for (int jj = 0; jj + 1 < NZ; jj += 2) {
-                            s0 = fma(abr[(xl ? r : 0) * LDZ + jj], zb[jj], s0);
-                            s1 = fma(abr[(xl ? r : 0) * LDZ + jj + 1], zb[jj + 1], s1);
-                        }
-                        if (NZ % 2) s0 = fma(abr[(xl ? r : 0) * LDZ + NZ - 1], zb[NZ - 1], s0);
-                        xn = s0 + s1;
-                    }
-                    xk = xn;
-#pragma unroll
-                    for (int i = 0; i < NU; i++) kq[i] = kqn[i];
-                    LPC_SYNC();   // zb / part are rewritten by the next stage
+                    for (int j = 0; j < NX; j++) fr[j] = frn[j];
+                    dd = ddn;
                 }
                 if (xl) {
                     const Bd bN = bnd(N);
@@ -624,6 +625,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             }
         }
         const bool need_full = __any(inst_ok && !fast_ok);
+        LPC_STICK(0);
         // ------------------------------------------------------------------ infeasibility certificate
         // interval reachability (oracle/c/riccati_ipm.c infeasible_stage): x-lane r carries the
         // midpoint / radius of state r of X_k, u-lanes the input box; X_{k+1} = hull([A B] X_k x U
@@ -676,7 +678,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             }
             infeas = gmax(infeas ? T(1) : T(0)) > T(0);
         }
-        LPC_STICK(0);
+        LPC_STICK(1);
         // ------------------------------------------------------------------ initial point
         // y = z with diagonal W (p.g_diag, every reference model): g_c = G_rr y_r from the lane's own
         // y component; stage rows are loaded YC stages at a time (one memory latency per chunk)
