@@ -213,7 +213,7 @@ struct nmpc_solver {
     int *d_status = nullptr, *d_iters = nullptr;
     unsigned long long *d_cycles = nullptr;
     size_t off_AB = 0, off_ABt = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
-    size_t off_lqr = 0, off_lqrf = 0;   // unconstrained Riccati records per stage (lqr_table)
+    size_t off_lqr = 0, off_lqrf = 0, off_lqrw = 0;   // unconstrained Riccati records (lqr_table, lqr_wmat)
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
     bool cl_ready = false;
@@ -355,6 +355,66 @@ void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::v
     }
 }
 
+// The projected inverse Hessian of the unconstrained LQ problem, ne = (N+1) nz elements e = k nz + r
+// (x_0 pinned: its rows and columns are zero; stage N has no inputs): column e' is minus the
+// solution of the homogeneous problem (x_0 = 0, c = 0) with a unit gradient at e', so the solution
+// with the bounds of a set S held, z = z_0 + W[:, S] nu, W_SS nu = b_S - z_0,S, has the multipliers
+// nu (the fast finish's active-set steps). Column-major, from the factorisation in tab.
+void lqr_wmat(int nx, int nu, int N, const std::vector<double> &A, const std::vector<double> &B,
+              const std::vector<double> &tab, std::vector<double> &w)
+{
+    const int nz = nx + nu, W = lqr_words(nx, nu), ne = (N + 1) * nz;
+    w.assign((size_t)ne * ne, 0.0);
+    auto ab = [&](int l, int c) { return c < nx ? A[l * nx + c] : B[l * nu + (c - nx)]; };
+    std::vector<double> kff((size_t)N * nu), z((size_t)ne);
+    for (int e1 = 0; e1 < ne; e1++) {
+        const int k1 = e1 / nz, r1 = e1 % nz;
+        if ((k1 == 0 && r1 < nx) || (k1 == N && r1 >= nx)) continue;
+        std::vector<double> p(nx, 0.0), h(nz);
+        if (k1 == N) p[r1] = 1.0;
+        for (int k = N - 1; k >= 0; k--) {
+            const double *t = &tab[(size_t)k * nz * W];
+            for (int i = 0; i < nz; i++) {
+                double s_ = (k == k1 && i == r1) ? 1.0 : 0.0;
+                for (int l = 0; l < nx; l++) s_ += ab(l, i) * p[l];
+                h[i] = s_;
+            }
+            for (int u = 0; u < nu; u++) {
+                double s_ = 0.0;
+                for (int i = 0; i < nu; i++) s_ -= t[(nx + u) * W + i] * h[nx + i];
+                kff[(size_t)k * nu + u] = s_;
+            }
+            for (int j = 0; j < nx; j++) {
+                double s_ = h[j];
+                for (int i = 0; i < nu; i++) s_ += t[j * W + nx + i] * h[nx + i];
+                p[j] = s_;
+            }
+        }
+        std::vector<double> x(nx, 0.0), xn(nx);
+        for (int k = 0; k < N; k++) {
+            const double *t = &tab[(size_t)k * nz * W];
+            double uu[64];
+            for (int u = 0; u < nu; u++) {
+                double s_ = kff[(size_t)k * nu + u];
+                for (int j = 0; j < nx; j++) s_ += t[j * W + nx + u] * x[j];
+                uu[u] = s_;
+            }
+            for (int j = 0; j < nx; j++) z[(size_t)k * nz + j] = x[j];
+            for (int u = 0; u < nu; u++) z[(size_t)k * nz + nx + u] = uu[u];
+            for (int i = 0; i < nx; i++) {
+                double s_ = 0.0;
+                for (int j = 0; j < nx; j++) s_ += A[i * nx + j] * x[j];
+                for (int u = 0; u < nu; u++) s_ += B[i * nu + u] * uu[u];
+                xn[i] = s_;
+            }
+            x = xn;
+        }
+        for (int j = 0; j < nx; j++) z[(size_t)N * nz + j] = x[j];
+        for (int j = 0; j < nu; j++) z[(size_t)N * nz + nx + j] = 0.0;
+        for (int e = 0; e < ne; e++) w[(size_t)e1 * ne + e] = (e < nx) ? 0.0 : -z[e];
+    }
+}
+
 int hip_fail(nmpc_solver *h, hipError_t e, const char *what)
 {
     return h->fail(NMPC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
@@ -492,6 +552,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     const bool no_lqr = std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0';
     p.lqr = no_lqr ? nullptr : (const T *)(m + h->off_lqr);
     p.lqrf = no_lqr ? nullptr : (const T *)(m + h->off_lqrf);
+    const bool no_w = std::getenv("NMPC_WSET") && std::getenv("NMPC_WSET")[0] == '0';
+    p.lqrw = (no_lqr || no_w) ? nullptr : (const T *)(m + h->off_lqrw);
     p.x0 = (const T *)h->d_x0;
     p.yref = (const T *)h->d_yref;
     p.xout = (T *)h->d_x;
@@ -833,6 +895,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_ub = carve(3 * nz);
     h->off_lqr = carve((size_t)N * nz * lqr_words(nx, nu));
     h->off_lqrf = carve((size_t)N * nz * lqrf_words(nx, nu));
+    h->off_lqrw = carve((size_t)(N + 1) * nz * (N + 1) * nz);
     const size_t model_bytes = off;
     if (h->cond) {
         if (!nmpc::cond_build(nx, nu, N, ny, ny_e, h->A, h->B, h->c, h->H, h->G, h->He, h->Ge, h->lbnd, h->ubnd, h->ch)) {
@@ -917,6 +980,9 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         lqr_table(nx, nu, N, h->A, h->B, h->c, h->H, h->He, lqr, lqrf);
         put(h->off_lqr, lqr);
         put(h->off_lqrf, lqrf);
+        std::vector<double> wm;
+        lqr_wmat(nx, nu, N, h->A, h->B, lqr, wm);
+        put(h->off_lqrw, wm);
     }
     if (h->cond) {
         const nmpc::CondHost &c = h->ch;

@@ -63,6 +63,7 @@ struct IpmParams {
     const T *ubnd;  // [3][nz]
     const T *lqr;   // [N][nz][nz+1] unconstrained Riccati records (nmpc_api.cpp lqr_table), or null
     const T *lqrf;  // [N][nz][1+2nu+nx] the fast finish's rollout records (lqr_table), or null
+    const T *lqrw;  // [(N+1)nz]^2 projected inverse Hessian of the unconstrained problem (lqr_wmat), or null
     const T *x0;    // [B][nx]
     const T *yref;  // [B][N*ny + ny_e]
     T *xout;        // [B][N+1][nx]

@@ -493,13 +493,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // (status 0, one Newton system) and the group skips the certificate, the initial point and
         // the IPM; otherwise it runs the full solve below.
         bool fast_ok = false;
+        int fin_ws = 0;   // active-set steps on the shared factorisation (counted in qp_iter)
         {
             // rollout records (p.lqrf, lqr_table): x-lane [q_r | K(:, r) | (B F_uu^{-1})(r, :) |
             // (A + B K)(r, :)], u-lane [0 | 0 | F_uu^{-1}(u, :) | K(u, :)]
             constexpr int WF = 1 + 2 * NU + NX, OM = 1, OW = 1 + NU, OR = 1 + 2 * NU;
             constexpr double FAST_TOL = 1e-13;
             const bool try_fast = SP::hdiag && p.lqrf != nullptr && p.g_diag && p.polish_mu > T(0) && warm && inst_ok &&
-                                  !prev_failed && warm_act == T(0) && p.fast_mode != 0 && (p.fast_mode == 1 || cstep > 0);
+                                  !prev_failed && p.fast_mode != 0 && (p.fast_mode == 1 || cstep > 0) &&
+                                  (warm_act == T(0) || p.lqrw != nullptr);
+            const bool empty0 = warm_act == T(0);   // the unconstrained solution is the first set step
             if (__any(try_fast)) {
                 const T gdr = p.G[r * p.ny + r], gde = xl ? p.Ge[r * p.ny_e + r] : T(0);
                 T gdu[NU];
@@ -574,6 +577,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 // forward rollout, one LDS exchange per stage (x_k, two alternating buffers):
                 // x_{k+1} = (A + B K_k) x_k + B kff_k + c, u_k = kff_k + K_k x_k; bound test, outputs
                 T xk = x0r, nbad = 0;
+                T wcv = 0, wcs = 0;   // the lane's most violated stage (state lanes: the set's first member)
+                int wck = -1;
                 T fr[NX], frn[NX], dd = ldE(L::DZ, 0), ddn;
                 {
                     const T *t_ = frow(0, r);
@@ -604,9 +609,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     // stricter than the finish's 1e-9: a bound violated inside that band goes through the
                     // full solve, whose rounding decides it exactly as without the fast path
                     const T tl = T(FAST_TOL) * (T(1) + fabs(bk.lb)), tu = T(FAST_TOL) * (T(1) + fabs(bk.ub));
-                    nbad += (!isfinite(z) || (has_bound(bk.lb) && z < bk.lb - tl) || (has_bound(bk.ub) && z > bk.ub + tu))
-                                ? T(1) : T(0);
-                    if (try_fast) fin_out(k, z, bk);
+                    const bool lo_ = has_bound(bk.lb) && z < bk.lb - tl, hi_ = has_bound(bk.ub) && z > bk.ub + tu;
+                    nbad += (!isfinite(z) || lo_ || hi_) ? T(1) : T(0);
+                    stE(L::Z, k, z);   // z_0 of the active-set steps below
+                    if (try_fast && empty0) {
+                        fin_out(k, z, bk);
+                        // first set of the active-set steps: violated inputs, each state's most violated stage
+                        const T v_ = lo_ ? bk.lb - z : (hi_ ? z - bk.ub : T(0));
+                        if (ul) stE(L::DZA, k, lo_ ? T(-1) : (hi_ ? T(1) : T(0)));
+                        wck = v_ > wcv ? k : wck;
+                        wcs = v_ > wcv ? (lo_ ? T(-1) : T(1)) : wcs;
+                        wcv = fmax(wcv, v_);
+                    }
                     xk = xl ? s0 + s1 + c_r : xk;   // x-lane: x_{k+1} = (A + B K) x_k + d_k + c
 #pragma unroll
                     for (int j = 0; j < NX; j++) fr[j] = frn[j];
@@ -615,12 +629,158 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 if (xl) {
                     const Bd bN = bnd(N);
                     const T tl = T(FAST_TOL) * (T(1) + fabs(bN.lb)), tu = T(FAST_TOL) * (T(1) + fabs(bN.ub));
-                    nbad += (!isfinite(xk) || (has_bound(bN.lb) && xk < bN.lb - tl) || (has_bound(bN.ub) && xk > bN.ub + tu))
-                                ? T(1) : T(0);
-                    if (try_fast) fin_out(N, xk, bN);
+                    const bool lo_ = has_bound(bN.lb) && xk < bN.lb - tl, hi_ = has_bound(bN.ub) && xk > bN.ub + tu;
+                    nbad += (!isfinite(xk) || lo_ || hi_) ? T(1) : T(0);
+                    stE(L::Z, N, xk);
+                    if (try_fast && empty0) {
+                        fin_out(N, xk, bN);
+                        const T v_ = lo_ ? bN.lb - xk : (hi_ ? xk - bN.ub : T(0));
+                        wck = v_ > wcv ? N : wck;
+                        wcs = v_ > wcv ? (lo_ ? T(-1) : T(1)) : wcs;
+                        wcv = fmax(wcv, v_);
+                    }
                 }
+                if (try_fast && empty0 && xl && wck >= 0) stE(L::DZA, wck, wcs);
                 nbad = gsum(nbad);
-                fast_ok = try_fast && nbad == T(0);
+                fast_ok = try_fast && empty0 && nbad == T(0);
+                // ---- active-set steps on the shared factorisation (p.lqrw): S = the flagged bounds
+                // (DZA: the warm-start set, or the first set from the unconstrained solution's
+                // violations), z = z_0 + W[:, S] nu with W_SS nu = b_S - z_0,S — the exact solution with S
+                // held, its multipliers nu. Accepted when every other bound holds and every multiplier has
+                // its sign (the finish's KKT test, no penalty and no refinement); otherwise the PDAS update
+                // of the finish. At most polish_steps steps and sets of at most WSMAX bounds; a group that
+                // ends unaccepted runs the full solve below from the set it reached.
+                fin_ws = 0;
+                bool wrun = try_fast && !fast_ok && p.lqrw != nullptr;
+                for (int ws = 0; ws < p.polish_steps && __any(wrun); ws++) {
+                    constexpr int WSMAX = 8;
+                    const int ne = (N + 1) * NZ;
+                    // the set: per-lane count, group prefix, entries in LDS (element, sign, b - z_0)
+                    T *le = gb + Gm::G_MT;                       // [WSMAX] element index
+                    T *ls = le + WSMAX, *lt = ls + WSMAX;        // [WSMAX] sign, [WSMAX] target step
+                    int nmine = 0;
+                    for (int k = 0; k <= N; k++) nmine += (k < N || xl) && !(k == 0 && xl) && ldE(L::DZA, k) != T(0);
+                    int pre = nmine;
+#pragma unroll
+                    for (int sh = 1; sh < NZ; sh <<= 1) {
+                        const int o = __shfl(pre, lane - sh >= 0 ? lane - sh : 0, 64);
+                        pre += r >= sh ? o : 0;
+                    }
+                    const int m = (int)gsum(r == NZ - 1 ? T(pre) : T(0));   // the last lane's prefix = |S|
+                    pre -= nmine;   // exclusive prefix
+                    LPC_SYNC();
+                    if (wrun && m <= WSMAX) {
+                        int q_ = pre;
+                        for (int k = 0; k <= N; k++) {
+                            const T f = ((k < N || xl) && !(k == 0 && xl)) ? ldE(L::DZA, k) : T(0);
+                            if (f != T(0)) {
+                                const Bd b_ = bnd(k);
+                                le[q_] = T(k * NZ + r);
+                                ls[q_] = f;
+                                lt[q_] = (f < T(0) ? b_.lb : b_.ub) - ldE(L::Z, k);
+                                q_++;
+                            }
+                        }
+                    }
+                    LPC_SYNC();
+                    wrun = wrun && m >= 1 && m <= WSMAX;
+                    // nu = W_SS^{-1} (b - z_0)_S by Cholesky, every lane (m <= WSMAX)
+                    T L_[WSMAX][WSMAX], nu_[WSMAX];
+                    int ei[WSMAX];
+#pragma unroll
+                    for (int i = 0; i < WSMAX; i++) {
+                        ei[i] = (wrun && i < m) ? (int)le[i] : 0;
+                        nu_[i] = (wrun && i < m) ? lt[i] : T(0);
+                    }
+                    bool pdf = true;
+#pragma unroll
+                    for (int i = 0; i < WSMAX; i++)
+#pragma unroll
+                        for (int j = 0; j <= i; j++) {
+                            T s_ = (i < m && j < m) ? p.lqrw[(size_t)ei[j] * ne + ei[i]] : (i == j ? T(1) : T(0));
+#pragma unroll
+                            for (int l = 0; l < j; l++) s_ = fma(-L_[i][l], L_[j][l], s_);
+                            if (i == j) {
+                                pdf = pdf && s_ > T(0);
+                                L_[i][i] = s_ > T(0) ? sqrt(s_) : T(1);
+                            } else {
+                                L_[i][j] = s_ / L_[j][j];
+                            }
+                        }
+#pragma unroll
+                    for (int i = 0; i < WSMAX; i++) {
+                        T s_ = nu_[i];
+#pragma unroll
+                        for (int l = 0; l < i; l++) s_ = fma(-L_[i][l], nu_[l], s_);
+                        nu_[i] = s_ / L_[i][i];
+                    }
+#pragma unroll
+                    for (int i = WSMAX - 1; i >= 0; i--) {
+                        T s_ = nu_[i];
+#pragma unroll
+                        for (int l = i + 1; l < WSMAX; l++) s_ = fma(-L_[l][i], nu_[l], s_);
+                        nu_[i] = s_ / L_[i][i];
+                    }
+                    wrun = wrun && pdf;
+                    // multiplier signs (lower: nu >= 0, upper: nu <= 0, to the finish's few-ulp tolerance)
+                    int nrem = 0;
+                    bool remk[WSMAX];
+#pragma unroll
+                    for (int i = 0; i < WSMAX; i++) {
+                        const T f = (i < m) ? ls[i] : T(0);
+                        const T tol_ = p.polish_rho * T(1e-15) * (T(1) + fabs(lt[i]));
+                        remk[i] = i < m && ((f < T(0) && nu_[i] < -tol_) || (f > T(0) && nu_[i] > tol_) || !isfinite(nu_[i]));
+                        nrem += remk[i] ? 1 : 0;
+                    }
+                    // z = z_0 + W[:, S] nu at the lane's elements: bounds, the next set, tentative outputs
+                    T wbad = T(nrem), cv2 = 0, cs2 = 0;
+                    int ck2 = -1;
+                    const bool addok = ws == 0 || nrem == 0;
+                    for (int k = 0; k <= N; k++) {
+                        if (k == N && ul) break;
+                        const int e = k * NZ + r;
+                        T z = ldE(L::Z, k);
+#pragma unroll
+                        for (int i = 0; i < WSMAX; i++)
+                            if (i < m) z = fma(p.lqrw[(size_t)ei[i] * ne + e], nu_[i], z);
+                        const Bd b_ = bnd(k);
+                        const T f = ldE(L::DZA, k);
+                        T nf = f;
+                        if (f != T(0)) {
+                            // held: z_0 + W[:, S] nu lands on the bound up to the solve's rounding (1e-9, the
+                            // refinement's test); then exactly on it
+                            const T bb = f < T(0) ? b_.lb : b_.ub;
+                            wbad += (!(fabs(z - bb) <= T(1e-9) * (T(1) + fabs(bb)))) ? T(1) : T(0);
+                            z = bb;
+#pragma unroll
+                            for (int i = 0; i < WSMAX; i++)
+                                if (remk[i] && ei[i] == e) nf = T(0);
+                        } else if (!(k == 0 && xl)) {
+                            const T tl = T(1e-13) * (T(1) + fabs(b_.lb)), tu = T(1e-13) * (T(1) + fabs(b_.ub));
+                            const bool lo_ = has_bound(b_.lb) && z < b_.lb - tl, hi_ = has_bound(b_.ub) && z > b_.ub + tu;
+                            wbad += (lo_ || hi_ || !isfinite(z)) ? T(1) : T(0);
+                            const T v_ = lo_ ? b_.lb - z : (hi_ ? z - b_.ub : T(0));
+                            if (ul && addok && (lo_ || hi_)) nf = lo_ ? T(-1) : T(1);
+                            ck2 = v_ > cv2 ? k : ck2;
+                            cs2 = v_ > cv2 ? (lo_ ? T(-1) : T(1)) : cs2;
+                            cv2 = fmax(cv2, v_);
+                        }
+                        if (wrun) {
+                            if (nf != f) stE(L::DZA, k, nf);
+                            fin_out(k, z, b_);
+                        }
+                    }
+                    if (wrun && xl && addok && ck2 >= 0) stE(L::DZA, ck2, cs2);
+                    wbad = gsum(wbad);
+                    fin_ws += wrun ? 1 : 0;
+                    const bool acc = wrun && wbad == T(0);
+                    fast_ok = fast_ok || acc;
+                    wrun = wrun && !acc;
+                    LPC_SYNC();
+                }
+                // a group that took active-set steps left its last set in DZA: the full solve's first
+                // finish step starts from it (never as an empty set)
+                if (fin_ws > 0) warm_act = T(1);
                 if (fastpl) cly[r] = yref[xl || r < p.ny ? r : 0];   // yref row 0 (cost / AED reference)
             }
         }
@@ -786,7 +946,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         T theta = 1;
         bool active = inst_ok && !infeas && !fast_ok;
         // certified infeasible: status 4, the initial point; completed by the fast finish: status -1
-        int status = fast_ok ? -1 : (infeas ? 4 : 2), iters = fast_ok ? 1 : 0;
+        int status = fast_ok ? -1 : (infeas ? 4 : 2), iters = fast_ok ? 1 + fin_ws : 0;
         bool fail = false, pending = false;
         T alpha = 0, smu = 0;
         // exact finish (oracle/c/riccati_ipm.c "exact finish"): a primal-dual active-set run of at
@@ -797,7 +957,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         // its correction. status -1: completed by the finish, outputs = Z + DZ + DZA (B and D skip
         // the group's DZA / DZ)
         T polish_at = p.polish_mu;
-        int fin_steps = fast_ok ? 1 : 0, fin_runs = 0;
+        int fin_steps = fast_ok ? 1 + fin_ws : 0, fin_runs = 0;
         bool pol = false, fref = false;
         bool fs0 = false;   // wave-uniform: the current finish pass is the first step of its runs
 
