@@ -1296,7 +1296,10 @@ static int kernel_kind(int nx, int nu, int batch)
     const int nz = nx + nu;
     if (nz > 64) return 0;
     const long waves = ((long)batch + 64 / nz - 1) / (64 / nz);
-    return (nz >= 12 || waves >= 384) ? 1 : 0;
+    // round 2 (fast finish in the lane-per-component family): jerk (nz = 8) runs it faster from
+    // B = 1024 (6.8M vs 6.0M steps/s; B = 2048 12.8M vs 10.0M), force (nz = 6) still not at B = 1024
+    // (1.95M vs 3.5M: its input-saturation sets exceed the fast finish's 8 bounds)
+    return (nz >= 8 || waves >= 384) ? 1 : 0;
 }
 
 template <typename T>
