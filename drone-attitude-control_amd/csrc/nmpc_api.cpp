@@ -214,6 +214,8 @@ struct nmpc_solver {
     unsigned long long *d_cycles = nullptr;
     size_t off_AB = 0, off_ABt = 0, off_c = 0, off_H = 0, off_He = 0, off_G = 0, off_Ge = 0, off_lb = 0, off_ub = 0;
     size_t off_lqr = 0, off_lqrf = 0, off_lqrw = 0;   // unconstrained Riccati records (lqr_table, lqr_wmat)
+    std::vector<double> lqr_host;                      // the lqr_table records (host copy)
+    void *d_cltx = nullptr, *d_clv = nullptr;          // closed loop: explicit unconstrained solution (cl_explicit)
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
     bool cl_ready = false;
@@ -415,6 +417,57 @@ void lqr_wmat(int nx, int nu, int N, const std::vector<double> &A, const std::ve
     }
 }
 
+// The unconstrained LQ solution from base 0 (the fast finish's first step, oracle-free host form of
+// the kernel's recursion on the lqr_table records): gradient g (stage-stacked, nz per stage, stage N
+// nx), initial state x0, affine term c on or off. z: (N+1) nz.
+void lqr_solve(int nx, int nu, int N, const std::vector<double> &A, const std::vector<double> &B,
+               const std::vector<double> &c, const std::vector<double> &tab, const double *g, const double *x0,
+               bool use_c, double *z)
+{
+    const int nz = nx + nu, W = lqr_words(nx, nu);
+    auto ab = [&](int l, int q) { return q < nx ? A[l * nx + q] : B[l * nu + (q - nx)]; };
+    std::vector<double> p(g + (size_t)N * nz, g + (size_t)N * nz + nx), v(nx), h(nz), kff((size_t)N * nu);
+    for (int k = N - 1; k >= 0; k--) {
+        const double *t = &tab[(size_t)k * nz * W];
+        for (int r = 0; r < nx; r++) v[r] = p[r] + (use_c ? t[r * W + nz] : 0.0);
+        for (int i = 0; i < nz; i++) {
+            double s_ = g[(size_t)k * nz + i];
+            for (int l = 0; l < nx; l++) s_ += ab(l, i) * v[l];
+            h[i] = s_;
+        }
+        for (int u = 0; u < nu; u++) {
+            double s_ = 0.0;
+            for (int i = 0; i < nu; i++) s_ -= t[(nx + u) * W + i] * h[nx + i];
+            kff[(size_t)k * nu + u] = s_;
+        }
+        for (int j = 0; j < nx; j++) {
+            double s_ = h[j];
+            for (int i = 0; i < nu; i++) s_ += t[j * W + nx + i] * h[nx + i];
+            p[j] = s_;
+        }
+    }
+    std::vector<double> x(x0, x0 + nx), xn(nx), uu(nu);
+    for (int k = 0; k < N; k++) {
+        const double *t = &tab[(size_t)k * nz * W];
+        for (int u = 0; u < nu; u++) {
+            double s_ = kff[(size_t)k * nu + u];
+            for (int j = 0; j < nx; j++) s_ += t[j * W + nx + u] * x[j];
+            uu[u] = s_;
+        }
+        for (int j = 0; j < nx; j++) z[(size_t)k * nz + j] = x[j];
+        for (int u = 0; u < nu; u++) z[(size_t)k * nz + nx + u] = uu[u];
+        for (int i = 0; i < nx; i++) {
+            double s_ = use_c ? c[i] : 0.0;
+            for (int j = 0; j < nx; j++) s_ += A[i * nx + j] * x[j];
+            for (int u = 0; u < nu; u++) s_ += B[i * nu + u] * uu[u];
+            xn[i] = s_;
+        }
+        x = xn;
+    }
+    for (int j = 0; j < nx; j++) z[(size_t)N * nz + j] = x[j];
+    for (int u = 0; u < nu; u++) z[(size_t)N * nz + nx + u] = 0.0;
+}
+
 int hip_fail(nmpc_solver *h, hipError_t e, const char *what)
 {
     return h->fail(NMPC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
@@ -426,7 +479,7 @@ void free_all(nmpc_solver *h)
     for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
                     (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
-                    (void *)h->d_fnoise, (void *)h->d_iter_log})
+                    (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -514,6 +567,9 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
             hipMalloc((void **)&h->d_iter_log, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(int)) != hipSuccess)
             h->d_iter_log = nullptr;
         p.iter_log = iter_log ? h->d_iter_log : nullptr;
+        const bool no_expl = std::getenv("NMPC_EXPLICIT") && std::getenv("NMPC_EXPLICIT")[0] == '0';
+        p.cl_tx = no_expl ? nullptr : (const T *)h->d_cltx;
+        p.cl_v = no_expl ? nullptr : (const T *)h->d_clv;
         h->iter_log_steps = p.iter_log ? cl_steps : 0;
     }
     p.B = h->batch;
@@ -976,7 +1032,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     put(h->off_lb, h->lbnd);
     put(h->off_ub, h->ubnd);
     {
-        std::vector<double> lqr, lqrf;
+        std::vector<double> &lqr = h->lqr_host, lqrf;
         lqr_table(nx, nu, N, h->A, h->B, h->c, h->H, h->He, lqr, lqrf);
         put(h->off_lqr, lqr);
         put(h->off_lqrf, lqrf);
@@ -1462,6 +1518,42 @@ int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d)
         e = hipMemcpy(h->d_noise, d->noise_table, (size_t)h->batch * d->noise_len * sizeof(double),
                       hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init upload");
+    // explicit unconstrained solution for the fused closed loop's fast finish: z_0 = T_x x_0 + v_t, v_t
+    // the response to the reference window starting at table row t (t < ref_period) and to c
+    if (h->d_cltx) hipFree(h->d_cltx);
+    if (h->d_clv) hipFree(h->d_clv);
+    h->d_cltx = h->d_clv = nullptr;
+    if (!h->cond && !h->lqr_host.empty()) {
+        const int N = h->N, nz = nx + nu, ne = (N + 1) * nz, ny = h->ny, nye = h->ny_e, P_ = d->ref_period;
+        std::vector<double> tx((size_t)ne * nx), vv((size_t)P_ * ne), g((size_t)ne, 0.0), z((size_t)ne), e0(nx);
+        for (int j = 0; j < nx; j++) {
+            std::fill(e0.begin(), e0.end(), 0.0);
+            e0[j] = 1.0;
+            lqr_solve(nx, nu, N, h->A, h->B, h->c, h->lqr_host, g.data(), e0.data(), false, z.data());
+            for (int e = 0; e < ne; e++) tx[(size_t)e * nx + j] = z[e];
+        }
+        std::fill(e0.begin(), e0.end(), 0.0);
+        for (int t = 0; t < P_; t++) {
+            std::fill(g.begin(), g.end(), 0.0);
+            for (int k = 0; k <= N; k++) {
+                const double *y = d->ref_table + (size_t)(t + k) * d->ref_cols;
+                const int n = k < N ? nz : nx, m = k < N ? ny : nye;
+                const double *Gm = k < N ? h->G.data() : h->Ge.data();
+                for (int i = 0; i < n; i++) {
+                    double s_ = 0.0;
+                    for (int q = 0; q < m; q++) s_ += Gm[i * m + q] * y[q];
+                    g[(size_t)k * nz + i] = s_;
+                }
+            }
+            lqr_solve(nx, nu, N, h->A, h->B, h->c, h->lqr_host, g.data(), e0.data(), true, z.data());
+            std::copy(z.begin(), z.end(), vv.begin() + (size_t)t * ne);
+        }
+        if (hipMalloc(&h->d_cltx, tx.size() * es) != hipSuccess || hipMalloc(&h->d_clv, vv.size() * es) != hipSuccess)
+            return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: explicit-solution tables");
+        e = put_typed(h->d_cltx, tx.data(), tx.size(), f64);
+        if (e == hipSuccess) e = put_typed(h->d_clv, vv.data(), vv.size(), f64);
+        if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init explicit tables");
+    }
     h->cl = *d;
     h->cl.ref_table = nullptr;
     h->cl.offsets = nullptr;

@@ -81,6 +81,9 @@ struct IpmParams {
     ClParams<T> cl;
     const double *cl_noise;   // [B][cl_steps] noise draws of the launch's steps (cl_noise_launch)
     int *iter_log;            // optional [cl_steps][B]: finish steps | IPM iterations << 8 | status << 16 per fused step
+    // fused closed loop, explicit unconstrained solution (nmpc_closed_loop_init): z_0 = T_x x_0 + v_t
+    const T *cl_tx;           // [(N+1) nz][nx]
+    const T *cl_v;            // [period][(N+1) nz]
 };
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);

@@ -480,6 +480,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         }
         warm_act = gsum(warm_act);
     }
+#ifdef NMPC_STEP_SPLIT
+    LPC_STICK(4);   // experiment builds: the warm-flag copy
+#endif
 
 
         // ------------------------------------------------------------------ fast exact finish
@@ -529,6 +532,68 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         b.w[i] = t_[OW + i];
                     }
                 };
+                // the bound test of the unconstrained solution at element (k, r), its z_0 word, the
+                // tentative outputs and the first set of the active-set steps (violated inputs, each
+                // state's most violated stage)
+                T nbad = 0;
+                T wcv = 0, wcs = 0;
+                int wck = -1;
+                auto fcheck = [&](int k, T z, const Bd &bk) {
+                    // stricter than the finish's 1e-9: a bound violated inside that band goes through the
+                    // full solve, whose rounding decides it exactly as without the fast path
+                    const T tl = T(FAST_TOL) * (T(1) + fabs(bk.lb)), tu = T(FAST_TOL) * (T(1) + fabs(bk.ub));
+                    const bool lo_ = has_bound(bk.lb) && z < bk.lb - tl, hi_ = has_bound(bk.ub) && z > bk.ub + tu;
+                    nbad += (!isfinite(z) || lo_ || hi_) ? T(1) : T(0);
+                    stE(L::Z, k, z);   // z_0 of the active-set steps below
+                    if (try_fast && empty0) {
+                        fin_out(k, z, bk);
+                        const T v_ = lo_ ? bk.lb - z : (hi_ ? z - bk.ub : T(0));
+                        if (ul) stE(L::DZA, k, lo_ ? T(-1) : (hi_ ? T(1) : T(0)));
+                        wck = v_ > wcv ? k : wck;
+                        wcs = v_ > wcv ? (lo_ ? T(-1) : T(1)) : wcs;
+                        wcv = fmax(wcv, v_);
+                    }
+                };
+                if (p.cl_tx != nullptr) {
+                    // explicit form (nmpc_closed_loop_init): the unconstrained solution is linear in x_0
+                    // and the reference window, z_0 = T_x x_0 + v_t with v_t per reference row t (the
+                    // closed loop's yref windows are rows of its table), so each lane forms its elements
+                    // directly — one LDS exchange (x_0) per step, no recursion
+                    T *xb = gb + Gm::G_MT;
+                    if (xl) xb[r] = x0r;
+                    LPC_SYNC();
+                    T x0v[NX];
+#pragma unroll
+                    for (int j = 0; j < NX; j++) x0v[j] = xb[j];
+                    const int ne = (N + 1) * NZ;
+                    const T *vt = p.cl_v + (size_t)t_ref * ne;
+                    const Bd b0 = bnd(0), bm = bnd(1), bN = bnd(N);
+                    constexpr int EC = 4;
+                    for (int kc = 0; kc <= N; kc += EC) {
+                        T zc[EC];
+#pragma unroll
+                        for (int j = 0; j < EC; j++) {
+                            const int k = kc + j <= N ? kc + j : N, e = k * NZ + r;
+                            const T *tx = p.cl_tx + (size_t)e * NX;
+                            T s0 = vt[e], s1 = 0;
+#pragma unroll
+                            for (int jj = 0; jj + 1 < NX; jj += 2) {
+                                s0 = fma(tx[jj], x0v[jj], s0);
+                                s1 = fma(tx[jj + 1], x0v[jj + 1], s1);
+                            }
+                            if (NX % 2) s0 = fma(tx[NX - 1], x0v[NX - 1], s0);
+                            zc[j] = s0 + s1;
+                        }
+#pragma unroll
+                        for (int j = 0; j < EC; j++) {
+                            const int k = kc + j;
+                            if (k > N) break;
+                            if (k == N && ul) continue;
+                            fcheck(k, (k == 0 && xl) ? x0r : zc[j], k == 0 ? b0 : (k == N ? bN : bm));
+                        }
+                    }
+                    LPC_SYNC();
+                } else {
                 T pv = gde * yref[(size_t)N * yrow + (xl ? r : 0)];   // p_N = g_N (x-lanes)
                 Bk bc;
                 bload(N - 1, bc);
@@ -576,9 +641,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 // forward rollout, one LDS exchange per stage (x_k, two alternating buffers):
                 // x_{k+1} = (A + B K_k) x_k + B kff_k + c, u_k = kff_k + K_k x_k; bound test, outputs
-                T xk = x0r, nbad = 0;
-                T wcv = 0, wcs = 0;   // the lane's most violated stage (state lanes: the set's first member)
-                int wck = -1;
+                T xk = x0r;
                 T fr[NX], frn[NX], dd = ldE(L::DZ, 0), ddn;
                 {
                     const T *t_ = frow(0, r);
@@ -605,44 +668,20 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     }
                     if (NX % 2) s0 = fma(fr[NX - 1], xb[NX - 1], s0);
                     const T z = xl ? xk : s0 + s1;   // u-lane: u_k = kff + K(u, :) x_k
-                    const Bd bk = k == 0 ? b0 : bm;
-                    // stricter than the finish's 1e-9: a bound violated inside that band goes through the
-                    // full solve, whose rounding decides it exactly as without the fast path
-                    const T tl = T(FAST_TOL) * (T(1) + fabs(bk.lb)), tu = T(FAST_TOL) * (T(1) + fabs(bk.ub));
-                    const bool lo_ = has_bound(bk.lb) && z < bk.lb - tl, hi_ = has_bound(bk.ub) && z > bk.ub + tu;
-                    nbad += (!isfinite(z) || lo_ || hi_) ? T(1) : T(0);
-                    stE(L::Z, k, z);   // z_0 of the active-set steps below
-                    if (try_fast && empty0) {
-                        fin_out(k, z, bk);
-                        // first set of the active-set steps: violated inputs, each state's most violated stage
-                        const T v_ = lo_ ? bk.lb - z : (hi_ ? z - bk.ub : T(0));
-                        if (ul) stE(L::DZA, k, lo_ ? T(-1) : (hi_ ? T(1) : T(0)));
-                        wck = v_ > wcv ? k : wck;
-                        wcs = v_ > wcv ? (lo_ ? T(-1) : T(1)) : wcs;
-                        wcv = fmax(wcv, v_);
-                    }
+                    fcheck(k, z, k == 0 ? b0 : bm);
                     xk = xl ? s0 + s1 + c_r : xk;   // x-lane: x_{k+1} = (A + B K) x_k + d_k + c
 #pragma unroll
                     for (int j = 0; j < NX; j++) fr[j] = frn[j];
                     dd = ddn;
                 }
-                if (xl) {
-                    const Bd bN = bnd(N);
-                    const T tl = T(FAST_TOL) * (T(1) + fabs(bN.lb)), tu = T(FAST_TOL) * (T(1) + fabs(bN.ub));
-                    const bool lo_ = has_bound(bN.lb) && xk < bN.lb - tl, hi_ = has_bound(bN.ub) && xk > bN.ub + tu;
-                    nbad += (!isfinite(xk) || lo_ || hi_) ? T(1) : T(0);
-                    stE(L::Z, N, xk);
-                    if (try_fast && empty0) {
-                        fin_out(N, xk, bN);
-                        const T v_ = lo_ ? bN.lb - xk : (hi_ ? xk - bN.ub : T(0));
-                        wck = v_ > wcv ? N : wck;
-                        wcs = v_ > wcv ? (lo_ ? T(-1) : T(1)) : wcs;
-                        wcv = fmax(wcv, v_);
-                    }
+                if (xl) fcheck(N, xk, bnd(N));
                 }
                 if (try_fast && empty0 && xl && wck >= 0) stE(L::DZA, wck, wcs);
                 nbad = gsum(nbad);
                 fast_ok = try_fast && empty0 && nbad == T(0);
+#ifdef NMPC_STEP_SPLIT
+                LPC_STICK(0);   // experiment builds: the unconstrained solve (slot 5: the active-set steps)
+#endif
                 // ---- active-set steps on the shared factorisation (p.lqrw): S = the flagged bounds
                 // (DZA: the warm-start set, or the first set from the unconstrained solution's
                 // violations), z = z_0 + W[:, S] nu with W_SS nu = b_S - z_0,S — the exact solution with S
@@ -781,6 +820,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 // a group that took active-set steps left its last set in DZA: the full solve's first
                 // finish step starts from it (never as an empty set)
                 if (fin_ws > 0) warm_act = T(1);
+#ifdef NMPC_STEP_SPLIT
+                LPC_STICK(5);
+#endif
                 if (fastpl) cly[r] = yref[xl || r < p.ny ? r : 0];   // yref row 0 (cost / AED reference)
             }
         }
