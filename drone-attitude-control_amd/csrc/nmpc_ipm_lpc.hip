@@ -386,6 +386,20 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // bounds, an infeasible QP) skips the finish in the next step — its active-set runs cannot be
     // accepted and would only lengthen its wavefront's step chain
     bool prev_failed = false;
+    // fused closed loop: the active flags of the last solution (the warm start) as a per-lane bit
+    // mask, 2 bits per stage (1 lower, 2 upper; N <= 31), kept in registers for the whole launch and
+    // in the scratch ACT words between launches — instead of one scratch word per stage and step
+    const bool amask = fused && N <= 31;
+    auto mflag = [](unsigned long long m, int k) {
+        const unsigned b = (unsigned)(m >> (2 * k)) & 3u;
+        return b == 1u ? T(-1) : (b == 2u ? T(1) : T(0));
+    };
+    auto mset = [](unsigned long long &m, int k, T f) {
+        m = (m & ~(3ull << (2 * k))) | (f < T(0) ? (1ull << (2 * k)) : (f > T(0) ? (2ull << (2 * k)) : 0ull));
+    };
+    unsigned long long actm = 0;
+    if (amask && p.cl.step > 0)
+        for (int k = 0; k <= N; k++) mset(actm, k, ldE(L::ACT, k));
     // fused closed loop with the controller-model plant (quad13), fp64, cost at x_0: the state stays in
     // the group's LDS for the whole launch (G_CL: state, this step's output z_0, yref row 0, sums),
     // the plant step is one LDS exchange and a row of the solver's own [A B] (the same data
@@ -445,8 +459,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 const bool onl = has_bound(b.lb) && z <= b.lb + T(1e-7) * (T(1) + fabs(b.lb));
                 const bool onu = has_bound(b.ub) && z >= b.ub - T(1e-7) * (T(1) + fabs(b.ub));
                 const T f = onl ? T(-1) : (onu ? T(1) : T(0));
-                stE(L::ACT, k, f);
-                if (ul && k == N - 1) stE(L::ACT, N, f);
+                if (amask) {
+                    mset(actm, k, f);
+                    if (ul && k == N - 1) mset(actm, N, f);
+                } else {
+                    stE(L::ACT, k, f);
+                    if (ul && k == N - 1) stE(L::ACT, N, f);
+                }
             }
         };
         // row r of [A B] as a compact list (structured kernels): certificate, initial point, plant step
@@ -461,7 +480,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // DZA words the first finish step reads its flags from (so ACT is free for this solve's outputs),
     // and counted (an empty set takes the fast finish / lqr_back)
     T warm_act = 0;
-    if (warm) {
+    unsigned long long wm = 0;   // mask mode: the fast finish's working set (DZA only for a full solve)
+    if (warm && amask) {
+        for (int k = 0; k <= N; k++) {
+            const bool valid = !(k == 0 && xl) && (k < N || xl);
+            if (valid) mset(wm, k, mflag(actm, (p.warm_shift && k < N) ? k + 1 : k));
+        }
+        warm_act = gsum(T(__popcll(wm)));
+    } else if (warm) {
         constexpr int AC = 4;
         for (int kc = 0; kc <= N; kc += AC) {
             T a_[AC];
@@ -548,7 +574,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if (try_fast && empty0) {
                         fin_out(k, z, bk);
                         const T v_ = lo_ ? bk.lb - z : (hi_ ? z - bk.ub : T(0));
-                        if (ul) stE(L::DZA, k, lo_ ? T(-1) : (hi_ ? T(1) : T(0)));
+                        if (ul) {
+                            if (amask) mset(wm, k, lo_ ? T(-1) : (hi_ ? T(1) : T(0)));
+                            else stE(L::DZA, k, lo_ ? T(-1) : (hi_ ? T(1) : T(0)));
+                        }
                         wck = v_ > wcv ? k : wck;
                         wcs = v_ > wcv ? (lo_ ? T(-1) : T(1)) : wcs;
                         wcv = fmax(wcv, v_);
@@ -676,7 +705,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 }
                 if (xl) fcheck(N, xk, bnd(N));
                 }
-                if (try_fast && empty0 && xl && wck >= 0) stE(L::DZA, wck, wcs);
+                if (try_fast && empty0 && xl && wck >= 0) {
+                    if (amask) mset(wm, wck, wcs);
+                    else stE(L::DZA, wck, wcs);
+                }
                 nbad = gsum(nbad);
                 fast_ok = try_fast && empty0 && nbad == T(0);
 #ifdef NMPC_STEP_SPLIT
@@ -698,7 +730,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     T *le = gb + Gm::G_MT;                       // [WSMAX] element index
                     T *ls = le + WSMAX, *lt = ls + WSMAX;        // [WSMAX] sign, [WSMAX] target step
                     int nmine = 0;
-                    for (int k = 0; k <= N; k++) nmine += (k < N || xl) && !(k == 0 && xl) && ldE(L::DZA, k) != T(0);
+                    if (amask) nmine = __popcll(wm);
+                    else
+                        for (int k = 0; k <= N; k++) nmine += (k < N || xl) && !(k == 0 && xl) && ldE(L::DZA, k) != T(0);
                     int pre = nmine;
 #pragma unroll
                     for (int sh = 1; sh < NZ; sh <<= 1) {
@@ -711,7 +745,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if (wrun && m <= WSMAX) {
                         int q_ = pre;
                         for (int k = 0; k <= N; k++) {
-                            const T f = ((k < N || xl) && !(k == 0 && xl)) ? ldE(L::DZA, k) : T(0);
+                            const T f = ((k < N || xl) && !(k == 0 && xl)) ? (amask ? mflag(wm, k) : ldE(L::DZA, k)) : T(0);
                             if (f != T(0)) {
                                 const Bd b_ = bnd(k);
                                 le[q_] = T(k * NZ + r);
@@ -783,7 +817,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         for (int i = 0; i < WSMAX; i++)
                             if (i < m) z = fma(p.lqrw[(size_t)ei[i] * ne + e], nu_[i], z);
                         const Bd b_ = bnd(k);
-                        const T f = ldE(L::DZA, k);
+                        const T f = amask ? mflag(wm, k) : ldE(L::DZA, k);
                         T nf = f;
                         if (f != T(0)) {
                             // held: z_0 + W[:, S] nu lands on the bound up to the solve's rounding (1e-9, the
@@ -805,11 +839,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             cv2 = fmax(cv2, v_);
                         }
                         if (wrun) {
-                            if (nf != f) stE(L::DZA, k, nf);
+                            if (nf != f) {
+                                if (amask) mset(wm, k, nf);
+                                else stE(L::DZA, k, nf);
+                            }
                             fin_out(k, z, b_);
                         }
                     }
-                    if (wrun && xl && addok && ck2 >= 0) stE(L::DZA, ck2, cs2);
+                    if (wrun && xl && addok && ck2 >= 0) {
+                        if (amask) mset(wm, ck2, cs2);
+                        else stE(L::DZA, ck2, cs2);
+                    }
                     wbad = gsum(wbad);
                     fin_ws += wrun ? 1 : 0;
                     const bool acc = wrun && wbad == T(0);
@@ -827,6 +867,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             }
         }
         const bool need_full = __any(inst_ok && !fast_ok);
+        if (amask && warm && need_full && inst_ok && !fast_ok)   // the full solve reads its warm set from DZA
+            for (int k = 0; k <= N; k++) stE(L::DZA, k, mflag(wm, k));
         LPC_STICK(0);
         // ------------------------------------------------------------------ infeasibility certificate
         // interval reachability (oracle/c/riccati_ipm.c infeasible_stage): x-lane r carries the
@@ -2120,8 +2162,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 for (int j = 0; j < OC; j++) {
                     const int k = kc + j;
                     if (k > N) break;
-                    if (k == N && ul) {
-                        if (fused) stE(L::ACT, N, fprev);   // u-lanes: stage N mirrors N - 1 for the shift
+                    if (k == N && ul) {   // u-lanes: stage N mirrors N - 1 for the shift
+                        if (amask) mset(actm, N, fprev);
+                        else if (fused) stE(L::ACT, N, fprev);
                         continue;
                     }
                     const Bd bk = bnd(k);
@@ -2134,7 +2177,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         const bool onl = has_bound(bk.lb) && z <= bk.lb + T(1e-7) * (T(1) + fabs(bk.lb));
                         const bool onu = has_bound(bk.ub) && z >= bk.ub - T(1e-7) * (T(1) + fabs(bk.ub));
                         fprev = onl ? T(-1) : (onu ? T(1) : T(0));
-                        stE(L::ACT, k, fprev);
+                        if (amask) mset(actm, k, fprev);
+                        else stE(L::ACT, k, fprev);
                     }
                 }
             }
@@ -2207,6 +2251,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         }
         LPC_STICK(7);
     }
+    if (amask)   // the warm start of the next launch
+        for (int k = 0; k <= N; k++) stE(L::ACT, k, mflag(actm, k));
     if (fastpl && inst_ok) {   // the launch's final state and its closed-loop sums
         if (xl) p.cl.state[(size_t)inst * NX + r] = clx[r];
         if (r < 4) p.cl.acc[(size_t)inst * 4 + r] += (double)cls[r];
