@@ -1287,7 +1287,7 @@ static const IpmEntry<T> *table(int *n)
 // small batches their per-instance latency floor is lower (tools/family_pairs.sh, fp64, lpc vs
 // wave: force N=20 B=1024 1.09 vs 0.98 ms, B=4096 1.19 vs 1.31, B=8192 1.29 vs 1.88; jerk N=40
 // B=2048 1.03 vs 0.91, B=4096 1.05 vs 1.16, B=8192 1.14 vs 1.79)
-static int kernel_kind(int nx, int nu, int batch)
+static int kernel_kind(int nx, int nu, int batch, bool f64)
 {
     const char *k = getenv("NMPC_KERNEL");
     if (k && (k[0] == 'w' || k[0] == 'W')) return 0;
@@ -1296,10 +1296,13 @@ static int kernel_kind(int nx, int nu, int batch)
     const int nz = nx + nu;
     if (nz > 64) return 0;
     const long waves = ((long)batch + 64 / nz - 1) / (64 / nz);
-    // round 2 (fast finish in the lane-per-component family): jerk (nz = 8) runs it faster from
-    // B = 1024 (6.8M vs 6.0M steps/s; B = 2048 12.8M vs 10.0M), force (nz = 6) still not at B = 1024
-    // (1.95M vs 3.5M: its input-saturation sets exceed the fast finish's 8 bounds)
-    return (nz >= 8 || waves >= 384) ? 1 : 0;
+    // round 2 (fast finish in the lane-per-component family, fp64 closed loops): jerk (nz = 8) runs it
+    // faster from B = 1024 (7.3M vs 6.1M steps/s; B = 2048 12.8M vs 10.0M); force (nz = 6) does not —
+    // its input-saturation sets exceed the fast finish's 8 bounds — so fp64 force stays on the
+    // wavefront family up to B = 8192 (B = 1024 3.5M vs 2.0M, 4096 8.2M vs 6.2M, 8192 10.1M either);
+    // fp32 (no finish) keeps the IPM-only crossover of 384 lane-per-component wavefronts
+    if (nz >= 8) return 1;
+    return waves >= (f64 ? 820 : 384) ? 1 : 0;
 }
 
 template <typename T>
@@ -1307,7 +1310,7 @@ int ipm_find(int nx, int nu, int ipw_req, int batch, int *ipw_out, int *lds_out,
 {
     int n;
     const IpmEntry<T> *t = table<T>(&n);
-    const int kind = kernel_kind(nx, nu, batch);
+    const int kind = kernel_kind(nx, nu, batch, sizeof(T) == 8);
     int best = -1;
     // NMPC_VARIANT=k picks the k-th compiled kernel of this (nx, nu) and family (tuning runs)
     const char *var = getenv("NMPC_VARIANT");
