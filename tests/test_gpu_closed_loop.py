@@ -207,12 +207,13 @@ def test_fused_closed_loop_matches_per_step(model, N, B, kernel):
 
 @pytest.mark.parametrize("model,N,B", [("quad13", 20, 3000), ("jerk", 40, 1001), ("force", 20, 2049)])
 def test_shared_factorisation_paths_match_full_factorisation(model, N, B):
-    """The exact finish's shortcuts for an empty active set — the fast finish (unconstrained LQ
-    solution from base 0 on the handle's shared Riccati factorisation, skipping certificate, initial
-    point and IPM) and lqr_back (the same factorisation inside the finish loop) — give the results
-    of factoring every finish step (NMPC_LQR=0, no shared factorisation): states and per-instance
-    cost / AED sums to rounding, failure counts exactly, over 40 steps of the lane-per-component
-    fused closed loop (two launches: 25 + 15)."""
+    """The exact finish's shortcuts on the handle's shared factorisation — the fast finish (the
+    unconstrained LQ solution, explicit from the closed loop's tables or by the recursion
+    (NMPC_EXPLICIT=0), then active-set steps on the projected inverse Hessian (off: NMPC_WSET=0),
+    skipping certificate, initial point and IPM) and lqr_back (inside the finish loop) — give the
+    results of factoring every finish step (NMPC_LQR=0): states and per-instance cost / AED sums to
+    rounding, failure counts exactly, over 40 steps of the lane-per-component fused closed loop
+    (two launches: 25 + 15)."""
     from drone_attitude_control_amd.batched import ClosedLoop
 
     def run(env):
@@ -227,7 +228,7 @@ def test_shared_factorisation_paths_match_full_factorisation(model, N, B):
                 os.environ.pop(k, None)
 
     x0, s0 = run({"NMPC_LQR": "0"})
-    for env in ({}, {"NMPC_FAST": "0"}, {"NMPC_FAST": "2"}):
+    for env in ({}, {"NMPC_FAST": "0"}, {"NMPC_FAST": "2"}, {"NMPC_EXPLICIT": "0"}, {"NMPC_WSET": "0"}):
         x1, s1 = run(env)
         assert np.array_equal(s0[:, 2:], s1[:, 2:]), env
         assert np.allclose(x1, x0, rtol=1e-9, atol=1e-9), (env, np.abs(x1 - x0).max())
