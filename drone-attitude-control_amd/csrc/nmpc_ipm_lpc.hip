@@ -597,7 +597,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     const int ne = (N + 1) * NZ;
                     const T *vt = p.cl_v + (size_t)t_ref * ne;
                     const Bd b0 = bnd(0), bm = bnd(1), bN = bnd(N);
-                    constexpr int EC = 4;
+#ifndef NMPC_FAST_EC
+#define NMPC_FAST_EC 2
+#endif
+                    constexpr int EC = NMPC_FAST_EC;   // stages whose table rows are in flight together (A/B on one box, quad13 B=8192: 1 0.110-0.112 ms, 2 0.106-0.107, 3 0.108, 4 0.121, 7 0.19)
                     for (int kc = 0; kc <= N; kc += EC) {
                         T zc[EC];
 #pragma unroll
