@@ -727,7 +727,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                 fin_ws = 0;
                 bool wrun = try_fast && !fast_ok && p.lqrw != nullptr;
                 for (int ws = 0; ws < p.polish_steps && __any(wrun); ws++) {
-                    constexpr int WSMAX = 8;
+#ifndef NMPC_WSMAX
+#define NMPC_WSMAX 8
+#endif
+                    constexpr int WSMAX = NMPC_WSMAX;   // largest active set of the fast finish's steps
                     const int ne = (N + 1) * NZ;
                     // the set: per-lane count, group prefix, entries in LDS (element, sign, b - z_0)
                     T *le = gb + Gm::G_MT;                       // [WSMAX] element index
