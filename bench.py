@@ -7,23 +7,26 @@ Workload (BASELINE.json metric "NMPC steps/sec (batched trajectories), N=20 nx=1
 the synthetic quad13 OCP (nx=13, nu=4, horizon N=20, no reference counterpart: SURVEY §0),
 B = 8192 independent closed-loop trajectories per GPU (weak scaling), fp64. One step = for
 every instance: build the yref window + pin x0 (set_up_ocp, ocp.py:117-122), solve the OCP
-(AcadosOcpSolver.solve, controller.py:32) to 1e-15 complementarity, advance the plant with
-Philox noise and accumulate cost/AED — all resident in HBM. value = instances x steps /
-wall time (max over ranks) for all ranks together. Ranks exchange nothing during the run;
-RCCL (torch.distributed "nccl") reduces the cost/AED/failure statistics once at the end.
+(AcadosOcpSolver.solve, controller.py:32) to its exact solution (the warm-started exact finish:
+explicit unconstrained solution, primal-dual active-set steps, full IPM + finish where those
+fail), advance the plant with Philox noise and accumulate cost/AED — all resident
+in HBM. value = instances x steps / wall time (max over ranks) for all ranks together. Ranks
+exchange nothing during the run; RCCL (torch.distributed "nccl") reduces the cost/AED/failure
+statistics once at the end.
 
 Also reported (one JSON line on rank 0):
-  roofline — the solve kernel (the dominant kernel): algorithmic flops per launch = SURVEY
-    §8d F_iter x n_ipm (mean IPM iterations of the CPU baseline on the same inputs) x B,
-    divided by the kernel's mean duration from HIP events around each launch;
-    bound "mfma" = the dense FP64 FMA roofline: peak = MI355X FP64 78.6 TFLOP/s, the rate of
-    both the FP64 matrix and the FP64 vector pipe (half the 157.3 TFLOP/s F32 rate of
-    MI355X_MICROARCH.md); the kernel issues its FP64 FMAs on the vector pipe (DESIGN.md §4
-    explains why 17-wide stage operands do not pay on MFMA). traffic = memory-side bytes per
-    launch (FETCH_SIZE + WRITE_SIZE) from the rocprofv3 PMC passes committed under profiles/
-    (profiles/pmc_traffic.json) when one matches this config, else null.
-  cpu_baseline — oracle/c/riccati_ipm.c (same algorithm, fp64, OpenMP over instances) on the
-    host cores, rank 0 at N=1 only, on a bounded sample of the same instances.
+  roofline — the solve kernel (the dominant kernel), bound "valu_fp64": achieved = the FP64 flops
+    per instance-step that the CPU baseline executes on the same closed loop (the same algorithm,
+    counted per path it takes: explicit solution 2 nx per element, active-set steps
+    m^3/3 + 2 m^2 + 2 ne m, full solves SURVEY §8d's F_iter per Newton system, plant 2 nx nz)
+    x B / the kernel's mean duration per step from HIP events around each launch; peak = MI355X
+    FP64 78.6 TFLOP/s (the FP64 vector and matrix peaks are equal). executed_frac = the FP64 flops
+    the kernel really issues (SQ_INSTS_VALU_FLOPS_FP64 of the committed rocprofv3 PMC pass, idle
+    lanes included) / kernel time / peak. traffic = memory-side bytes per step (FETCH_SIZE +
+    WRITE_SIZE) from the same PMC pass (profiles/pmc_traffic.json) when one matches, else null.
+  cpu_baseline — oracle/c/riccati_ipm.c's closed loop in mode 1 (the GPU's algorithm: warm-started
+    fast finish, fp64, OpenMP over instances) on the host cores, rank 0 at N=1 only, over the same
+    instances and steps as the timed GPU run.
 """
 import argparse
 import json
@@ -78,45 +81,48 @@ def ipm_tolerances(model, N, precision="fp64"):
     return tc, tr, pm, ps
 
 
-def cpu_baseline(model, N, table, offsets, x_init, seconds, precision):
-    """Time the C oracle (same Riccati IPM, fp64 arithmetic, the GPU run's tolerances) on a
-    bounded sample of the same instances."""
+def cpu_baseline(model, N, table, offsets, x_init, warmup, steps, seconds, precision, seed):
+    """Time the C oracle's closed loop in mode 1 — the GPU's algorithm (warm-started fast finish on
+    the shared factorisation, full IPM + finish where it fails; fp64 arithmetic, the handle's
+    options) — on the same instances and steps as the timed GPU run: `warmup` untimed steps, then
+    `steps` timed ones (all host threads; fewer instances if the whole batch would take longer than
+    ~`seconds`), then a single-thread figure on a slice. Also returns the FP64 flops per
+    instance-step it executed over the timed steps (the roofline credit)."""
     from oracle import cref, models
     spec = models.MODELS[model](N)
     tc, tr, pm, ps = ipm_tolerances(model, N, precision)
-    R = cref.RiccatiIpmRef(spec, tol_comp=tc, tol_res=tr, polish_mu=pm, polish_steps=ps)
-    ny, nye = spec.ny, spec.nx
-    nsamp = min(len(offsets), 4096)
-    Y = np.stack([np.concatenate([table[t:t + N, :ny].ravel(), table[t + N, :nye]]) for t in offsets[:nsamp]])
-    X0 = x_init[:nsamp]
-    threads = R.max_threads()
-    # n_ipm on exactly the first-step inputs of the GPU run
-    _, _, st, it = R.solve(X0, Y, nthreads=threads)
-    n_ipm = float(it[st == 0].mean()) if (st == 0).any() else float(it.mean())
-    # bounded timing loop (~`seconds` of CPU work)
-    solves, t0 = 0, time.perf_counter()
-    while True:
-        R.solve(X0, Y, nthreads=threads)
-        solves += nsamp
+
+    def loop(n, threads, nsteps):
+        cl = cref.ClosedLoopRef(spec, model, table, offsets[:n], x_init[:n], mode=1, seed=seed,
+                                tol_comp=tc, tol_res=tr, polish_mu=pm, polish_steps=ps)
+        cl.run(warmup, nthreads=threads)
+        c0 = cl.stats()
+        t0 = time.perf_counter()
+        cl.run(nsteps, nthreads=threads)
         el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    # single-core figure (SURVEY §8d), on a smaller slice of the same inputs (~1/5 of the time)
-    n1 = max(1, min(nsamp, 256))
-    s1, t1 = 0, time.perf_counter()
-    while True:
-        R.solve(X0[:n1], Y[:n1], nthreads=1)
-        s1 += n1
-        e1 = time.perf_counter() - t1
-        if e1 >= seconds / 5:
-            break
-    return {"value": solves / el, "unit": "NMPC steps/s", "cores": threads, "kind": "port",
-            "sample": f"{solves} solves of the first closed-loop step of {nsamp} bench instances "
-                      f"({model}, N={N}, fp64 arithmetic, tol_comp {tc:g} / tol_res {tr:g}, exact finish from "
-                      f"mu <= {pm:g} with <= {ps} active-set steps) in {el:.1f} s, "
-                      f"OpenMP over instances; oracle/c/riccati_ipm.c -O3 -march=x86-64-v3",
-            "single_core": {"value": s1 / e1, "cores": 1,
-                            "sample": f"{s1} solves of {n1} of those instances in {e1:.1f} s"}}, n_ipm
+        c1 = cl.stats()
+        return el, {k: c1[k] - c0[k] for k in c1}
+
+    threads = cref.RiccatiIpmRef(spec).max_threads()
+    B = len(offsets)
+    # probe the rate on a slice, then size the sample to ~`seconds`
+    n0, s0 = min(B, 256), max(1, min(steps, 20))
+    el, _ = loop(n0, threads, s0)
+    n = int(min(B, max(n0, n0 * s0 / max(el, 1e-6) * seconds / max(1, steps))))
+    el, st = loop(n, threads, steps)
+    n1 = min(n, 128)
+    e1, _ = loop(n1, 1, steps)
+    solves = max(1.0, st["solves"])
+    paths = {k: st[k] / solves for k in ("fast_unconstrained", "fast_set", "full", "failed")}
+    return {"value": n * steps / el, "unit": "NMPC steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} of the {B} bench instances, closed-loop steps {warmup}..{warmup + steps - 1} ({model}, "
+                      f"N={N}, fp64 arithmetic) in {el:.2f} s after {warmup} untimed steps: oracle/c/riccati_ipm.c "
+                      f"riccati_ipm_closed_loop mode 1 (the GPU's algorithm: warm-started fast finish, explicit "
+                      f"unconstrained solution, active-set steps on the shared factorisation, full IPM + exact finish "
+                      f"where they fail; tol_comp {tc:g} / tol_res {tr:g}), OpenMP over instances, -O3 -march=x86-64-v3",
+            "paths_per_step": paths, "flops_per_instance_step": st["flops"] / solves,
+            "single_core": {"value": n1 * steps / e1, "cores": 1,
+                            "sample": f"{n1} of those instances, the same steps, in {e1:.2f} s"}}, st["flops"] / solves
 
 
 def load_pmc(model, N, batch, precision, kernel):
@@ -182,9 +188,10 @@ def main():
     nx, nu = cl.solver.nx, cl.solver.nu
 
     # CPU baseline and the B=1 Python drop-in loop first (rank 0, single-GPU runs only)
-    cpu, n_ipm_cpu, pyloop = None, None, None
+    cpu, flops_cpu, pyloop = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, n_ipm_cpu = cpu_baseline(model, N, table, offsets_r, x_r, args.cpu_seconds, args.precision)
+        cpu, flops_cpu = cpu_baseline(model, N, table, offsets_r, x_r, args.warmup, args.repeats * args.steps,
+                                      args.cpu_seconds, args.precision, args.seed)
         if args.python_loop_steps > 0:
             pyloop = python_loop_rate(20, args.python_loop_steps)
             cpu["python_loop"] = pyloop
@@ -220,10 +227,12 @@ def main():
     if rank == 0:
         tols = ipm_tolerances(model, N, args.precision)
         value = world * B * args.steps / elapsed
-        # credited IPM iterations: the CPU baseline's on the same inputs at the same tolerances,
-        # never more than the GPU's own mean (extra iterations on either side earn nothing)
-        n_ipm = st["mean_qp_iter"] if n_ipm_cpu is None else min(n_ipm_cpu, st["mean_qp_iter"])
-        fl_launch = flops_per_iter(nx, nu, N) * n_ipm * B
+        # credit: the FP64 flops per instance-step the CPU baseline executes on the same closed loop
+        # (same algorithm, same steps); without it (multi-rank runs) the engine's own path mix is
+        # unknown here and the credit falls back to one explicit unconstrained solution per step
+        nz_, ne_ = nx + nu, (N + 1) * (nx + nu)
+        fl_step = flops_cpu if flops_cpu is not None else 2.0 * nx * (ne_ - nx - nu) + 2.0 * nx * nz_
+        fl_launch = fl_step * B
         achieved = fl_launch / (kernel_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.precision]
         info = cl.solver.launch_info()
@@ -252,29 +261,37 @@ def main():
                        "instances_per_wave": info["instances_per_wave"]},
             "timing": {"regions": len(regions), "steps_per_region": args.steps, "value_from": "median region",
                        "region_ms": [round(float(r) * 1e3, 4) for r in regions],
-                       "spread": float((regions.max() - regions.min()) / elapsed)},
+                       "spread": float((regions.max() - regions.min()) / elapsed),
+                       "iqr_rel": float((np.percentile(regions, 75) - np.percentile(regions, 25)) / elapsed),
+                       "note": "each region is one fused launch whose time is set by its slowest wavefront; "
+                               "region-to-region differences below the IQR are not resolved"},
             "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32",
                          "pipe": ("FP64 FMA on the VALU" if args.precision == "fp64" else "FP32 FMA on the VALU")
                          + " (MI355X: FP64 matrix peak = FP64 vector peak; FP32 matrix peak = FP32 vector peak)",
                          "kernel": info["kernel"], "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak,
+                         "credit": "FP64 flops per instance-step of the CPU baseline's run of the same algorithm on "
+                                   "the same steps (oracle closed loop mode 1, counted per path: explicit solution "
+                                   "2 nx per element, active-set steps m^3/3 + 2 m^2 + 2 ne m, full solves F_iter "
+                                   "(SURVEY 8d) per Newton system, plant 2 nx nz) x B / kernel time per step",
+                         "flops_per_instance_step": fl_step, "flops_per_launch": fl_launch, "kernel_ms": kernel_ms,
+                         "executed_fp64_flops_per_step": pmc.get("fp64_flops_per_step"),
+                         "executed_frac": (pmc["fp64_flops_per_step"] / (kernel_ms * 1e-3) / 1e12 / peak
+                                           if pmc.get("fp64_flops_per_step") else None),
+                         "executed_note": "FP64 flops the kernel issues (64 x SQ_INSTS_VALU_FLOPS_FP64 per step, idle "
+                                          f"lanes included; {pmc.get('source', 'no PMC pass for this config')}) / this "
+                                          "run's kernel time / peak",
+                         "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
                          "traffic": pmc.get("hbm_bytes_per_step", pmc.get("hbm_bytes_per_launch")),
                          "traffic_note": "FETCH_SIZE + WRITE_SIZE per closed-loop step (per launch / fused steps per "
                                          "launch) from the committed rocprofv3 PMC pass "
                                          f"({pmc.get('source', 'none for this config')}); no x2 FETCH_SIZE "
                                          "correction: the kernel's loads are 4/8-B per lane, the guide's x2 is "
                                          "calibrated for 16-B streams; includes Infinity-Cache hits",
-                         "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
-                         "executed_fp64_flops_per_step": pmc.get("fp64_flops_per_step"),
-                         "flops_note": "achieved credits SURVEY 8d's F_iter (one Riccati factorisation) per Newton "
-                                       "system (n_ipm: the CPU baseline's count on the same first-step QPs); the "
-                                       "GPU's empty-active-set finish steps (fast finish, lqr_back) run a vector "
-                                       "recursion on the handle's shared factorisation instead, so the FP64 work "
-                                       "the kernel executes (executed_fp64_flops_per_step, SQ_INSTS_VALU_FLOPS_FP64 "
-                                       "from the committed PMC pass) is below the credit; the path is bound by "
-                                       "LDS-exchange and dependency latency, not by the FP64 pipe or HBM",
-                         "flops_per_launch": fl_launch, "kernel_ms": kernel_ms,
-                         "n_ipm": n_ipm, "n_ipm_cpu": n_ipm_cpu, "gpu_mean_qp_iter": st["mean_qp_iter"]},
+                         "riccati_credit_frac": flops_per_iter(nx, nu, N) * B / (kernel_ms * 1e-3) / 1e12 / peak,
+                         "riccati_credit_note": "rounds 1-2's credit (one full Riccati factorisation, SURVEY 8d F_iter, "
+                                                "per step) for comparison only: the fast finish does not factor",
+                         "gpu_mean_qp_iter": st["mean_qp_iter"]},
             "solve_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "QP solves/s",
                            "note": "solve kernel alone (median of the regions' mean launch durations, HIP events), "
                                    "all ranks"},

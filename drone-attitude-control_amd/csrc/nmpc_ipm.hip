@@ -384,10 +384,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // one solve per closed-loop step; plain solves run one step (p.cl_steps = 0)
     const bool fused = p.cl_steps > 0;
     const int nsteps = fused ? p.cl_steps : 1;
-    // fused closed loop: an instance whose last solve failed (typically a state pushed past its
-    // bounds, an infeasible QP) skips the finish in the next step — its active-set runs cannot be
-    // accepted and would only lengthen its wavefront's step chain
-    bool prev_failed = false;
     for (int cstep = 0; cstep < nsteps; cstep++) {
         // fused closed loop: the yref window straight from the reference table rows (offset + step) %
         // period (cl_prepare_kernel's gather), x0 from the closed-loop state
@@ -882,7 +878,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // active-set run of penalised factorisations + forward sweeps (<= polish_steps set steps,
             // then the refinement); accepted groups write their outputs and are done, the others go on
             // with this iteration from their untouched IPM iterate
-            pol = active && p.polish_mu > T(0) && mu <= polish_at && !prev_failed;
+            pol = active && p.polish_mu > T(0) && mu <= polish_at;
             if (__any(pol)) {
                 polish_at = pol ? fmin(polish_at, mu) * p.polish_drop : polish_at;
                 const int plim = fin_runs == 0 ? p.polish_first : p.polish_steps;   // set steps of this run
@@ -1166,7 +1162,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #endif
             }
         }
-        prev_failed = status > 0;
         if (fused) {
             // closed-loop advance of this step by the instance's lanes (nmpc_cl_device.h), after the
             // outputs written above by this wavefront; the next step reads the new state

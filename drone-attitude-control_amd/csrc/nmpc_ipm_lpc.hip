@@ -382,10 +382,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // one solve per closed-loop step; plain solves run one step (p.cl_steps = 0)
     const bool fused = p.cl_steps > 0;
     const int nsteps = fused ? p.cl_steps : 1;
-    // fused closed loop: an instance whose last solve failed (typically a state pushed past its
-    // bounds, an infeasible QP) skips the finish in the next step — its active-set runs cannot be
-    // accepted and would only lengthen its wavefront's step chain
-    bool prev_failed = false;
     // fused closed loop: the active flags of the last solution (the warm start) as a per-lane bit
     // mask, 2 bits per stage (1 lower, 2 upper; N <= 31), kept in registers for the whole launch and
     // in the scratch ACT words between launches — instead of one scratch word per stage and step
@@ -529,7 +525,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             constexpr int WF = 1 + 2 * NU + NX, OM = 1, OW = 1 + NU, OR = 1 + 2 * NU;
             constexpr double FAST_TOL = 1e-13;
             const bool try_fast = SP::hdiag && p.lqrf != nullptr && p.g_diag && p.polish_mu > T(0) && warm && inst_ok &&
-                                  !prev_failed && p.fast_mode != 0 && (p.fast_mode == 1 || cstep > 0) &&
+                                  p.fast_mode != 0 && (p.fast_mode == 1 || cstep > 0) &&
                                   (warm_act == T(0) || p.lqrw != nullptr);
             const bool empty0 = warm_act == T(0);   // the unconstrained solution is the first set step
             if (__any(try_fast)) {
@@ -764,7 +760,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     LPC_SYNC();
                     wrun = wrun && m >= 1 && m <= WSMAX;
                     // nu = W_SS^{-1} (b - z_0)_S by Cholesky, every lane (m <= WSMAX)
-                    T L_[WSMAX][WSMAX], nu_[WSMAX];
+                    T L_[WSMAX][WSMAX], nu_[WSMAX], wd_[WSMAX];
                     int ei[WSMAX];
 #pragma unroll
                     for (int i = 0; i < WSMAX; i++) {
@@ -777,6 +773,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #pragma unroll
                         for (int j = 0; j <= i; j++) {
                             T s_ = (i < m && j < m) ? p.lqrw[(size_t)ei[j] * ne + ei[i]] : (i == j ? T(1) : T(0));
+                            if (i == j) wd_[i] = s_;
 #pragma unroll
                             for (int l = 0; l < j; l++) s_ = fma(-L_[i][l], L_[j][l], s_);
                             if (i == j) {
@@ -801,14 +798,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         nu_[i] = s_ / L_[i][i];
                     }
                     wrun = wrun && pdf;
-                    // multiplier signs (lower: nu >= 0, upper: nu <= 0, to the finish's few-ulp tolerance)
+                    // multiplier signs (lower: nu >= 0, upper: nu <= 0), measured as the displacement
+                    // nu_i W_ii the multiplier causes at its own element: a wrong-sign multiplier of
+                    // displacement d moves the solution by about d, so the tolerance is a z-scale one,
+                    // 1e-10 (1 + |b - z_0|), above the rounding of the W_SS solve (oracle/c/riccati_ipm.c
+                    // fast_finish; a gradient-scale tolerance let quad13's low-curvature angular
+                    // accelerations and the force inputs keep wrong-sign bounds worth 1e-6..1e-5)
                     int nrem = 0;
                     bool remk[WSMAX];
 #pragma unroll
                     for (int i = 0; i < WSMAX; i++) {
                         const T f = (i < m) ? ls[i] : T(0);
-                        const T tol_ = p.polish_rho * T(1e-15) * (T(1) + fabs(lt[i]));
-                        remk[i] = i < m && ((f < T(0) && nu_[i] < -tol_) || (f > T(0) && nu_[i] > tol_) || !isfinite(nu_[i]));
+                        const T tol_ = T(1e-10) * (T(1) + fabs(lt[i])), dsp = nu_[i] * wd_[i];
+                        remk[i] = i < m && ((f < T(0) && dsp < -tol_) || (f > T(0) && dsp > tol_) || !isfinite(nu_[i]));
                         nrem += remk[i] ? 1 : 0;
                     }
                     // z = z_0 + W[:, S] nu at the lane's elements: bounds, the next set, tentative outputs
@@ -1965,7 +1967,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
             // active-set run of penalised factorisations + forward sweeps (<= polish_steps set steps,
             // then the refinement) for the polishing groups; accepted groups are done, the others go
             // on with this iteration from their untouched IPM iterate
-            pol = active && p.polish_mu > T(0) && mu <= polish_at && !prev_failed;
+            pol = active && p.polish_mu > T(0) && mu <= polish_at;
             if (__any(pol)) {
                 polish_at = pol ? fmin(polish_at, mu) * p.polish_drop : polish_at;
                 const int plim = fin_runs == 0 ? p.polish_first : p.polish_steps;   // set steps of this run
@@ -2204,7 +2206,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #endif
             }
         }
-        prev_failed = status > 0;
         LPC_STICK(6);
         if (fused) {
             // closed-loop advance of this step by the instance's lanes (its outputs were written by

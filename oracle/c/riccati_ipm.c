@@ -279,7 +279,7 @@ static int pdas_update(const ocp_ref_desc *d, ws_t *w, int first)
 }
 
 static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref,
-                     double *xo, double *uo, int *iters_out, ws_t *w)
+                     double *xo, double *uo, int *iters_out, ws_t *w, const signed char *warm, int no_finish)
 {
     const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ny = d->ny;
     const double *A = d->A, *B = d->B, *c = d->c;
@@ -354,7 +354,8 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
         }
     double theta = 1.0;
     if (m == 0) m = 1;
-    double polish_at = d->polish_mu > 0.0 ? d->polish_mu : -1.0, rho = 1.0;
+    /* no_finish: the fused closed loop runs no finish after a failed step (IPM only) */
+    double polish_at = d->polish_mu > 0.0 && !no_finish ? d->polish_mu : -1.0, rho = 1.0;
     int fin_steps = 0;
     for (i = 0; i < nz * nz; i += nz + 1) rho = fmax(rho, fabs(d->H[i]));
     for (i = 0; i < nx * nx; i += nx + 1) rho = fmax(rho, fabs(d->He[i]));
@@ -420,7 +421,10 @@ static int solve_one(const ocp_ref_desc *d, const double *x0, const double *yref
              * drop 100-fold. */
             polish_at = (mu < polish_at ? mu : polish_at) * 1e-2;
             memset(w->act, 0, (size_t)(N + 1) * nz);
-            for (k = 0; k <= N; k++) {
+            /* warm start (closed loop): the first run of a solve starts from the given set instead
+             * of the multiplier rule */
+            if (warm && it == 0) memcpy(w->act, warm, (size_t)(N + 1) * nz);
+            else for (k = 0; k <= N; k++) {
                 int n = k < N ? nz : nx;
                 for (i = 0; i < n; i++) {
                     signed char a = 0;
@@ -718,7 +722,7 @@ int riccati_ipm_solve_batch(const ocp_ref_desc *d, int batch, const double *x0, 
         for (int b = 0; b < batch; b++) {
             int st = solve_one(d, x0 + (size_t)b * nx, yref + (size_t)b * ystride,
                                xout + (size_t)b * (N + 1) * nx, uout + (size_t)b * N * nu,
-                               &iters[b], &w);
+                               &iters[b], &w, NULL, 0);
             status[b] = st;
             if (st != 0) nfail++;
         }
@@ -734,4 +738,718 @@ int riccati_ipm_max_threads(void)
 #else
     return 1;
 #endif
+}
+
+/* ======================================================================================
+ * Closed loops (TEST INFRASTRUCTURE / CPU BASELINE). Restates the batched Monte-Carlo
+ * closed loop the engine runs on the device (nmpc_closed_loop_run): per instance and step
+ *   yref window from the shared reference table at row (offset + step) % period
+ *   (set_up_ocp, src/force_model/ocp.py:117-122; table = src/generate_trajectory.py:7-28),
+ *   x0 pinned to the state (src/force_model/controller.py:29-31, jerk :30-32), solve
+ *   (controller.py:32 / :33), closed-loop cost (controller.py:40-41) and AED numerator
+ *   (src/store_results.py:233-236), then the plant: the controller's own discrete model for the
+ *   synthetic quad13 instances, or converter + Crazyflie plant (force_model/dynamics.py:54-79 +
+ *   force_model/ocp.py:106-115: atan2/|F|, RK4 over dt; jerk_model/dynamics.py:59-83 +
+ *   jerk_model/ocp.py:106-116: 10 Euler sub-steps over dt_conv), plus one scalar noise draw per
+ *   (instance, step) on the first noise_dims states (ocp.py:114).
+ * Two solve modes:
+ *   mode 0 (the oracle): every QP solved cold by solve_one (IPM + exact finish, KKT-accepted),
+ *     i.e. each step takes the exact QP solution;
+ *   mode 1 (the GPU's algorithm, the CPU baseline): the fused closed loop's warm-started fast
+ *     finish — the previous solution's active set shifted by one stage; an empty set takes the
+ *     explicit unconstrained solution z_0 = T_x x_0 + v_t (tables per reference row) and is done if
+ *     every bound holds (1e-13); otherwise primal-dual active-set steps on the projected inverse
+ *     Hessian W of the unconstrained problem (z = z_0 + W[:, S] nu, W_SS nu = b_S - z_0,S; sets of
+ *     at most WSMAX bounds); a step still unaccepted runs solve_one warm-started from the set it
+ *     reached.
+ * Both modes give the same closed loop up to the solve tolerances (a strictly convex QP has one
+ * KKT point); mode 1 counts the FP64 work of the path it takes (the roofline credit).
+ * ====================================================================================== */
+
+typedef struct {
+    int plant;              /* 0 controller model (d->A, d->B, d->c), 1 Crazyflie + force converter, 2 + jerk converter */
+    const double *table;    /* [rows][cols] */
+    int rows, cols, period;
+    int cost_stage, ncl, aed_dims, noise_dims, substeps;
+    const double *wcl;      /* [ncl] */
+    double mass, g, dt, dt_conv;
+    const double *noise;    /* optional [batch][noise_len] injected draws (else Philox, else none) */
+    int noise_len;
+    double noise_std;
+    unsigned long long seed;
+    long long inst_base;
+    const long long *inst_ids;   /* optional [batch] global instance ids of the Philox stream (else inst_base + b) */
+} cl_ref_desc;
+
+#ifndef WSMAX
+#define WSMAX 8
+#endif
+
+/* Philox4x32-10 + Box-Muller: the device's noise stream (nmpc_cl_device.h philox_normal_dev) */
+static double philox_normal(unsigned long long seed, unsigned long long inst, unsigned long long step)
+{
+    unsigned c0 = (unsigned)step, c1 = (unsigned)(step >> 32), c2 = (unsigned)inst, c3 = (unsigned)(inst >> 32);
+    unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+    for (int r = 0; r < 10; r++) {
+        const unsigned long long p0 = 0xD2511F53ull * c0, p1 = 0xCD9E8D57ull * c2;
+        const unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0, h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
+        const unsigned n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+        c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    const double u1 = ((double)c0 + 1.0) * (1.0 / 4294967296.0), u2 = (double)c1 * (1.0 / 4294967296.0);
+    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+/* SURVEY 8d F_iter: FP64 flops of one Riccati-IPM Newton system */
+static double f_iter(int nx, int nu, int N)
+{
+    const double z = nx + nu;
+    return N * (2.0 * nx * nx * z + 2.0 * nx * z * z + nu * nu * nu / 3.0 + 2.0 * nu * nu * nx + 2.0 * nu * nx * nx +
+                2.0 * (2.0 * nx * z + 2.0 * nu * nx + 2.0 * nx * nx) + 40.0 * z);
+}
+
+/* The unconstrained LQ problem's Riccati factorisation (shared by every instance and step):
+ * per stage k < N the gain K_k (nu x nx), F_uu^{-1} (nu x nu) and P_{k+1} (nx x nx). */
+typedef struct {
+    int ne;
+    double *K, *Fi, *P;      /* [N][nu*nx], [N][nu*nu], [N][nx*nx] (P_{k+1}) */
+    double *tx, *v, *W;      /* explicit form: T_x [ne][nx], v_t [period][ne]; W [ne][ne] column-major */
+} fast_tables;
+
+static void lqr_factor(const ocp_ref_desc *d, fast_tables *f)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu;
+    double P[NZMAX * NZMAX], M[NZMAX * NZMAX], F[NZMAX * NZMAX], L[NZMAX * NZMAX];
+    for (int i = 0; i < nx * nx; i++) P[i] = d->He[i];
+    for (int k = N - 1; k >= 0; k--) {
+        double *K = f->K + (size_t)k * nu * nx, *Fi = f->Fi + (size_t)k * nu * nu;
+        memcpy(f->P + (size_t)k * nx * nx, P, sizeof(double) * nx * nx);
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < nz; j++) {
+                double s = 0.0;
+                for (int l = 0; l < nx; l++) s += P[i * nx + l] * (j < nx ? d->A[l * nx + j] : d->B[l * nu + j - nx]);
+                M[i * nz + j] = s;
+            }
+        for (int i = 0; i < nz; i++)
+            for (int j = 0; j < nz; j++) {
+                double s = d->H[i * nz + j];
+                for (int l = 0; l < nx; l++) s += (i < nx ? d->A[l * nx + i] : d->B[l * nu + i - nx]) * M[l * nz + j];
+                F[i * nz + j] = s;
+            }
+        for (int i = 0; i < nu; i++)
+            for (int j = 0; j <= i; j++) {
+                double s = F[(nx + i) * nz + nx + j];
+                for (int l = 0; l < j; l++) s -= L[i * nu + l] * L[j * nu + l];
+                L[i * nu + j] = i == j ? sqrt(s > 1e-300 ? s : 1e-300) : s / L[j * nu + j];
+            }
+        for (int c = 0; c < nu; c++) {
+            double y[NZMAX];
+            for (int i = 0; i < nu; i++) {
+                double s = i == c ? 1.0 : 0.0;
+                for (int l = 0; l < i; l++) s -= L[i * nu + l] * y[l];
+                y[i] = s / L[i * nu + i];
+            }
+            for (int i = nu - 1; i >= 0; i--) {
+                double s = y[i];
+                for (int l = i + 1; l < nu; l++) s -= L[l * nu + i] * y[l];
+                y[i] = s / L[i * nu + i];
+            }
+            for (int i = 0; i < nu; i++) Fi[i * nu + c] = y[i];
+        }
+        for (int i = 0; i < nu; i++)
+            for (int j = 0; j < nx; j++) {
+                double s = 0.0;
+                for (int l = 0; l < nu; l++) s -= Fi[i * nu + l] * F[(nx + l) * nz + j];
+                K[i * nx + j] = s;
+            }
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < nx; j++) {
+                double s = F[i * nz + j];
+                for (int l = 0; l < nu; l++) s += F[i * nz + nx + l] * K[l * nx + j];
+                P[i * nx + j] = s;
+            }
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < i; j++) P[i * nx + j] = P[j * nx + i] = 0.5 * (P[i * nx + j] + P[j * nx + i]);
+    }
+}
+
+/* unconstrained solution for gradient g (stage-stacked nz, stage N nx), initial state x0, affine
+ * term c on / off: backward p_N = g_N, v = p_{k+1} + P_{k+1} c, h = g_k + [A B]' v,
+ * kff = -F_uu^{-1} h_u, p_k = h_x + K_k' h_u; forward u_k = kff_k + K_k x_k, x_{k+1} = A x_k + B u_k + c */
+static void lqr_solve_ref(const ocp_ref_desc *d, const fast_tables *f, const double *g, const double *x0, int use_c,
+                          double *z)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu;
+    double p[NZMAX], v[NZMAX], h[NZMAX], x[NZMAX], xn[NZMAX];
+    double *kff = (double *)malloc(sizeof(double) * N * nu);
+    for (int i = 0; i < nx; i++) p[i] = g[N * nz + i];
+    for (int k = N - 1; k >= 0; k--) {
+        const double *K = f->K + (size_t)k * nu * nx, *Fi = f->Fi + (size_t)k * nu * nu, *P = f->P + (size_t)k * nx * nx;
+        for (int r = 0; r < nx; r++) {
+            double s = p[r];
+            if (use_c)
+                for (int j = 0; j < nx; j++) s += P[r * nx + j] * d->c[j];
+            v[r] = s;
+        }
+        for (int i = 0; i < nz; i++) {
+            double s = g[k * nz + i];
+            for (int l = 0; l < nx; l++) s += (i < nx ? d->A[l * nx + i] : d->B[l * nu + i - nx]) * v[l];
+            h[i] = s;
+        }
+        for (int u = 0; u < nu; u++) {
+            double s = 0.0;
+            for (int i = 0; i < nu; i++) s -= Fi[u * nu + i] * h[nx + i];
+            kff[k * nu + u] = s;
+        }
+        for (int j = 0; j < nx; j++) {
+            double s = h[j];
+            for (int i = 0; i < nu; i++) s += K[i * nx + j] * h[nx + i];
+            p[j] = s;
+        }
+    }
+    for (int i = 0; i < nx; i++) x[i] = x0[i];
+    for (int k = 0; k < N; k++) {
+        const double *K = f->K + (size_t)k * nu * nx;
+        for (int i = 0; i < nx; i++) z[k * nz + i] = x[i];
+        for (int u = 0; u < nu; u++) {
+            double s = kff[k * nu + u];
+            for (int j = 0; j < nx; j++) s += K[u * nx + j] * x[j];
+            z[k * nz + nx + u] = s;
+        }
+        for (int i = 0; i < nx; i++) {
+            double s = use_c ? d->c[i] : 0.0;
+            for (int j = 0; j < nx; j++) s += d->A[i * nx + j] * x[j];
+            for (int u = 0; u < nu; u++) s += d->B[i * nu + u] * z[k * nz + nx + u];
+            xn[i] = s;
+        }
+        for (int i = 0; i < nx; i++) x[i] = xn[i];
+    }
+    for (int i = 0; i < nx; i++) z[N * nz + i] = x[i];
+    for (int u = 0; u < nu; u++) z[N * nz + nx + u] = 0.0;
+    free(kff);
+}
+
+/* Tables of the fast finish: T_x (response to x0 = e_j), v_t (response to the reference window at
+ * table row t and to c) and W (column e' = minus the homogeneous response to a unit gradient at e';
+ * x_0 rows / columns and stage N's input slots are zero). */
+static fast_tables *fast_init(const ocp_ref_desc *d, const cl_ref_desc *c)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = (N + 1) * nz, ny = d->ny, nye = d->ny_e;
+    fast_tables *f = (fast_tables *)calloc(1, sizeof(fast_tables));
+    f->ne = ne;
+    f->K = (double *)malloc(sizeof(double) * N * nu * nx);
+    f->Fi = (double *)malloc(sizeof(double) * N * nu * nu);
+    f->P = (double *)malloc(sizeof(double) * N * nx * nx);
+    f->tx = (double *)malloc(sizeof(double) * ne * nx);
+    f->v = (double *)malloc(sizeof(double) * (size_t)c->period * ne);
+    f->W = (double *)calloc((size_t)ne * ne, sizeof(double));
+    lqr_factor(d, f);
+    double *g = (double *)calloc(ne, sizeof(double)), *z = (double *)malloc(sizeof(double) * ne), e0[NZMAX];
+    for (int j = 0; j < nx; j++) {
+        for (int i = 0; i < nx; i++) e0[i] = i == j;
+        lqr_solve_ref(d, f, g, e0, 0, z);
+        for (int e = 0; e < ne; e++) f->tx[(size_t)e * nx + j] = z[e];
+    }
+    for (int i = 0; i < nx; i++) e0[i] = 0.0;
+    for (int t = 0; t < c->period; t++) {
+        for (int k = 0; k <= N; k++) {
+            const double *y = c->table + (size_t)(t + k) * c->cols;
+            const int n = k < N ? nz : nx, m = k < N ? ny : nye;
+            const double *Gm = k < N ? d->G : d->Ge;
+            for (int i = 0; i < nz; i++) g[k * nz + i] = 0.0;
+            for (int i = 0; i < n; i++) {
+                double s = 0.0;
+                for (int q = 0; q < m; q++) s += Gm[i * m + q] * y[q];
+                g[k * nz + i] = s;
+            }
+        }
+        lqr_solve_ref(d, f, g, e0, 1, z);
+        memcpy(f->v + (size_t)t * ne, z, sizeof(double) * ne);
+    }
+    for (int e1 = 0; e1 < ne; e1++) {
+        const int k1 = e1 / nz, r1 = e1 % nz;
+        if ((k1 == 0 && r1 < nx) || (k1 == N && r1 >= nx)) continue;
+        for (int e = 0; e < ne; e++) g[e] = e == e1;
+        lqr_solve_ref(d, f, g, e0, 0, z);
+        for (int e = 0; e < ne; e++) f->W[(size_t)e1 * ne + e] = (e < nx || (e / nz == N && e % nz >= nx)) ? 0.0 : -z[e];
+    }
+    free(g);
+    free(z);
+    return f;
+}
+
+static void fast_free(fast_tables *f)
+{
+    if (!f) return;
+    free(f->K); free(f->Fi); free(f->P); free(f->tx); free(f->v); free(f->W);
+    free(f);
+}
+
+/* element (k, i) is a decision variable of the QP (x_0 pinned; stage N has no inputs) */
+static int valid_el(int nx, int N, int k, int i) { return !(k == 0 && i < nx) && (k < N || i < nx); }
+
+/* The fast finish of one step (mode 1). wf: the warm set (shifted flags, in), the set reached
+ * (out). Returns 1 and the solution in z (clamped onto the bounds) when accepted; counts the
+ * active-set steps and the FP64 work. */
+static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double *x0, int t, signed char *wf,
+                       double *z0, double *z, int *wsteps, double *flops)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
+    const double *vt = f->v + (size_t)t * ne;
+    int nwarm = 0, nbad = 0;
+    for (int e = 0; e < ne; e++) nwarm += wf[e] != 0;
+    *wsteps = 0;
+    for (int k = 0; k <= N; k++)
+        for (int i = 0; i < nz; i++) {
+            const int e = k * nz + i;
+            if (k == 0 && i < nx) { z0[e] = x0[i]; continue; }
+            if (k == N && i >= nx) { z0[e] = 0.0; continue; }
+            double s = vt[e];
+            for (int j = 0; j < nx; j++) s += f->tx[(size_t)e * nx + j] * x0[j];
+            z0[e] = s;
+            *flops += 2.0 * nx;
+        }
+    if (nwarm == 0) {
+        /* the unconstrained solution: done if every bound holds to 1e-13; else the first set =
+         * the violated inputs and each state component's most violated stage */
+        double cv[NZMAX];
+        int ck[NZMAX];
+        for (int i = 0; i < nz; i++) { cv[i] = 0.0; ck[i] = -1; }
+        for (int k = 0; k <= N; k++)
+            for (int i = 0; i < nz; i++) {
+                if (!valid_el(nx, N, k, i)) continue;
+                const int e = k * nz + i;
+                const double zz = z0[e], lb = LBk(d, k, i), ub = UBk(d, k, i);
+                const int lo = has(lb) && zz < lb - 1e-13 * (1.0 + fabs(lb)), hi = has(ub) && zz > ub + 1e-13 * (1.0 + fabs(ub));
+                nbad += lo || hi || !isfinite(zz);
+                const double v = lo ? lb - zz : (hi ? zz - ub : 0.0);
+                if (i >= nx && (lo || hi)) wf[e] = lo ? -1 : 1;   /* inputs join at once */
+                if (i < nx && v > cv[i]) { cv[i] = v; ck[i] = k; }
+            }
+        if (nbad == 0) {
+            for (int e = 0; e < ne; e++) z[e] = z0[e];
+            goto accept;
+        }
+        for (int i = 0; i < nx; i++)
+            if (ck[i] >= 0) {
+                const int e = ck[i] * nz + i;
+                wf[e] = z0[e] < LBk(d, ck[i], i) ? -1 : 1;
+            }
+    }
+    for (int ws = 0; ws < d->polish_steps; ws++) {
+        int S[WSMAX], m = 0;
+        for (int e = 0; e < ne; e++)
+            if (wf[e]) { if (m < WSMAX) S[m] = e; m++; }
+        if (m == 0 || m > WSMAX) return 0;
+        double L[WSMAX][WSMAX], nu_[WSMAX], lt[WSMAX], wd[WSMAX];
+        for (int i = 0; i < m; i++) {
+            const int k = S[i] / nz, c = S[i] % nz;
+            lt[i] = (wf[S[i]] < 0 ? LBk(d, k, c) : UBk(d, k, c)) - z0[S[i]];
+            nu_[i] = lt[i];
+        }
+        for (int i = 0; i < m; i++)
+            for (int j = 0; j <= i; j++) {
+                double s = f->W[(size_t)S[j] * ne + S[i]];
+                if (i == j) wd[i] = s;
+                for (int l = 0; l < j; l++) s -= L[i][l] * L[j][l];
+                if (i == j) {
+                    if (!(s > 0.0)) return 0;
+                    L[i][i] = sqrt(s);
+                } else {
+                    L[i][j] = s / L[j][j];
+                }
+            }
+        for (int i = 0; i < m; i++) {
+            double s = nu_[i];
+            for (int l = 0; l < i; l++) s -= L[i][l] * nu_[l];
+            nu_[i] = s / L[i][i];
+        }
+        for (int i = m - 1; i >= 0; i--) {
+            double s = nu_[i];
+            for (int l = i + 1; l < m; l++) s -= L[l][i] * nu_[l];
+            nu_[i] = s / L[i][i];
+        }
+        (*wsteps)++;
+        *flops += m * m * m / 3.0 + 2.0 * m * m + 2.0 * ne * m;
+        /* multiplier signs (lower: nu >= 0, upper: nu <= 0), measured as the displacement nu_i W_ii
+         * the multiplier causes at its own element: a wrong-sign multiplier of displacement d moves
+         * the solution by about d, so the tolerance is a z-scale one (1e-10 (1 + |b - z_0|), above
+         * the rounding of the W_SS solve, eps cond(W_SS) |b - z_0| <= 1e-11 on the reference models) */
+        int nrem = 0, rem[WSMAX];
+        for (int i = 0; i < m; i++) {
+            const double tol = 1e-10 * (1.0 + fabs(lt[i])), dsp = nu_[i] * wd[i];
+            rem[i] = (wf[S[i]] < 0 && dsp < -tol) || (wf[S[i]] > 0 && dsp > tol) || !isfinite(nu_[i]);
+            nrem += rem[i];
+        }
+        const int addok = ws == 0 || nrem == 0;
+        int wbad = nrem;
+        double cv[NZMAX];
+        int ck[NZMAX];
+        for (int i = 0; i < nz; i++) { cv[i] = 0.0; ck[i] = -1; }
+        signed char nf_[NZMAX * 64];
+        for (int k = 0; k <= N; k++)
+            for (int c = 0; c < nz; c++) {
+                const int e = k * nz + c;
+                nf_[e] = wf[e];
+                if (!valid_el(nx, N, k, c)) { z[e] = z0[e]; continue; }
+                double zz = z0[e];
+                for (int i = 0; i < m; i++) zz += f->W[(size_t)S[i] * ne + e] * nu_[i];
+                const double lb = LBk(d, k, c), ub = UBk(d, k, c);
+                if (wf[e]) {
+                    const double bb = wf[e] < 0 ? lb : ub;
+                    wbad += !(fabs(zz - bb) <= 1e-9 * (1.0 + fabs(bb)));
+                    zz = bb;
+                    for (int i = 0; i < m; i++)
+                        if (rem[i] && S[i] == e) nf_[e] = 0;
+                } else {
+                    const int lo = has(lb) && zz < lb - 1e-13 * (1.0 + fabs(lb)), hi = has(ub) && zz > ub + 1e-13 * (1.0 + fabs(ub));
+                    wbad += lo || hi || !isfinite(zz);
+                    const double v = lo ? lb - zz : (hi ? zz - ub : 0.0);
+                    if (c >= nx && addok && (lo || hi)) nf_[e] = lo ? -1 : 1;
+                    if (c < nx && v > cv[c]) { cv[c] = v; ck[c] = k; }
+                }
+                z[e] = zz;
+            }
+        memcpy(wf, nf_, (size_t)ne);
+        if (addok)
+            for (int c = 0; c < nx; c++)
+                if (ck[c] >= 0) {
+                    const int e = ck[c] * nz + c;
+                    wf[e] = z[e] < LBk(d, ck[c], c) ? -1 : 1;
+                }
+        if (wbad == 0) goto accept;
+    }
+    return 0;
+accept:
+    for (int k = 0; k <= N; k++)
+        for (int i = 0; i < nz; i++) {
+            const int e = k * nz + i;
+            if (!valid_el(nx, N, k, i)) continue;
+            const double lb = LBk(d, k, i), ub = UBk(d, k, i);
+            if (has(lb) && z[e] < lb) z[e] = lb;
+            if (has(ub) && z[e] > ub) z[e] = ub;
+        }
+    return 1;
+}
+
+static void crazyflie_rhs_ref(const double x[4], double st, double ct, double Fd, double inv_m, double g, double f[4])
+{
+    f[0] = x[2];
+    f[1] = x[3];
+    f[2] = inv_m * Fd * st;
+    f[3] = inv_m * Fd * ct - g;
+}
+
+/* the plant step, cost and AED of one instance (nmpc_cl_device.h cl_advance_instance's order) */
+static void cl_advance_ref(const ocp_ref_desc *d, const cl_ref_desc *c, double *st, const double *xo, const double *u0,
+                           const double *xref, double w, double *acc, int status)
+{
+    const int nx = d->nx, nu = d->nu;
+    double cost = 0.0, aed = 0.0;
+    for (int i = 0; i < c->ncl; i++) {
+        const double e = xo[i] - xref[i];
+        cost += c->wcl[i] * e * e;
+    }
+    for (int i = 0; i < c->aed_dims; i++) aed += fabs(xref[i] - st[i]);
+    if (c->plant == 0) {
+        double xn[NZMAX];
+        for (int i = 0; i < nx; i++) {
+            double s = d->c[i];
+            for (int j = 0; j < nx; j++) s += d->A[i * nx + j] * st[j];
+            for (int j = 0; j < nu; j++) s += d->B[i * nu + j] * u0[j];
+            xn[i] = s;
+        }
+        for (int i = 0; i < nx; i++) st[i] = xn[i] + (i < c->noise_dims ? w : 0.0);
+    } else {
+        double x[4], f[4];
+        const double inv_m = 1.0 / c->mass;
+        for (int i = 0; i < 4; i++) x[i] = st[i];
+        if (c->plant == 1) {
+            const double Fx = u0[0], Fz = u0[1], th = atan2(Fx, Fz), Fd = sqrt(Fx * Fx + Fz * Fz);
+            const double s_ = sin(th), c_ = cos(th), h = c->dt;
+            double k1[4], k2[4], k3[4], k4[4], tt[4];
+            crazyflie_rhs_ref(x, s_, c_, Fd, inv_m, c->g, k1);
+            for (int i = 0; i < 4; i++) tt[i] = x[i] + 0.5 * h * k1[i];
+            crazyflie_rhs_ref(tt, s_, c_, Fd, inv_m, c->g, k2);
+            for (int i = 0; i < 4; i++) tt[i] = x[i] + 0.5 * h * k2[i];
+            crazyflie_rhs_ref(tt, s_, c_, Fd, inv_m, c->g, k3);
+            for (int i = 0; i < 4; i++) tt[i] = x[i] + h * k3[i];
+            crazyflie_rhs_ref(tt, s_, c_, Fd, inv_m, c->g, k4);
+            for (int i = 0; i < 4; i++) x[i] += h / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+            for (int i = 0; i < 4; i++) st[i] = x[i] + w;
+        } else {
+            double a0 = st[4], a1 = st[5];
+            const double h0 = u0[0], h1 = u0[1];
+            for (int j = 0; j < c->substeps; j++) {
+                a0 = a0 + h0 * c->dt_conv;
+                a1 = a1 + h1 * c->dt_conv;
+                const double Fx = c->mass * a0, Fz = c->mass * a1, th = atan2(Fx, Fz), Fd = sqrt(Fx * Fx + Fz * Fz);
+                crazyflie_rhs_ref(x, sin(th), cos(th), Fd, inv_m, c->g, f);
+                for (int i = 0; i < 4; i++) x[i] += c->dt_conv * f[i];
+            }
+            for (int i = 0; i < 4; i++) st[i] = x[i] + w;
+            st[4] = a0;
+            st[5] = a1;
+        }
+    }
+    acc[0] += cost;
+    acc[1] += aed;
+    acc[2] += status != 0 ? 1.0 : 0.0;
+    acc[3] += 1.0;
+}
+
+/* Oracle refinement of an exact-finish solution (mode 0): the equality-constrained QP with the
+ * solution's active bounds held is solved by a dense LU of its KKT matrix (independent of the
+ * Riccati recursion and of the projected inverse Hessian W), the bound multipliers are read off
+ * and the set is corrected primal-dual active-set style until every held bound has a multiplier
+ * of the right sign (to 1e-13 (1 + |mu|max)) and every other bound holds (to 1e-12 (1 + |b|)).
+ * The penalised finish decides a held bound's multiplier sign on z - b, which cannot resolve a
+ * small multiplier of a low-curvature element (quad13's angular accelerations, R = 2e-4: a sign
+ * error of 1e-7 moves the input by 1e-5); this pass removes that limit from the oracle. Variables
+ * z = [x_k; u_k] stage-stacked ((N+1) nz, stage N's input slots carry a unit Hessian and no
+ * gradient). Returns the number of set corrections, or -1 if it did not settle (z untouched). */
+static int kkt_refine(const ocp_ref_desc *d, const double *x0, const double *yref, double *xo, double *uo)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = (N + 1) * nz, ny = d->ny;
+    signed char *act = (signed char *)calloc(ne, 1);
+    double *z = (double *)malloc(sizeof(double) * ne), *g = (double *)calloc(ne, sizeof(double));
+    int m = 0;
+    for (int k = 0; k <= N; k++)
+        for (int i = 0; i < nz; i++) {
+            const int e = k * nz + i;
+            z[e] = i < nx ? xo[k * nx + i] : (k < N ? uo[k * nu + i - nx] : 0.0);
+            if (!valid_el(nx, N, k, i)) continue;
+            const double lb = LBk(d, k, i), ub = UBk(d, k, i);
+            if (has(lb) && fabs(z[e] - lb) <= 1e-9 * (1.0 + fabs(lb))) act[e] = -1;
+            else if (has(ub) && fabs(z[e] - ub) <= 1e-9 * (1.0 + fabs(ub))) act[e] = 1;
+            m += act[e] != 0;
+        }
+    for (int k = 0; k <= N; k++) {
+        const int n = k < N ? nz : nx, nyk = k < N ? ny : d->ny_e;
+        const double *Gm = k < N ? d->G : d->Ge, *y = yref + (size_t)k * ny;
+        for (int i = 0; i < n; i++) {
+            double s_ = 0.0;
+            for (int j = 0; j < nyk; j++) s_ += Gm[i * nyk + j] * y[j];
+            g[k * nz + i] = s_;
+        }
+    }
+    int result = -1;
+    if (m == 0) { result = 0; goto out; }
+    for (int pass = 0; pass < 30; pass++) {
+        m = 0;
+        for (int e = 0; e < ne; e++) m += act[e] != 0;
+        const int neq = nx + N * nx + m, n = ne + neq;
+        double *K = (double *)calloc((size_t)n * n, sizeof(double)), *r = (double *)calloc(n, sizeof(double));
+        for (int k = 0; k <= N; k++)
+            for (int i = 0; i < nz; i++)
+                for (int j = 0; j < nz; j++) {
+                    double h;
+                    if (k < N) h = d->H[i * nz + j];
+                    else h = (i < nx && j < nx) ? d->He[i * nx + j] : (i == j ? 1.0 : 0.0);
+                    K[(size_t)(k * nz + i) * n + k * nz + j] = h;
+                }
+        for (int e = 0; e < ne; e++) r[e] = -g[e];
+        int row = ne;
+        for (int i = 0; i < nx; i++, row++) {   /* x_0 = x0 */
+            K[(size_t)row * n + i] = K[(size_t)i * n + row] = 1.0;
+            r[row] = x0[i];
+        }
+        for (int k = 0; k < N; k++)             /* x_{k+1} - A x_k - B u_k = c */
+            for (int i = 0; i < nx; i++, row++) {
+                const int e1 = (k + 1) * nz + i;
+                K[(size_t)row * n + e1] = K[(size_t)e1 * n + row] = 1.0;
+                for (int j = 0; j < nz; j++) {
+                    const double a = j < nx ? d->A[i * nx + j] : d->B[i * nu + j - nx];
+                    K[(size_t)row * n + k * nz + j] = K[(size_t)(k * nz + j) * n + row] = -a;
+                }
+                r[row] = d->c[i];
+            }
+        int brow[NZMAX * 64];
+        for (int e = 0; e < ne; e++)
+            if (act[e]) {                      /* z_e = b_e */
+                const int k = e / nz, i = e % nz;
+                K[(size_t)row * n + e] = K[(size_t)e * n + row] = 1.0;
+                r[row] = act[e] < 0 ? LBk(d, k, i) : UBk(d, k, i);
+                brow[e] = row++;
+            }
+        /* LU with partial pivoting, in place */
+        int ok = 1;
+        for (int c = 0; c < n && ok; c++) {
+            int p = c;
+            for (int q = c + 1; q < n; q++)
+                if (fabs(K[(size_t)q * n + c]) > fabs(K[(size_t)p * n + c])) p = q;
+            if (fabs(K[(size_t)p * n + c]) < 1e-300) { ok = 0; break; }
+            if (p != c) {
+                for (int j = 0; j < n; j++) { double t = K[(size_t)c * n + j]; K[(size_t)c * n + j] = K[(size_t)p * n + j]; K[(size_t)p * n + j] = t; }
+                double t = r[c]; r[c] = r[p]; r[p] = t;
+            }
+            const double inv = 1.0 / K[(size_t)c * n + c];
+            for (int q = c + 1; q < n; q++) {
+                const double f = K[(size_t)q * n + c] * inv;
+                if (f == 0.0) continue;
+                for (int j = c + 1; j < n; j++) K[(size_t)q * n + j] -= f * K[(size_t)c * n + j];
+                r[q] -= f * r[c];
+            }
+        }
+        if (ok)
+            for (int c = n - 1; c >= 0; c--) {
+                double s_ = r[c];
+                for (int j = c + 1; j < n; j++) s_ -= K[(size_t)c * n + j] * r[j];
+                r[c] = s_ / K[(size_t)c * n + c];
+            }
+        free(K);
+        if (!ok) { free(r); break; }
+        /* multipliers of the held bounds: stationarity H z + g + E' mu = 0, so a held lower bound
+         * has lambda = -mu >= 0 and an upper one lambda = mu >= 0 */
+        double mmax = 0.0;
+        for (int e = 0; e < ne; e++)
+            if (act[e]) mmax = fmax(mmax, fabs(r[brow[e]]));
+        int changed = 0;
+        signed char nact[NZMAX * 64];
+        for (int e = 0; e < ne; e++) {
+            const int k = e / nz, i = e % nz;
+            nact[e] = act[e];
+            if (!valid_el(nx, N, k, i)) continue;
+            const double lb = LBk(d, k, i), ub = UBk(d, k, i), ze = r[e];
+            if (act[e]) {
+                const double lam = act[e] < 0 ? -r[brow[e]] : r[brow[e]];
+                if (lam < -1e-13 * (1.0 + mmax)) { nact[e] = 0; changed++; }
+            } else if (has(lb) && ze < lb - 1e-12 * (1.0 + fabs(lb))) { nact[e] = -1; changed++; }
+            else if (has(ub) && ze > ub + 1e-12 * (1.0 + fabs(ub))) { nact[e] = 1; changed++; }
+        }
+        if (!changed) {
+            for (int k = 0; k <= N; k++) {
+                for (int i = 0; i < nx; i++) xo[k * nx + i] = r[k * nz + i];
+                if (k < N)
+                    for (int i = 0; i < nu; i++) uo[k * nu + i] = r[k * nz + nx + i];
+            }
+            free(r);
+            result = pass;
+            break;
+        }
+        memcpy(act, nact, ne);
+        free(r);
+    }
+out:
+    free(act); free(z); free(g);
+    return result;
+}
+
+/* Run `steps` closed-loop steps (global steps step0 .. step0 + steps - 1) of `batch` instances.
+ * state [batch][nx] and acc [batch][4] in/out; act [batch][(N+1) nz] (mode 1: the last solution's
+ * active flags, in/out) and failed [batch] (the last step failed, in/out). Optional logs, per
+ * instance and step: the applied input u0 [batch][steps][nu], the state after the step
+ * [batch][steps][nx], the status and the path (0 fast unconstrained, 1 fast active-set steps,
+ * 2 full solve) [batch][steps]. counters[10] (added to): solves, fast-unconstrained, fast-set
+ * accepted, fast active-set steps, full solves, failures, FP64 flops of the path taken (mode 1;
+ * mode 0: F_iter per Newton system), Newton systems of the full solves, and (mode 0) solutions
+ * whose active set kkt_refine corrected / could not settle. Returns the failures. */
+int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int batch, int step0, int steps,
+                            const int *offsets, double *state, double *acc, signed char *act, unsigned char *failed,
+                            int mode, double *u_log, double *x_log, int *status_log, int *path_log, double *counters,
+                            int nthreads)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ny = d->ny, nye = d->ny_e, ne = (N + 1) * nz;
+    if (nx + nu > NZMAX || d->ny != nz || d->ny_e != nx || c->period < 1 || c->period - 1 + N >= c->rows ||
+        c->cols < ny || ne > NZMAX * 64)
+        return -1;
+    fast_tables *f = mode == 1 ? fast_init(d, c) : NULL;
+    const double fi = f_iter(nx, nu, N);
+    double cnt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int nfail = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+    nthreads = 1;
+#endif
+#pragma omp parallel num_threads(nthreads) reduction(+ : nfail, cnt[:10])
+    {
+        const size_t S = (size_t)(N + 1) * nz;
+        double *buf = (double *)malloc(sizeof(double) * (9 * S + (size_t)N * (2 * nx + nu * nu + nx * nu + nu)) + S);
+        ws_t w;
+        w.z = buf; w.ll = w.z + S; w.lu = w.ll + S; w.dza = w.lu + S; w.dz = w.dza + S;
+        w.gc = w.dz + S; w.gf = w.gc + S; w.gh = w.gf + S;
+        w.re = w.gh + S; w.Pr = w.re + (size_t)N * nx; w.Luu = w.Pr + (size_t)N * nx;
+        w.Lxu = w.Luu + (size_t)N * nu * nu; w.lu_vec = w.Lxu + (size_t)N * nx * nu;
+        w.sg = w.lu_vec + (size_t)N * nu;
+        w.act = (signed char *)(w.sg + S);
+        double *yref = (double *)malloc(sizeof(double) * ((size_t)N * ny + nye));
+        double *xo = (double *)malloc(sizeof(double) * (N + 1) * nx), *uo = (double *)malloc(sizeof(double) * N * nu);
+        double *z0 = (double *)malloc(sizeof(double) * ne), *zf = (double *)malloc(sizeof(double) * ne);
+        signed char *wf = (signed char *)malloc(ne);
+#pragma omp for schedule(dynamic, 4)
+        for (int b = 0; b < batch; b++) {
+            double *st = state + (size_t)b * nx;
+            signed char *ab = act ? act + (size_t)b * ne : NULL;
+            for (int s = 0; s < steps; s++) {
+                const int step = step0 + s, t = (int)(((long long)offsets[b] + step) % c->period);
+                for (int k = 0; k < N; k++) memcpy(yref + (size_t)k * ny, c->table + (size_t)(t + k) * c->cols, sizeof(double) * ny);
+                memcpy(yref + (size_t)N * ny, c->table + (size_t)(t + N) * c->cols, sizeof(double) * nye);
+                int status = 0, path = 2, iters = 0, ok = 0;
+                const int warm = mode == 1 && step > 0 && ab != NULL;
+                if (warm) {   /* the previous solution's flags shifted by one stage */
+                    for (int k = 0; k <= N; k++)
+                        for (int i = 0; i < nz; i++)
+                            wf[k * nz + i] = valid_el(nx, N, k, i) ? ab[(k < N ? k + 1 : k) * nz + i] : 0;
+                    if (d->polish_mu > 0.0) {
+                        int wst = 0, nw = 0;
+                        for (int e = 0; e < ne; e++) nw += wf[e] != 0;
+                        ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6]);
+                        cnt[3] += wst;
+                        if (ok) {
+                            path = (nw == 0 && wst == 0) ? 0 : 1;
+                            cnt[path == 0 ? 1 : 2] += 1;
+                            for (int k = 0; k <= N; k++) {
+                                for (int i = 0; i < nx; i++) xo[k * nx + i] = zf[k * nz + i];
+                                if (k < N)
+                                    for (int i = 0; i < nu; i++) uo[k * nu + i] = zf[k * nz + nx + i];
+                            }
+                        }
+                    }
+                }
+                if (!ok) {
+                    status = solve_one(d, st, yref, xo, uo, &iters, &w, warm ? wf : NULL, 0);
+                    if (mode == 0 && status == 0) {
+                        const int kr = kkt_refine(d, st, yref, xo, uo);
+                        cnt[kr < 0 ? 9 : 8] += kr != 0;
+                    }
+                    cnt[4] += 1;
+                    cnt[7] += iters;
+                    cnt[6] += fi * iters;
+                }
+                cnt[0] += 1;
+                if (ab) {   /* the solution's active flags (z on a bound to 1e-7); inputs of stage N mirror N - 1 */
+                    for (int k = 0; k <= N; k++)
+                        for (int i = 0; i < nz; i++) {
+                            const int e = k * nz + i;
+                            if (k == N && i >= nx) { ab[e] = ab[(N - 1) * nz + i]; continue; }
+                            const double zz = i < nx ? xo[k * nx + i] : uo[k * nu + i - nx];
+                            const double lb = LBk(d, k, i), ub = UBk(d, k, i);
+                            ab[e] = (has(lb) && zz <= lb + 1e-7 * (1.0 + fabs(lb))) ? -1
+                                  : (has(ub) && zz >= ub - 1e-7 * (1.0 + fabs(ub))) ? 1 : 0;
+                        }
+                }
+                if (failed) failed[b] = status > 0;
+                if (status) { cnt[5] += 1; nfail++; }
+                double wn = 0.0;
+                if (c->noise) wn = step < c->noise_len ? c->noise[(size_t)b * c->noise_len + step] : 0.0;
+                else if (c->noise_std > 0)
+                    wn = c->noise_std * philox_normal(c->seed, (unsigned long long)(c->inst_ids ? c->inst_ids[b] : c->inst_base + b),
+                                                      (unsigned long long)step);
+                cl_advance_ref(d, c, st, xo + (size_t)c->cost_stage * nx, uo, c->table + (size_t)t * c->cols, wn,
+                               acc + (size_t)b * 4, status);
+                cnt[6] += 2.0 * nx * nz;
+                if (u_log) memcpy(u_log + ((size_t)b * steps + s) * nu, uo, sizeof(double) * nu);
+                if (x_log) memcpy(x_log + ((size_t)b * steps + s) * nx, st, sizeof(double) * nx);
+                if (status_log) status_log[(size_t)b * steps + s] = status;
+                if (path_log) path_log[(size_t)b * steps + s] = path;
+            }
+        }
+        free(buf); free(yref); free(xo); free(uo); free(z0); free(zf); free(wf);
+    }
+    fast_free(f);
+    if (counters)
+        for (int i = 0; i < 10; i++) counters[i] += cnt[i];
+    return nfail;
 }

@@ -128,3 +128,105 @@ class RiccatiIpmRef:
         if rc < 0:
             raise ValueError("riccati_ipm_solve_batch rejected the problem dimensions")
         return X, U, st, it
+
+
+class _ClDesc(ctypes.Structure):
+    _fields_ = [
+        ("plant", ctypes.c_int), ("table", ctypes.c_void_p),
+        ("rows", ctypes.c_int), ("cols", ctypes.c_int), ("period", ctypes.c_int),
+        ("cost_stage", ctypes.c_int), ("ncl", ctypes.c_int), ("aed_dims", ctypes.c_int),
+        ("noise_dims", ctypes.c_int), ("substeps", ctypes.c_int),
+        ("wcl", ctypes.c_void_p),
+        ("mass", ctypes.c_double), ("g", ctypes.c_double), ("dt", ctypes.c_double), ("dt_conv", ctypes.c_double),
+        ("noise", ctypes.c_void_p), ("noise_len", ctypes.c_int),
+        ("noise_std", ctypes.c_double), ("seed", ctypes.c_ulonglong), ("inst_base", ctypes.c_longlong),
+        ("inst_ids", ctypes.c_void_p),
+    ]
+
+
+class ClosedLoopRef:
+    """CPU restatement of the device closed loop (nmpc_closed_loop_run; oracle/c/riccati_ipm.c
+    riccati_ipm_closed_loop): per instance and step the yref window from the shared reference
+    table at row (offset + step) % period (force_model/ocp.py:117-122), x0 pinned to the state
+    (force_model/controller.py:29-31), the solve (controller.py:32), cost (controller.py:40-41),
+    AED numerator (store_results.py:233-236) and the plant with its noise draw.
+
+    model: "force" | "jerk" | "quad13" (plants: Crazyflie + force converter, Crazyflie + jerk
+    converter, the controller's own discrete model). mode 0 = the oracle (every QP solved cold
+    to its exact solution); mode 1 = the GPU's algorithm (warm-started fast finish on the shared
+    factorisation, full solves only where it fails) — the closed-loop CPU baseline. Noise: the
+    injected `noise_table` [batch, steps] if given, else the device's Philox stream
+    (seed, instance_base + b or instance_ids[b], step) x noise_std."""
+
+    PLANTS = {"quad13": 0, "force": 1, "jerk": 2}
+
+    def __init__(self, spec, model, table, offsets, x_init, mode=0, noise_table=None, seed=42, instance_base=0,
+                 noise_std=None, tol_comp=None, tol_res=None, polish_mu=DEFAULT_POLISH_MU,
+                 polish_steps=DEFAULT_POLISH_STEPS, period=None, instance_ids=None):
+        from . import params as P
+        self.ipm = RiccatiIpmRef(spec, tol_comp=tol_comp or 1e-15, tol_res=tol_res or 1e-12, polish_mu=polish_mu,
+                                 polish_steps=polish_steps)
+        self.lib = self.ipm.lib
+        self.lib.riccati_ipm_closed_loop.restype = ctypes.c_int
+        self.spec, self.model, self.mode = spec, model, int(mode)
+        nx, N = spec.nx, spec.N
+        self.batch = len(offsets)
+        keep = self._keep = {
+            "table": np.ascontiguousarray(table, dtype=np.float64),
+            "offsets": np.ascontiguousarray(offsets, dtype=np.int32),
+            "wcl": np.array([1e2] * 3 + [1e0] * 3 if model == "quad13" else list(P.W_CL), dtype=np.float64),
+        }
+        self.state = np.ascontiguousarray(x_init, dtype=np.float64).reshape(self.batch, nx).copy()
+        self.acc = np.zeros((self.batch, 4))
+        self.act = np.zeros((self.batch, (N + 1) * (nx + spec.nu)), dtype=np.int8)
+        self.failed = np.zeros(self.batch, dtype=np.uint8)
+        self.step = 0
+        self.counters = np.zeros(10)
+        d = self.desc = _ClDesc()
+        d.plant = self.PLANTS[model]
+        d.table = keep["table"].ctypes.data
+        d.rows, d.cols = keep["table"].shape
+        d.period = int(period or P.N_SIM)
+        d.cost_stage = 1 if model == "jerk" else 0
+        d.ncl = keep["wcl"].size
+        d.aed_dims = 3 if model == "quad13" else 2
+        d.noise_dims = 6 if model == "quad13" else nx
+        d.substeps = P.CTRLS_PER_SAMPLE
+        d.wcl = keep["wcl"].ctypes.data
+        d.mass, d.g, d.dt, d.dt_conv = P.MASS, P.GRAVITY_ACC, P.DT, P.DT_CONV
+        if noise_table is not None:
+            keep["noise"] = np.ascontiguousarray(noise_table, dtype=np.float64).reshape(self.batch, -1)
+            d.noise, d.noise_len = keep["noise"].ctypes.data, keep["noise"].shape[1]
+        d.noise_std = P.NOISE if noise_std is None else float(noise_std)
+        d.seed, d.inst_base = int(seed), int(instance_base)
+        if instance_ids is not None:   # global ids of a subset of instances (Philox stream)
+            keep["ids"] = np.ascontiguousarray(instance_ids, dtype=np.int64)
+            d.inst_ids = keep["ids"].ctypes.data
+
+    def run(self, steps, nthreads=None, logs=False):
+        """Advance `steps` steps. logs=True returns per-step (u0 [B, steps, nu], state after the
+        step [B, steps, nx], status [B, steps], path [B, steps]: 0 fast unconstrained, 1 fast
+        active-set steps, 2 full solve)."""
+        sp, B = self.spec, self.batch
+        lg = None
+        if logs:
+            lg = (np.zeros((B, steps, sp.nu)), np.zeros((B, steps, sp.nx)), np.zeros((B, steps), dtype=np.int32),
+                  np.zeros((B, steps), dtype=np.int32))
+        p = lambda a: ctypes.c_void_p(a.ctypes.data) if a is not None else None
+        rc = self.lib.riccati_ipm_closed_loop(
+            ctypes.byref(self.ipm.desc), ctypes.byref(self.desc), B, self.step, int(steps),
+            p(self._keep["offsets"]), p(self.state), p(self.acc), p(self.act), p(self.failed), self.mode,
+            *(p(a) for a in (lg or (None,) * 4)), p(self.counters),
+            int(nthreads) if nthreads else self.ipm.max_threads())
+        if rc < 0:
+            raise ValueError("riccati_ipm_closed_loop rejected the problem")
+        self.step += steps
+        return lg
+
+    def stats(self):
+        """Counters: solves, fast unconstrained, fast active-set accepted, fast active-set steps,
+        full solves, failures, FP64 flops of the paths taken, Newton systems of the full solves,
+        (mode 0) solutions whose active set the dense KKT pass corrected / could not settle."""
+        k = ("solves", "fast_unconstrained", "fast_set", "fast_set_steps", "full", "failed", "flops", "full_newton",
+             "kkt_corrected", "kkt_unsettled")
+        return dict(zip(k, self.counters.tolist()))
