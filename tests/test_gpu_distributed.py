@@ -42,7 +42,10 @@ def _bench(args, world):
 def test_force_two_ranks_reduce_equals_one_process():
     """Split across the kernel-family crossover: each rank's 4096 instances run the wavefront
     family, the single process's 8192 the lane-per-component family (fp64 force crossover at
-    B = 8192, nmpc_ipm.hip kernel_kind) — sharding must not change the statistics either way."""
+    B = 8192, nmpc_ipm.hip kernel_kind) — sharding must not change the statistics either way.
+    Across the families the sums agree to the solvers' precision (1e-8 relative; both families
+    return the exact QP solutions, by different paths), not bit for bit (a family bug that moved a
+    solution showed as 7e-7 relative in round 2)."""
     common = ["--model", "force", "--steps", "4", "--warmup", "2", "--repeats", "2", "--no-cpu-baseline"]
     two = _bench(common + ["--gpus", "2", "--batch", "4096"], 2)
     one = _bench(common + ["--gpus", "1", "--batch", "8192"], 1)
@@ -51,8 +54,8 @@ def test_force_two_ranks_reduce_equals_one_process():
     a, b = two["closed_loop"], one["closed_loop"]
     assert a["instance_steps"] == b["instance_steps"] == 8192 * (2 + 2 * 4)
     assert a["failed_solves"] == b["failed_solves"]
-    assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=1e-10)
-    assert a["aed"] == pytest.approx(b["aed"], rel=1e-10)
+    assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=1e-8)
+    assert a["aed"] == pytest.approx(b["aed"], rel=1e-8)
     assert two["value"] > 0 and len(two["timing"]["region_ms"]) == 2
 
 
