@@ -743,8 +743,46 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     }
                     const int m = (int)gsum(r == NZ - 1 ? T(pre) : T(0));   // the last lane's prefix = |S|
                     pre -= nmine;   // exclusive prefix
+                    // restart: a group whose set is empty (every held bound left) is at the unconstrained
+                    // solution z_0 — accepted if every bound holds (1e-13), else its set becomes the
+                    // violated inputs and each state component's most violated stage (this round takes
+                    // no active-set step; oracle/c/riccati_ipm.c fast_finish)
+                    const bool rst = wrun && m == 0;
+                    if (__any(rst)) {
+                        T nb = 0, cv3 = 0, cs3 = 0;
+                        int ck3 = -1;
+                        for (int k = 0; rst && k <= N; k++) {
+                            if ((k == N && ul) || (k == 0 && xl)) continue;
+                            const T z = ldE(L::Z, k);
+                            const Bd b_ = bnd(k);
+                            const T tl = T(1e-13) * (T(1) + fabs(b_.lb)), tu = T(1e-13) * (T(1) + fabs(b_.ub));
+                            const bool lo_ = has_bound(b_.lb) && z < b_.lb - tl, hi_ = has_bound(b_.ub) && z > b_.ub + tu;
+                            nb += (lo_ || hi_ || !isfinite(z)) ? T(1) : T(0);
+                            const T v_ = lo_ ? b_.lb - z : (hi_ ? z - b_.ub : T(0));
+                            if (ul && (lo_ || hi_)) {
+                                if (amask) mset(wm, k, lo_ ? T(-1) : T(1));
+                                else stE(L::DZA, k, lo_ ? T(-1) : T(1));
+                            }
+                            ck3 = v_ > cv3 ? k : ck3;
+                            cs3 = v_ > cv3 ? (lo_ ? T(-1) : T(1)) : cs3;
+                            cv3 = fmax(cv3, v_);
+                            fin_out(k, z, b_);   // tentative outputs (z_0 accepted)
+                        }
+                        if (rst && xl && ck3 >= 0) {
+                            if (amask) mset(wm, ck3, cs3);
+                            else stE(L::DZA, ck3, cs3);
+                        }
+                        nb = gsum(nb);
+                        const bool acc0 = rst && nb == T(0);
+                        fast_ok = fast_ok || acc0;
+                        wrun = wrun && !acc0;
+                    }
+                    // the groups that take an active-set step this round (a set larger than WSMAX ends
+                    // the group's fast finish: it runs the full solve)
+                    bool wact = wrun && !rst && m <= WSMAX;
+                    wrun = wrun && (rst || m <= WSMAX);
                     LPC_SYNC();
-                    if (wrun && m <= WSMAX) {
+                    if (wact) {
                         int q_ = pre;
                         for (int k = 0; k <= N; k++) {
                             const T f = ((k < N || xl) && !(k == 0 && xl)) ? (amask ? mflag(wm, k) : ldE(L::DZA, k)) : T(0);
@@ -758,14 +796,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         }
                     }
                     LPC_SYNC();
-                    wrun = wrun && m >= 1 && m <= WSMAX;
                     // nu = W_SS^{-1} (b - z_0)_S by Cholesky, every lane (m <= WSMAX)
                     T L_[WSMAX][WSMAX], nu_[WSMAX], wd_[WSMAX];
                     int ei[WSMAX];
 #pragma unroll
                     for (int i = 0; i < WSMAX; i++) {
-                        ei[i] = (wrun && i < m) ? (int)le[i] : 0;
-                        nu_[i] = (wrun && i < m) ? lt[i] : T(0);
+                        ei[i] = (wact && i < m) ? (int)le[i] : 0;
+                        nu_[i] = (wact && i < m) ? lt[i] : T(0);
                     }
                     bool pdf = true;
 #pragma unroll
@@ -797,7 +834,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                         for (int l = i + 1; l < WSMAX; l++) s_ = fma(-L_[l][i], nu_[l], s_);
                         nu_[i] = s_ / L_[i][i];
                     }
-                    wrun = wrun && pdf;
+                    wrun = wrun && (!wact || pdf);   // W_SS not positive definite: the full solve
+                    wact = wact && pdf;
                     // multiplier signs (lower: nu >= 0, upper: nu <= 0), measured as the displacement
                     // nu_i W_ii the multiplier causes at its own element: a wrong-sign multiplier of
                     // displacement d moves the solution by about d, so the tolerance is a z-scale one,
@@ -841,12 +879,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             const bool lo_ = has_bound(b_.lb) && z < b_.lb - tl, hi_ = has_bound(b_.ub) && z > b_.ub + tu;
                             wbad += (lo_ || hi_ || !isfinite(z)) ? T(1) : T(0);
                             const T v_ = lo_ ? b_.lb - z : (hi_ ? z - b_.ub : T(0));
-                            if (ul && addok && (lo_ || hi_)) nf = lo_ ? T(-1) : T(1);
+                            if (ul && (lo_ || hi_)) nf = lo_ ? T(-1) : T(1);   // inputs join at once
                             ck2 = v_ > cv2 ? k : ck2;
                             cs2 = v_ > cv2 ? (lo_ ? T(-1) : T(1)) : cs2;
                             cv2 = fmax(cv2, v_);
                         }
-                        if (wrun) {
+                        if (wact) {
                             if (nf != f) {
                                 if (amask) mset(wm, k, nf);
                                 else stE(L::DZA, k, nf);
@@ -854,13 +892,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                             fin_out(k, z, b_);
                         }
                     }
-                    if (wrun && xl && addok && ck2 >= 0) {
+                    if (wact && xl && addok && ck2 >= 0) {
                         if (amask) mset(wm, ck2, cs2);
                         else stE(L::DZA, ck2, cs2);
                     }
                     wbad = gsum(wbad);
-                    fin_ws += wrun ? 1 : 0;
-                    const bool acc = wrun && wbad == T(0);
+                    fin_ws += wact ? 1 : 0;
+                    const bool acc = wact && wbad == T(0);
                     fast_ok = fast_ok || acc;
                     wrun = wrun && !acc;
                     LPC_SYNC();

@@ -785,6 +785,7 @@ typedef struct {
 #define WSMAX 8
 #endif
 
+
 /* Philox4x32-10 + Box-Muller: the device's noise stream (nmpc_cl_device.h philox_normal_dev) */
 static double philox_normal(unsigned long long seed, unsigned long long inst, unsigned long long step)
 {
@@ -990,15 +991,16 @@ static void fast_free(fast_tables *f)
 static int valid_el(int nx, int N, int k, int i) { return !(k == 0 && i < nx) && (k < N || i < nx); }
 
 /* The fast finish of one step (mode 1). wf: the warm set (shifted flags, in), the set reached
- * (out). Returns 1 and the solution in z (clamped onto the bounds) when accepted; counts the
- * active-set steps and the FP64 work. */
+ * (out). Returns 1 and the solution in z (clamped onto the bounds) when accepted, else why not:
+ * -2 a set larger than WSMAX, -3 W_SS not positive definite (linearly dependent bounds: an
+ * infeasible QP), -4 polish_steps rounds without acceptance. Counts the active-set steps and the
+ * FP64 work. */
 static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double *x0, int t, signed char *wf,
                        double *z0, double *z, int *wsteps, double *flops)
 {
     const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
     const double *vt = f->v + (size_t)t * ne;
-    int nwarm = 0, nbad = 0;
-    for (int e = 0; e < ne; e++) nwarm += wf[e] != 0;
+    int nbad = 0;
     *wsteps = 0;
     for (int k = 0; k <= N; k++)
         for (int i = 0; i < nz; i++) {
@@ -1010,38 +1012,44 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
             z0[e] = s;
             *flops += 2.0 * nx;
         }
-    if (nwarm == 0) {
-        /* the unconstrained solution: done if every bound holds to 1e-13; else the first set =
-         * the violated inputs and each state component's most violated stage */
-        double cv[NZMAX];
-        int ck[NZMAX];
-        for (int i = 0; i < nz; i++) { cv[i] = 0.0; ck[i] = -1; }
-        for (int k = 0; k <= N; k++)
-            for (int i = 0; i < nz; i++) {
-                if (!valid_el(nx, N, k, i)) continue;
-                const int e = k * nz + i;
-                const double zz = z0[e], lb = LBk(d, k, i), ub = UBk(d, k, i);
-                const int lo = has(lb) && zz < lb - 1e-13 * (1.0 + fabs(lb)), hi = has(ub) && zz > ub + 1e-13 * (1.0 + fabs(ub));
-                nbad += lo || hi || !isfinite(zz);
-                const double v = lo ? lb - zz : (hi ? zz - ub : 0.0);
-                if (i >= nx && (lo || hi)) wf[e] = lo ? -1 : 1;   /* inputs join at once */
-                if (i < nx && v > cv[i]) { cv[i] = v; ck[i] = k; }
-            }
-        if (nbad == 0) {
-            for (int e = 0; e < ne; e++) z[e] = z0[e];
-            goto accept;
-        }
-        for (int i = 0; i < nx; i++)
-            if (ck[i] >= 0) {
-                const int e = ck[i] * nz + i;
-                wf[e] = z0[e] < LBk(d, ck[i], i) ? -1 : 1;
-            }
-    }
-    for (int ws = 0; ws < d->polish_steps; ws++) {
+    for (int ws = 0, first = 1; ws < d->polish_steps; first = 0) {
         int S[WSMAX], m = 0;
         for (int e = 0; e < ne; e++)
             if (wf[e]) { if (m < WSMAX) S[m] = e; m++; }
-        if (m == 0 || m > WSMAX) return 0;
+        if (m == 0) {
+            /* no bound held (an empty warm set, or every held bound left): the iterate is the
+             * unconstrained solution z_0 — done if every bound holds to 1e-13; else the set = the
+             * violated inputs and each state component's most violated stage. Before any step
+             * (empty warm set) this is the first set; later it takes one of the polish_steps rounds
+             * (the GPU's restart pass) */
+            double cv[NZMAX];
+            int ck[NZMAX];
+            if (!first) ws++;
+            for (int i = 0; i < nz; i++) { cv[i] = 0.0; ck[i] = -1; }
+            nbad = 0;
+            for (int k = 0; k <= N; k++)
+                for (int i = 0; i < nz; i++) {
+                    if (!valid_el(nx, N, k, i)) continue;
+                    const int e = k * nz + i;
+                    const double zz = z0[e], lb = LBk(d, k, i), ub = UBk(d, k, i);
+                    const int lo = has(lb) && zz < lb - 1e-13 * (1.0 + fabs(lb)), hi = has(ub) && zz > ub + 1e-13 * (1.0 + fabs(ub));
+                    nbad += lo || hi || !isfinite(zz);
+                    const double v = lo ? lb - zz : (hi ? zz - ub : 0.0);
+                    if (i >= nx && (lo || hi)) wf[e] = lo ? -1 : 1;   /* inputs join at once */
+                    if (i < nx && v > cv[i]) { cv[i] = v; ck[i] = k; }
+                }
+            if (nbad == 0) {
+                for (int e = 0; e < ne; e++) z[e] = z0[e];
+                goto accept;
+            }
+            for (int i = 0; i < nx; i++)
+                if (ck[i] >= 0) {
+                    const int e = ck[i] * nz + i;
+                    wf[e] = z0[e] < LBk(d, ck[i], i) ? -1 : 1;
+                }
+            continue;
+        }
+        if (m > WSMAX) return -2;
         double L[WSMAX][WSMAX], nu_[WSMAX], lt[WSMAX], wd[WSMAX];
         for (int i = 0; i < m; i++) {
             const int k = S[i] / nz, c = S[i] % nz;
@@ -1054,7 +1062,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
                 if (i == j) wd[i] = s;
                 for (int l = 0; l < j; l++) s -= L[i][l] * L[j][l];
                 if (i == j) {
-                    if (!(s > 0.0)) return 0;
+                    if (!(s > 0.0)) return -3;
                     L[i][i] = sqrt(s);
                 } else {
                     L[i][j] = s / L[j][j];
@@ -1070,6 +1078,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
             for (int l = i + 1; l < m; l++) s -= L[l][i] * nu_[l];
             nu_[i] = s / L[i][i];
         }
+        const int round = ws++;   /* this step's round (addok: the first round or no removals) */
         (*wsteps)++;
         *flops += m * m * m / 3.0 + 2.0 * m * m + 2.0 * ne * m;
         /* multiplier signs (lower: nu >= 0, upper: nu <= 0), measured as the displacement nu_i W_ii
@@ -1082,7 +1091,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
             rem[i] = (wf[S[i]] < 0 && dsp < -tol) || (wf[S[i]] > 0 && dsp > tol) || !isfinite(nu_[i]);
             nrem += rem[i];
         }
-        const int addok = ws == 0 || nrem == 0;
+        const int addok = round == 0 || nrem == 0;
         int wbad = nrem;
         double cv[NZMAX];
         int ck[NZMAX];
@@ -1106,7 +1115,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
                     const int lo = has(lb) && zz < lb - 1e-13 * (1.0 + fabs(lb)), hi = has(ub) && zz > ub + 1e-13 * (1.0 + fabs(ub));
                     wbad += lo || hi || !isfinite(zz);
                     const double v = lo ? lb - zz : (hi ? zz - ub : 0.0);
-                    if (c >= nx && addok && (lo || hi)) nf_[e] = lo ? -1 : 1;
+                    if (c >= nx && (lo || hi)) nf_[e] = lo ? -1 : 1;   /* inputs join at once */
                     if (c < nx && v > cv[c]) { cv[c] = v; ck[c] = k; }
                 }
                 z[e] = zz;
@@ -1120,7 +1129,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
                 }
         if (wbad == 0) goto accept;
     }
-    return 0;
+    return -4;
 accept:
     for (int k = 0; k <= N; k++)
         for (int i = 0; i < nz; i++) {
@@ -1395,7 +1404,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                     if (d->polish_mu > 0.0) {
                         int wst = 0, nw = 0;
                         for (int e = 0; e < ne; e++) nw += wf[e] != 0;
-                        ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6]);
+                        ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6]) > 0;
                         cnt[3] += wst;
                         if (ok) {
                             path = (nw == 0 && wst == 0) ? 0 : 1;
