@@ -216,6 +216,16 @@ struct nmpc_solver {
     size_t off_lqr = 0, off_lqrf = 0, off_lqrw = 0;   // unconstrained Riccati records (lqr_table, lqr_wmat)
     std::vector<double> lqr_host;                      // the lqr_table records (host copy)
     void *d_cltx = nullptr, *d_clv = nullptr;          // closed loop: explicit unconstrained solution (cl_explicit)
+    // lean closed loop (nmpc_cl_fast.hip): slot tables, per-instance step / flags, park list
+    bool clf = false;
+    int clf_nslot = 0, clf_epl = 0, clf_x1slot = 0, clf_sid = 0;
+    void *d_fsT = nullptr;                 // typed: s_lb, s_ub, s_tx, vb, uinit
+    size_t fso[5] = {0, 0, 0, 0, 0};
+    int *d_fsI = nullptr;                  // s_e, s_src, eslot
+    size_t fsi[3] = {0, 0, 0};
+    int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count + list [1 + B]
+    signed char *d_flags = nullptr;        // [B][nslot]
+    size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
     bool cl_ready = false;
@@ -479,7 +489,8 @@ void free_all(nmpc_solver *h)
     for (void *p : {h->d_model, h->d_x0, h->d_yref, h->d_x, h->d_u, h->d_scratch, (void *)h->d_status,
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
                     (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
-                    (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv})
+                    (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
+                    (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -552,13 +563,28 @@ nmpc::ClParams<T> cl_params(nmpc_solver *h);
 
 constexpr int CL_FUSED_CHUNK = 64;   // closed-loop steps per fused solve launch
 
+// list mode of the lane-per-component kernel (the lean closed loop's fallback)
+struct ListArgs {
+    int count, step0, noise_ld;
+};
+
 // cl_steps > 0: fused closed loop of that many steps (lane-per-component / wavefront kernels)
 template <typename T>
-int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0)
+int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0, const ListArgs *la = nullptr)
 {
     if (h->cond) return launch_cond<T>(h, e0, e1);
     nmpc::IpmParams<T> p{};
     p.cl_steps = cl_steps;
+    if (la) {
+        p.cl_list = h->d_park + 1;
+        p.cl_count = la->count;
+        p.cl_istep = h->d_istep;
+        p.cl_noise_ld = la->noise_ld;
+        p.cl_noise_step0 = la->step0;
+        p.cl_flags = h->d_flags;
+        p.cl_eslot = h->d_fsI + h->fsi[2];
+        p.cl_nslot = h->clf_nslot;
+    }
     if (cl_steps > 0) {
         p.cl = cl_params<T>(h);
         p.cl_noise = h->d_fnoise;
@@ -566,7 +592,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
         if (iter_log && !h->d_iter_log &&
             hipMalloc((void **)&h->d_iter_log, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(int)) != hipSuccess)
             h->d_iter_log = nullptr;
-        p.iter_log = iter_log ? h->d_iter_log : nullptr;
+        p.iter_log = iter_log && !la ? h->d_iter_log : nullptr;
         const bool no_expl = std::getenv("NMPC_EXPLICIT") && std::getenv("NMPC_EXPLICIT")[0] == '0';
         p.cl_tx = no_expl ? nullptr : (const T *)h->d_cltx;
         p.cl_v = no_expl ? nullptr : (const T *)h->d_clv;
@@ -1461,6 +1487,220 @@ hipError_t put_typed(void *dst, const double *src, size_t n, bool f64)
     return hipMemcpy(dst, t.data(), n * sizeof(float), hipMemcpyHostToDevice);
 }
 
+// The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, the
+// lane-per-component family (its list mode is the fallback), a compiled slot layout for (nx, nu);
+// on by default for quad13 and jerk, NMPC_CL_FAST=1 for any compiled shape (force: its input
+// saturation sets exceed the fast path's 8 bounds, the fused kernel stays faster), =0 off.
+// Slots: the bounded elements of z in stage-major order (stage 0's inputs first), their bounds,
+// T_x rows, v_t columns and warm-start sources (the element one stage later; stage N - 1's inputs
+// keep their own flag, as the fused kernel's mirror of stage N).
+int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<double> &tx, const std::vector<double> &vv)
+{
+    const int nx = h->nx, nu = h->nu, nz = nx + nu, N = h->N, ne = (N + 1) * nz, P_ = d.ref_period;
+    const char *env = std::getenv("NMPC_CL_FAST");
+    const bool want = env ? env[0] != '0' : ((nx == 13 && nu == 4) || (nx == 6 && nu == 2));
+    const int kind = nmpc::ipm_kind<double>(h->kidx);
+    const int epl = nmpc::cl_fast_epl(nx, nu);
+    if (!want || h->precision != NMPC_FP64 || !(h->polish_mu > 0) || !h->g_diag || h->cond || kind != 1 || epl <= 0)
+        return 0;
+    std::vector<int> el;
+    std::vector<double> lb, ub;
+    for (int k = 0; k <= N; k++)
+        for (int r = 0; r < nz; r++) {
+            if ((k == 0 && r < nx) || (k == N && r >= nx)) continue;
+            const int ty = k == 0 ? 0 : (k == N ? 2 : 1);
+            const double l = h->lbnd[ty * nz + r], u_ = h->ubnd[ty * nz + r];
+            if (!has_bound(l) && !has_bound(u_)) continue;
+            el.push_back(k * nz + r);
+            lb.push_back(l);
+            ub.push_back(u_);
+        }
+    const int nslot = (int)el.size(), NS = epl * 64;
+    if (nslot > NS) return 0;
+    // stage 0's inputs are slots 0..nu-1 (u0 broadcast), every input box two-sided (failure output)
+    std::vector<double> uinit(nu);
+    for (int i = 0; i < nu; i++) {
+        if (nslot <= i || el[i] != nx + i) return 0;
+        const double l = h->lbnd[nx + i], u_ = h->ubnd[nx + i];
+        if (!has_bound(l) || !has_bound(u_)) return 0;
+        uinit[i] = 0.5 * (l + u_);
+    }
+    std::vector<int> eslot(ne, -1);
+    for (int s = 0; s < nslot; s++) eslot[el[s]] = s;
+    int x1slot = 0;
+    if (d.cost_stage != 0) {   // x_1's cost components on consecutive slots of j = 0
+        if (d.cost_stage != 1) return 0;
+        x1slot = eslot[nz];
+        for (int i = 0; i < d.ncl; i++)
+            if (x1slot < 0 || eslot[nz + i] != x1slot + i || x1slot + i >= 64) return 0;
+    }
+    std::vector<int> src(nslot, -1);
+    for (int s = 0; s < nslot; s++) {
+        const int k = el[s] / nz, r = el[s] % nz;
+        int ks = k < N ? k + 1 : k;
+        if (k == N - 1 && r >= nx) ks = k;   // inputs of stage N mirror N - 1
+        src[s] = eslot[ks * nz + r];
+    }
+    std::vector<double> stx((size_t)nslot * nx), vb((size_t)P_ * NS, 0.0);
+    for (int s = 0; s < nslot; s++)
+        for (int c = 0; c < nx; c++) stx[(size_t)s * nx + c] = tx[(size_t)el[s] * nx + c];
+    for (int t = 0; t < P_; t++)
+        for (int s = 0; s < nslot; s++) vb[(size_t)t * NS + s] = vv[(size_t)t * ne + el[s]];
+    // device blobs
+    const std::vector<double> *parts[5] = {&lb, &ub, &stx, &vb, &uinit};
+    size_t tot = 0;
+    for (int i = 0; i < 5; i++) {
+        h->fso[i] = tot;
+        tot += (parts[i]->size() + 31) & ~(size_t)31;
+    }
+    const std::vector<int> *ip[3] = {&el, &src, &eslot};
+    size_t itot = 0;
+    for (int i = 0; i < 3; i++) {
+        h->fsi[i] = itot;
+        itot += (ip[i]->size() + 63) & ~(size_t)63;
+    }
+    for (void **q : {&h->d_fsT, (void **)&h->d_fsI, (void **)&h->d_istep, (void **)&h->d_park, (void **)&h->d_flags})
+        if (*q) {
+            hipFree(*q);
+            *q = nullptr;
+        }
+    bool ok = hipMalloc(&h->d_fsT, tot * sizeof(double)) == hipSuccess &&
+              hipMalloc((void **)&h->d_fsI, itot * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_istep, (size_t)h->batch * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_park, (size_t)(h->batch + 1) * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_flags, (size_t)h->batch * nslot) == hipSuccess;
+    if (!ok) return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: lean closed-loop tables");
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 5 && e == hipSuccess; i++)
+        e = hipMemcpy((double *)h->d_fsT + h->fso[i], parts[i]->data(), parts[i]->size() * sizeof(double), hipMemcpyHostToDevice);
+    for (int i = 0; i < 3 && e == hipSuccess; i++)
+        e = hipMemcpy(h->d_fsI + h->fsi[i], ip[i]->data(), ip[i]->size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(h->d_istep, 0, (size_t)h->batch * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * nslot);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init lean tables");
+    h->clf = true;
+    h->clf_nslot = nslot;
+    h->clf_epl = epl;
+    h->clf_x1slot = x1slot;
+    h->clf_sid = nmpc::ipm_structure<double>(h->kidx);
+    return 0;
+}
+
+nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int noise_ld)
+{
+    nmpc::ClFastParams<double> p{};
+    const nmpc_closed_loop_desc &d = h->cl;
+    const int nx = h->nx, nu = h->nu, nz = nx + nu;
+    p.B = h->batch;
+    p.N = h->N;
+    p.ne = (h->N + 1) * nz;
+    p.nslot = h->clf_nslot;
+    p.period = d.ref_period;
+    p.table_cols = d.ref_cols;
+    p.cost_stage = d.cost_stage;
+    p.ncl = d.ncl;
+    p.aed_dims = d.aed_dims;
+    p.noise_dims = d.noise_dims;
+    p.plant = d.plant;
+    p.substeps = d.substeps;
+    p.ny = h->ny;
+    p.ny_e = h->ny_e;
+    p.mass = d.mass;
+    p.g = d.g;
+    p.dt = d.dt;
+    p.dt_conv = d.dt_conv;
+    p.target = target;
+    p.step0 = step0;
+    p.noise_ld = noise_ld;
+    p.polish_steps = h->polish_steps;
+    p.x1_slot = h->clf_x1slot;
+    p.table = (const double *)h->d_table;
+    p.offset = h->d_offsets;
+    p.state = (double *)h->d_state;
+    p.acc = h->d_acc;
+    p.istep = h->d_istep;
+    p.flags = h->d_flags;
+    p.noise = h->d_fnoise;
+    const double *fT = (const double *)h->d_fsT;
+    p.s_lb = fT + h->fso[0];
+    p.s_ub = fT + h->fso[1];
+    p.s_tx = fT + h->fso[2];
+    p.vb = fT + h->fso[3];
+    p.uinit = fT + h->fso[4];
+    p.s_e = h->d_fsI + h->fsi[0];
+    p.s_src = h->d_fsI + h->fsi[1];
+    p.vfull = (const double *)h->d_clv;
+    p.txfull = (const double *)h->d_cltx;
+    const char *m = (const char *)h->d_model;
+    p.W = (const double *)(m + h->off_lqrw);
+    p.lbnd = (const double *)(m + h->off_lb);
+    p.ubnd = (const double *)(m + h->off_ub);
+    p.AB = (const double *)(m + h->off_AB);
+    p.c = (const double *)(m + h->off_c);
+    p.wcl = (const double *)h->d_wcl;
+    p.xout = (double *)h->d_x;
+    p.uout = (double *)h->d_u;
+    p.status = h->d_status;
+    p.iters = h->d_iters;
+    p.park_count = h->d_park;
+    p.park_list = h->d_park + 1;
+    return p;
+}
+
+hipEvent_t cl_event(nmpc_solver *h, size_t i)
+{
+    while (h->cl_events.size() <= i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        h->cl_events.push_back(e);
+    }
+    return h->cl_events[i];
+}
+
+// `steps` closed-loop steps on the lean loop: noise draws of the run, then rounds of (fast kernel
+// over every instance up to the target step; the count of parked instances back to the host; one
+// full solve + plant step per parked instance, ipm_lpc_kernel in list mode) until none is parked.
+// Returns the number of kernel launches (each bracketed by an event pair), or < 0.
+int clf_run(nmpc_solver *h, int steps)
+{
+    const int target = h->cl_step + steps;
+    const size_t need = (size_t)h->batch * steps;
+    if (h->fnoise_cap < need) {
+        if (h->d_fnoise) hipFree(h->d_fnoise);
+        h->d_fnoise = nullptr;
+        if (hipMalloc((void **)&h->d_fnoise, need * sizeof(double)) != hipSuccess)
+            return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: noise buffer");
+        h->fnoise_cap = need;
+    }
+    nmpc::ClParams<double> cp = cl_params<double>(h);
+    hipError_t e = nmpc::cl_noise_launch<double>(cp, h->cl_step, steps, h->d_fnoise, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
+    const nmpc::ClFastParams<double> fp = clf_params(h, target, h->cl_step, steps);
+    int launches = 0;
+    // one wavefront per instance at a time: at most 8 per SIMD resident, the rest stride
+    const int waves = std::min(h->batch, 8192);
+    for (int round = 0; round <= steps; round++) {
+        if ((e = hipMemsetAsync(h->d_park, 0, sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
+        hipEventRecord(cl_event(h, 2 * launches), h->stream);
+        e = nmpc::cl_fast_launch<double>(h->nx, h->nu, h->clf_sid, fp, waves, h->stream);
+        hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
+        launches++;
+        if (e != hipSuccess) return hip_fail(h, e, "lean closed-loop kernel launch");
+        int parked = 0;
+        e = hipMemcpyAsync(&parked, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return hip_fail(h, e, "lean closed loop");
+        if (parked <= 0) break;
+        // the fallback: one full solve + plant step for every parked instance
+        const ListArgs la{parked, h->cl_step, steps};
+        const int r = launch<double>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
+        launches++;
+        if (r < 0) return r;
+    }
+    h->cl_step = target;
+    return launches;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1523,6 +1763,7 @@ int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d)
     if (h->d_cltx) hipFree(h->d_cltx);
     if (h->d_clv) hipFree(h->d_clv);
     h->d_cltx = h->d_clv = nullptr;
+    h->clf = false;
     if (!h->cond && !h->lqr_host.empty()) {
         const int N = h->N, nz = nx + nu, ne = (N + 1) * nz, ny = h->ny, nye = h->ny_e, P_ = d->ref_period;
         std::vector<double> tx((size_t)ne * nx), vv((size_t)P_ * ne), g((size_t)ne, 0.0), z((size_t)ne), e0(nx);
@@ -1553,6 +1794,8 @@ int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d)
         e = put_typed(h->d_cltx, tx.data(), tx.size(), f64);
         if (e == hipSuccess) e = put_typed(h->d_clv, vv.data(), vv.size(), f64);
         if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init explicit tables");
+        const int r = clf_setup(h, *d, tx, vv);
+        if (r < 0) return r;
     }
     h->cl = *d;
     h->cl.ref_table = nullptr;
@@ -1578,9 +1821,18 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
     }
     h->out_valid = false;
     int launches = 0;
-    if (cl_fused(h)) {
-        if (!h->d_fnoise && hipMalloc((void **)&h->d_fnoise, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(double)) != hipSuccess)
-            return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: noise buffer");
+    const char *fused_env = std::getenv("NMPC_CL_FUSED");
+    if (h->clf && steps > 0 && !(fused_env && fused_env[0] == '0')) {
+        launches = clf_run(h, steps);
+        if (launches < 0) return launches;
+    } else if (cl_fused(h)) {
+        if (h->fnoise_cap < (size_t)h->batch * CL_FUSED_CHUNK) {
+            if (h->d_fnoise) hipFree(h->d_fnoise);
+            h->d_fnoise = nullptr;
+            if (hipMalloc((void **)&h->d_fnoise, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(double)) != hipSuccess)
+                return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: noise buffer");
+            h->fnoise_cap = (size_t)h->batch * CL_FUSED_CHUNK;
+        }
         for (int s = 0; s < steps; s += CL_FUSED_CHUNK, launches++) {
             const int n = std::min(CL_FUSED_CHUNK, steps - s);
             const int r = h->precision == NMPC_FP64 ? cl_fused_enqueue<double>(h, launches, n)

@@ -84,7 +84,56 @@ struct IpmParams {
     // fused closed loop, explicit unconstrained solution (nmpc_closed_loop_init): z_0 = T_x x_0 + v_t
     const T *cl_tx;           // [(N+1) nz][nx]
     const T *cl_v;            // [period][(N+1) nz]
+    // list mode (lane-per-component kernel, cl_steps = 1): the fallback of the lean closed loop —
+    // one cold full solve + plant step for each listed instance at its own step cl_istep[inst];
+    // noise cl_noise[inst * cl_noise_ld + step - cl_noise_step0]; the solution's active flags to
+    // cl_flags[inst][cl_eslot[k nz + r]] (bounded elements)
+    const int *cl_list;
+    int cl_count;
+    int *cl_istep;
+    int cl_noise_ld, cl_noise_step0;
+    signed char *cl_flags;
+    const int *cl_eslot;
+    int cl_nslot;
 };
+
+// Lean fused closed loop (nmpc_cl_fast.hip): the exact finish's fast path, one wavefront per
+// instance at a time, the bounded elements of z in per-lane "slots" (s = j * 64 + lane)
+template <typename T>
+struct ClFastParams {
+    int B, N, ne, nslot;          // ne = (N + 1)(nx + nu); nslot = bounded elements (slot count)
+    int period, table_cols, cost_stage, ncl, aed_dims, noise_dims, plant, substeps, ny, ny_e;
+    double mass, g, dt, dt_conv;
+    int target;                   // run every instance up to this closed-loop step
+    int step0, noise_ld;          // noise[b][step - step0], row length noise_ld
+    int polish_steps;             // active-set rounds of the fast path
+    int x1_slot;                  // slot (lane, j = 0) of x_1[0] (cost of the jerk loop: cost_stage 1)
+    const T *table;               // reference table [rows][table_cols]
+    const int *offset;            // [B]
+    T *state;                     // [B][nx]
+    double *acc;                  // [B][4] cost, AED numerator, failures, steps
+    int *istep;                   // [B] closed-loop step each instance has reached
+    signed char *flags;           // [B][nslot] the last solution's active flags (-1 lower, 1 upper)
+    const double *noise;          // [B][noise_ld]
+    const int *s_e, *s_src;       // [nslot] element index k nz + r; warm-start source slot (or -1)
+    const T *s_lb, *s_ub;         // [nslot]
+    const T *s_tx;                // [nslot][nx] rows of T_x
+    const T *vb;                  // [period][EPL * 64] v_t at the slots
+    const T *vfull;               // [period][ne]
+    const T *txfull;              // [ne][nx]
+    const T *W;                   // [ne][ne] projected inverse Hessian (lqr_wmat)
+    const T *lbnd, *ubnd;         // [3][nz]
+    const T *AB, *c;              // [nx][nz], [nx]: the controller model (plant 0, certificate)
+    const T *wcl;                 // [ncl]
+    const T *uinit;               // [nu] inputs of the solver's initial point (failure output)
+    T *xout, *uout;               // trajectories of the last solve (written at the last step)
+    int *status, *iters;
+    int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
+};
+// compiled fast kernels: EPL slots per lane (0 if none for this shape)
+int cl_fast_epl(int nx, int nu);
+template <typename T>
+hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, hipStream_t s);
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);
 

@@ -287,8 +287,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     const unsigned wave_u = __builtin_amdgcn_readfirstlane(wave);
     const size_t wg = (size_t)blockIdx.x * WPB + wave_u;
     const long long inst_raw = (long long)wg * IPW + grp;
-    const bool inst_ok = grp < IPW && inst_raw < p.B;
-    const int inst = inst_ok ? (int)inst_raw : 0;   // idle lanes read instance 0, never write outputs
+    // list mode (the lean closed loop's fallback): lane group g solves instance cl_list[g]
+    const bool lmode = p.cl_list != nullptr;
+    const bool inst_ok = grp < IPW && inst_raw < (lmode ? (long long)p.cl_count : (long long)p.B);
+    const int inst = inst_ok ? (lmode ? p.cl_list[inst_raw] : (int)inst_raw) : 0;   // idle lanes read instance 0, never write outputs
 
     // ---- model constants -> LDS (once per workgroup)
     for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) {
@@ -394,7 +396,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         m = (m & ~(3ull << (2 * k))) | (f < T(0) ? (1ull << (2 * k)) : (f > T(0) ? (2ull << (2 * k)) : 0ull));
     };
     unsigned long long actm = 0;
-    if (amask && p.cl.step > 0)
+    // the closed-loop step of this launch's first step: the handle's, or (list mode) the instance's own
+    const int cl_base = fused ? (lmode ? (inst_ok ? p.cl_istep[inst] : 0) : p.cl.step) : 0;
+    if (amask && p.cl.step > 0 && !lmode)
         for (int k = 0; k <= N; k++) mset(actm, k, ldE(L::ACT, k));
     // fused closed loop with the controller-model plant (quad13), fp64, cost at x_0: the state stays in
     // the group's LDS for the whole launch (G_CL: state, this step's output z_0, yref row 0, sums),
@@ -429,7 +433,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
 #endif
         // fused closed loop: the yref window straight from the reference table rows (offset + step) %
         // period (cl_prepare_kernel's gather), x0 from the closed-loop state
-        const int t_ref = fused ? (p.cl.offset[inst] + p.cl.step + cstep) % p.cl.period : 0;
+        const int t_ref = fused ? (p.cl.offset[inst] + cl_base + cstep) % p.cl.period : 0;
         const T *yref = fused ? p.cl.table + (size_t)t_ref * p.cl.table_cols
                               : p.yref + (size_t)inst * ((size_t)N * p.ny + p.ny_e);
         const int yrow = fused ? p.cl.table_cols : p.ny;
@@ -470,7 +474,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     // fused closed loop after its first step: the first finish run of a solve starts from the
     // previous step's active set shifted by one stage (ACT word; warm start, the acceptance tests
     // are unchanged), read into the dza slots, which the first iteration does not use otherwise
-    const bool warm = fused && (cstep > 0 || p.cl.step > 0);
+    // (list mode: a cold solve — the lean loop parks an instance its fast path could not finish)
+    const bool warm = fused && !lmode && (cstep > 0 || p.cl.step > 0);
     bool fwarm = false;   // wave-uniform: the current finish pass reads the warm flags
     // the warm-start set: the previous solution's flags (ACT), shifted by one stage, copied into the
     // DZA words the first finish step reads its flags from (so ACT is free for this solve's outputs),
@@ -2278,7 +2283,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     if (NZ % 2) s0 = fma(abr[(xl ? r : 0) * LDZ + NZ - 1], zx[NZ - 1], s0);
                     sx = s0 + s1;
                 }
-                const double w_ = p.cl_noise[(size_t)inst * nsteps + cstep];
+                const double w_ = lmode ? p.cl_noise[(size_t)inst * p.cl_noise_ld + (cl_base + cstep - p.cl_noise_step0)]
+                                        : p.cl_noise[(size_t)inst * nsteps + cstep];
                 if (xl) clx[r] = (T)((double)sx + (r < p.cl.noise_dims ? w_ : 0.0));
                 if (r == 0) {
                     cls[0] += (T)ce;
@@ -2287,8 +2293,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
                     cls[3] += T(1);
                 }
             } else if (inst_ok) {
-                cl_advance_group<T, NX, NU>(p.cl, inst, p.cl.step + cstep, status < 0 ? 0 : status, r,
-                                            p.cl_noise[(size_t)inst * nsteps + cstep]);
+                cl_advance_group<T, NX, NU>(p.cl, inst, cl_base + cstep, status < 0 ? 0 : status, r,
+                                            lmode ? p.cl_noise[(size_t)inst * p.cl_noise_ld + (cl_base + cstep - p.cl_noise_step0)]
+                                                  : p.cl_noise[(size_t)inst * nsteps + cstep]);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
@@ -2296,8 +2303,22 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         }
         LPC_STICK(7);
     }
-    if (amask)   // the warm start of the next launch
+    if (lmode) {
+        // the lean loop's state of the instance: its solution's active flags by slot, the next step
+        if (inst_ok) {
+            for (int k = 0; k <= N; k++) {
+                if ((k == N && ul) || (k == 0 && xl)) continue;
+                const int sl = p.cl_eslot[k * NZ + r];
+                if (sl >= 0) {
+                    const T f = amask ? mflag(actm, k) : ldE(L::ACT, k);
+                    p.cl_flags[(size_t)inst * p.cl_nslot + sl] = f < T(0) ? -1 : (f > T(0) ? 1 : 0);
+                }
+            }
+            if (r == 0) p.cl_istep[inst] = cl_base + nsteps;
+        }
+    } else if (amask) {   // the warm start of the next launch
         for (int k = 0; k <= N; k++) stE(L::ACT, k, mflag(actm, k));
+    }
     if (fastpl && inst_ok) {   // the launch's final state and its closed-loop sums
         if (xl) p.cl.state[(size_t)inst * NX + r] = clx[r];
         if (r < 4) p.cl.acc[(size_t)inst * 4 + r] += (double)cls[r];
@@ -2322,8 +2343,9 @@ template <typename T, int NX, int NU, int WPB, int MW, class SP>
 hipError_t launch_ipm_lpc(const IpmParams<T> &p, hipStream_t s)
 {
     using Gm = lpc::Geom<T, NX, NU, WPB>;
-    const int waves = (p.B + Gm::IPW - 1) / Gm::IPW;
+    const int waves = ((p.cl_list ? p.cl_count : p.B) + Gm::IPW - 1) / Gm::IPW;
     const int blocks = (waves + WPB - 1) / WPB;
+    if (blocks < 1) return hipSuccess;
     hipLaunchKernelGGL((lpc::ipm_lpc_kernel<T, NX, NU, WPB, MW, SP>), dim3(blocks), dim3(64 * WPB), 0, s, p);
     return hipGetLastError();
 }

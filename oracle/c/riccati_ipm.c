@@ -1396,7 +1396,8 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                 for (int k = 0; k < N; k++) memcpy(yref + (size_t)k * ny, c->table + (size_t)(t + k) * c->cols, sizeof(double) * ny);
                 memcpy(yref + (size_t)N * ny, c->table + (size_t)(t + N) * c->cols, sizeof(double) * nye);
                 int status = 0, path = 2, iters = 0, ok = 0;
-                const int warm = mode == 1 && step > 0 && ab != NULL;
+                /* mode 1 tries the fast path from the first step on (an empty warm set at step 0) */
+                const int warm = mode == 1 && ab != NULL;
                 if (warm) {   /* the previous solution's flags shifted by one stage */
                     for (int k = 0; k <= N; k++)
                         for (int i = 0; i < nz; i++)

@@ -197,7 +197,8 @@ def test_fused_closed_loop_matches_per_step(model, N, B, kernel):
 
     xs, ins, sts = run(False)
     xf, inf, stf = run(True)
-    assert sts["solve_launches"] == 70 and stf["solve_launches"] == 2 and stf["steps"] == 70
+    # fused: two launches of the solve kernel (64 + 6 steps), or the lean loop's rounds (quad13, jerk)
+    assert sts["solve_launches"] == 70 and 1 <= stf["solve_launches"] <= 70 and stf["steps"] == 70
     assert np.array_equal(ins[:, 2:], inf[:, 2:])            # failures, steps per instance
     # certified solutions reached by different paths (warm-started active sets, no finish after a
     # failed step in the fused loop) agree to rounding, far inside the 1e-6 solve bar
@@ -214,7 +215,9 @@ def test_shared_factorisation_paths_match_full_factorisation(model, N, B):
     every finish step (NMPC_LQR=0) all give the oracle's closed loop (oracle/c/riccati_ipm.c mode 0:
     cold exact solves, active sets confirmed by a dense KKT solve): states to 1e-6 relative (the solve
     bar), per-instance cost / AED sums to 1e-6 relative, failure counts exactly, over 40 steps of the
-    lane-per-component fused closed loop (two launches: 25 + 15). (The paths agree with each other to
+    lane-per-component fused closed loop (two launches: 25 + 15), and the same for the lean closed loop
+    (nmpc_cl_fast.hip: the fast path as its own kernel, parked instances solved in list mode). (The
+    paths agree with each other to
     ~1e-8, not to rounding: the penalised finish of a full factorisation decides a held bound's
     multiplier sign on z - b, which resolves small multipliers of low-curvature inputs less finely than
     the active-set steps' displacement test.)"""
@@ -238,7 +241,11 @@ def test_shared_factorisation_paths_match_full_factorisation(model, N, B):
     ref = cref.ClosedLoopRef(getattr(models, f"{model}_model")(N), model, table, off, x, mode=0, seed=11,
                              tol_comp=o.qp_solver_tol_comp, tol_res=o.qp_solver_tol_stat)
     ref.run(40)
-    for env in ({"NMPC_LQR": "0"}, {}, {"NMPC_FAST": "0"}, {"NMPC_FAST": "2"}, {"NMPC_EXPLICIT": "0"}, {"NMPC_WSET": "0"}):
+    # the fused lane-per-component kernel's switches (NMPC_CL_FAST=0: not the lean loop) and the lean
+    # loop itself (nmpc_cl_fast.hip, default for quad13 / jerk; forced for force)
+    for env in ({"NMPC_LQR": "0", "NMPC_CL_FAST": "0"}, {"NMPC_CL_FAST": "0"}, {"NMPC_FAST": "0", "NMPC_CL_FAST": "0"},
+                {"NMPC_FAST": "2", "NMPC_CL_FAST": "0"}, {"NMPC_EXPLICIT": "0", "NMPC_CL_FAST": "0"},
+                {"NMPC_WSET": "0", "NMPC_CL_FAST": "0"}, {"NMPC_CL_FAST": "1"}):
         x1, s1 = run(env)
         assert np.array_equal(s1[:, 2:], ref.acc[:, 2:]), env
         err = np.abs(x1 - ref.state).max(1) / np.maximum(1.0, np.abs(ref.state).max(1))

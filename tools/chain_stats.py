@@ -15,6 +15,7 @@ import sys
 import numpy as np
 
 os.environ.setdefault("NMPC_ITER_LOG", "1")
+os.environ.setdefault("NMPC_CL_FAST", "0")   # the iteration log is the fused lane-per-component kernel's
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
