@@ -1689,13 +1689,16 @@ int clf_run(nmpc_solver *h, int steps)
         int parked = 0;
         e = hipMemcpyAsync(&parked, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-        if (e != hipSuccess) return hip_fail(h, e, "lean closed loop");
+        if (e != hipSuccess) return hip_fail(h, e, "lean closed loop (fast kernel)");
+        static const bool dbg = std::getenv("NMPC_CLF_DEBUG") != nullptr;
+        if (dbg) std::fprintf(stderr, "[nmpc clf] steps %d..%d round %d: %d parked\n", h->cl_step, target, round, parked);
         if (parked <= 0) break;
         // the fallback: one full solve + plant step for every parked instance
         const ListArgs la{parked, h->cl_step, steps};
         const int r = launch<double>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
         launches++;
         if (r < 0) return r;
+        if (dbg && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "lean closed loop (list-mode fallback)");
     }
     h->cl_step = target;
     return launches;

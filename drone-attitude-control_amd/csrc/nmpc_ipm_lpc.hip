@@ -397,7 +397,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     };
     unsigned long long actm = 0;
     // the closed-loop step of this launch's first step: the handle's, or (list mode) the instance's own
-    const int cl_base = fused ? (lmode ? (inst_ok ? p.cl_istep[inst] : 0) : p.cl.step) : 0;
+    // (idle lanes of list mode sit at the noise table's first column: every address they form stays valid)
+    const int cl_base = fused ? (lmode ? (inst_ok ? p.cl_istep[inst] : p.cl_noise_step0) : p.cl.step) : 0;
     if (amask && p.cl.step > 0 && !lmode)
         for (int k = 0; k <= N; k++) mset(actm, k, ldE(L::ACT, k));
     // fused closed loop with the controller-model plant (quad13), fp64, cost at x_0: the state stays in
