@@ -60,13 +60,41 @@ __device__ __forceinline__ unsigned long long ballot(bool b) { return __ballot(b
 // the certificate's stage exchange
 template <int NSLOT, int NZ>
 struct Lds {
-    signed char fl[NSLOT];
+    double zb[NSLOT];          // z_0 into / z out of the active-set steps
+    signed char fl[NSLOT];     // flags: the warm-start shift buffer; the active-set steps' set
     double se_t[WSMAX], se_nu[WSMAX], wdg[WSMAX], wss[WSMAX][WSMAX];
     int se_e[WSMAX], se_s[WSMAX];
     unsigned long long vmax[NZ];
     int vslot[NZ];
-    double cm[32], cr[32];
+    double cm[32], cr[32], xs[32];   // certificate exchange; x_0 for the certificate and the outputs
 };
+
+// the workgroup's slot constants (LDS), seen from one lane: slot j of this lane is j * 64 + lane
+template <int EPL>
+struct SlotView {
+    const double *lb_, *ub_;
+    const int *e_, *src_;
+    int lane;
+    __device__ double lb(int j) const { return lb_[j * 64 + lane]; }
+    __device__ double ub(int j) const { return ub_[j * 64 + lane]; }
+    __device__ int e(int j) const { return e_[j * 64 + lane]; }
+    __device__ int src(int j) const { return src_[j * 64 + lane]; }
+};
+
+// 2-bit flags of a per-lane mask (bit 2j lower, 2j+1 upper) <-> -1 / 0 / 1
+__device__ __forceinline__ signed char flag_of(unsigned m, int j)
+{
+    const unsigned b = (m >> (2 * j)) & 3u;
+    return b == 1u ? (signed char)-1 : (b == 2u ? (signed char)1 : (signed char)0);
+}
+__device__ __forceinline__ unsigned bits_of(signed char f) { return f < 0 ? 1u : (f > 0 ? 2u : 0u); }
+
+// a bound violated beyond the fast path's 1e-13 (relative to 1 + |b|)
+template <typename T>
+__device__ __forceinline__ bool violated(T z, T l, T u)
+{
+    return (has_b(l) && z < l - T(1e-13) * (T(1) + fabs(l))) || (has_b(u) && z > u + T(1e-13) * (T(1) + fabs(u)));
+}
 
 #define CLF_SYNC()                                               \
     do {                                                         \
@@ -78,11 +106,11 @@ struct Lds {
 // the solver's initial point at element (k, r) (the lane-per-component kernel's failure output):
 // x_0 pinned, states at the reference projected 1 % inside their box, inputs mid-box
 template <typename T>
-__device__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, int t, const T *x0r)
+__device__ __noinline__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, int t, T x0r)
 {
     const int ty = k == 0 ? 0 : (k == p.N ? 2 : 1);
     const T lb = p.lbnd[ty * nz + r], ub = p.ubnd[ty * nz + r];
-    if (k == 0 && r < nx) return *x0r;
+    if (k == 0 && r < nx) return x0r;
     const bool yv = k < p.N ? r < p.ny : r < p.ny_e;
     T v = yv ? p.table[(size_t)(t + k) * p.table_cols + r] : T(0);
     const bool hl = has_b(lb), hu = has_b(ub);
@@ -109,12 +137,28 @@ __device__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, 
 // set restarts from z_0 (one round). false: set larger than WSMAX, W_SS not positive definite, or no
 // acceptance in polish_steps rounds.
 template <typename T, int NX, int NU, int EPL, class LdsT>
-__device__ bool wsteps_run(const ClFastParams<T> &p, LdsT &L, int lane, const int (&se)[EPL], const int (&sr)[EPL],
-                           const T (&lb)[EPL], const T (&ub)[EPL], const T (&z0)[EPL], T (&z)[EPL], unsigned &wf,
-                           int &wsteps, int &m_acc)
+__device__ __noinline__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane)
 {
     constexpr int NZ = NX + NU;
     const int ne = p.ne;
+    int se[EPL], sr[EPL], wsteps = 0;
+    T lb[EPL], ub[EPL], z0[EPL], z[EPL];
+    unsigned wf = 0;
+#pragma unroll
+    for (int j = 0; j < EPL; j++) {
+        se[j] = sv.e(j);
+        sr[j] = se[j] >= 0 ? se[j] % NZ : -1;
+        lb[j] = (T)sv.lb(j);
+        ub[j] = (T)sv.ub(j);
+        z0[j] = (T)L.zb[j * 64 + lane];
+        wf |= bits_of(L.fl[j * 64 + lane]) << (2 * j);
+    }
+    auto done = [&](int m) {   // accepted: z to LDS; result word ok | m << 8 | steps << 16
+#pragma unroll
+        for (int j = 0; j < EPL; j++) L.zb[j * 64 + lane] = (double)z[j];
+        CLF_SYNC();
+        return 1 | (m << 8) | (wsteps << 16);
+    };
     // per state component: the most violated slot (argmax by LDS atomics, ties to the first stage)
     auto argmax_states = [&](const double (&v)[EPL]) {
         if (lane < NZ) {
@@ -158,8 +202,7 @@ __device__ bool wsteps_run(const ClFastParams<T> &p, LdsT &L, int lane, const in
             if (!__any(bad)) {
 #pragma unroll
                 for (int j = 0; j < EPL; j++) z[j] = z0[j];
-                m_acc = 0;
-                return true;
+                return done(0);
             }
             argmax_states(v);
 #pragma unroll
@@ -168,7 +211,7 @@ __device__ bool wsteps_run(const ClFastParams<T> &p, LdsT &L, int lane, const in
             CLF_SYNC();
             continue;
         }
-        if (m > WSMAX) return false;
+        if (m > WSMAX) return wsteps << 16;
         // the set in LDS: element, sign, b - z_0
         int base = 0;
 #pragma unroll
@@ -205,32 +248,35 @@ __device__ bool wsteps_run(const ClFastParams<T> &p, LdsT &L, int lane, const in
             if (j > c && j <= i && i < m) L.wss[i][j] -= L.wss[i][c] * L.wss[j][c];
             CLF_SYNC();
         }
-        if (!pd) return false;
-        double nu_[WSMAX];
-#pragma unroll
-        for (int i = 0; i < WSMAX; i++) {
-            double s_ = i < m ? L.se_t[i] : 0.0;
-#pragma unroll
-            for (int l = 0; l < i; l++) s_ = fma(-L.wss[i][l], nu_[l], s_);
-            nu_[i] = i < m ? s_ / L.wss[i][i] : 0.0;
+        if (!pd) return wsteps << 16;
+        // nu = L^-T L^-1 (b - z_0)_S into L.se_nu (lane 0 writes, every lane reads; m <= WSMAX rows)
+#pragma unroll 1
+        for (int i = 0; i < m; i++) {
+            double s_ = L.se_t[i];
+#pragma unroll 1
+            for (int l = 0; l < i; l++) s_ = fma(-L.wss[i][l], L.se_nu[l], s_);
+            CLF_SYNC();
+            if (lane == 0) L.se_nu[i] = s_ / L.wss[i][i];
+            CLF_SYNC();
         }
-#pragma unroll
-        for (int i = WSMAX - 1; i >= 0; i--) {
-            double s_ = nu_[i];
-#pragma unroll
-            for (int l = i + 1; l < WSMAX; l++)
-                if (l < m) s_ = fma(-L.wss[l][i], nu_[l], s_);
-            nu_[i] = i < m ? s_ / L.wss[i][i] : 0.0;
+#pragma unroll 1
+        for (int i = m - 1; i >= 0; i--) {
+            double s_ = L.se_nu[i];
+#pragma unroll 1
+            for (int l = i + 1; l < m; l++) s_ = fma(-L.wss[l][i], L.se_nu[l], s_);
+            CLF_SYNC();
+            if (lane == 0) L.se_nu[i] = s_ / L.wss[i][i];
+            CLF_SYNC();
         }
         const int round = ws++;
         wsteps++;
         // multiplier signs as displacements nu_i W_ii (lower: >= 0, upper: <= 0) to 1e-10 (1 + |b - z_0|)
         unsigned remm = 0;
-#pragma unroll
-        for (int i = 0; i < WSMAX; i++) {
-            const double tol = 1e-10 * (1.0 + fabs(L.se_t[i])), dsp = nu_[i] * L.wdg[i];
+#pragma unroll 1
+        for (int i = 0; i < m; i++) {
+            const double nui = L.se_nu[i], tol = 1e-10 * (1.0 + fabs(L.se_t[i])), dsp = nui * L.wdg[i];
             const int sg = L.se_s[i];
-            if (i < m && ((sg < 0 && dsp < -tol) || (sg > 0 && dsp > tol) || !isfinite(nu_[i]))) remm |= 1u << i;
+            if ((sg < 0 && dsp < -tol) || (sg > 0 && dsp > tol) || !isfinite(nui)) remm |= 1u << i;
         }
         const int nrem = __popc(remm);
         const bool addok = round == 0 || nrem == 0;
@@ -245,16 +291,15 @@ __device__ bool wsteps_run(const ClFastParams<T> &p, LdsT &L, int lane, const in
                 continue;
             }
             T zz = z0[j];
-#pragma unroll
-            for (int i = 0; i < WSMAX; i++)
-                if (i < m) zz = fma(p.W[(size_t)L.se_e[i] * ne + se[j]], (T)nu_[i], zz);
+#pragma unroll 1
+            for (int i = 0; i < m; i++) zz = fma(p.W[(size_t)L.se_e[i] * ne + se[j]], (T)L.se_nu[i], zz);
             const unsigned f = (wf >> (2 * j)) & 3u;
             if (f) {
                 const T bb = f == 1u ? lb[j] : ub[j];
                 bad |= !(fabs(zz - bb) <= T(1e-9) * (T(1) + fabs(bb)));
                 zz = bb;
-#pragma unroll
-                for (int i = 0; i < WSMAX; i++)
+#pragma unroll 1
+                for (int i = 0; i < m; i++)
                     if (((remm >> i) & 1u) && L.se_e[i] == se[j]) nwf &= ~(3u << (2 * j));
             } else {
                 const T tl = T(1e-13) * (T(1) + fabs(lb[j])), tu = T(1e-13) * (T(1) + fabs(ub[j]));
@@ -266,14 +311,7 @@ __device__ bool wsteps_run(const ClFastParams<T> &p, LdsT &L, int lane, const in
             }
             z[j] = zz;
         }
-        if (!__any(bad)) {
-#pragma unroll
-            for (int i = 0; i < WSMAX; i++)
-                if (lane == i) L.se_nu[i] = nu_[i];
-            CLF_SYNC();
-            m_acc = m;
-            return true;
-        }
+        if (!__any(bad)) return done(m);
         if (addok) {
             argmax_states(v);
 #pragma unroll
@@ -283,20 +321,18 @@ __device__ bool wsteps_run(const ClFastParams<T> &p, LdsT &L, int lane, const in
         wf = nwf;
         CLF_SYNC();
     }
-    return false;
+    return wsteps << 16;
 }
 
 // interval certificate (oracle/c/riccati_ipm.c infeasible_stage): lane i < NX carries state i of
 // X_k in midpoint / radius form, X_{k+1} = hull([A B] X_k x U + c) meets the state box of stage
 // k + 1; an empty intersection proves the QP infeasible
 template <typename T, int NX, int NU, class LdsT>
-__device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, int lane, const T (&x)[NX])
+__device__ __noinline__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, int lane)
 {
+    // x_0 in L.xs (the caller's copy)
     constexpr int NZ = NX + NU;
-    T m = 0, r = 0;
-#pragma unroll
-    for (int c = 0; c < NX; c++)
-        if (c == lane) m = x[c];
+    T m = lane < NX ? (T)L.xs[lane] : T(0), r = 0;
     T mu[NU], ru[NU];
 #pragma unroll
     for (int j = 0; j < NU; j++) {
@@ -405,11 +441,15 @@ __device__ __forceinline__ void plant_step(const ClFastParams<T> &p, const doubl
 // full tables plus the accepted active-set step (LDS), held bounds exact, bounded elements clamped;
 // a failed last step (status 4) outputs the initial point
 template <typename T, int NX, int NU, int EPL, class LdsT>
-__device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int inst, const T (&x0)[NX], int t, int status,
-                              int m)
+__device__ __noinline__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int inst, int t, int status, int m)
 {
+    // x_0 in L.xs (the caller's copy)
     constexpr int NZ = NX + NU;
     const int N = p.N, ne = p.ne;
+    T x0[NX];
+#pragma unroll
+    for (int c = 0; c < NX; c++) x0[c] = (T)L.xs[c];
+#pragma unroll 1
     for (int e = lane; e < ne; e += 64) {
         const int k = e / NZ, r = e % NZ;
         if (k == N && r >= NX) continue;
@@ -421,7 +461,7 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int i
         const T lb = p.lbnd[ty * NZ + r], ub = p.ubnd[ty * NZ + r];
         T z;
         if (status != 0) {
-            z = init_point(p, NX, NZ, k, r, t, &x0r);
+            z = init_point(p, NX, NZ, k, r, t, x0r);
         } else if (k == 0 && r < NX) {
             z = x0r;
         } else {
@@ -453,33 +493,33 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
 {
     constexpr int NZ = NX + NU, NSLOT = EPL * 64;
     __shared__ Lds<NSLOT, NZ> lds_all[WPB];
-    __shared__ double abl[NX * NZ], cl[NX];
+    // workgroup constants: [A B], c (plant), the slots' bounds, elements and warm-start sources
+    __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT];
+    __shared__ int sse[NSLOT], ssrc[NSLOT];
     for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) abl[e] = (double)p.AB[e];
     for (int e = threadIdx.x; e < NX; e += 64 * WPB) cl[e] = (double)p.c[e];
+    for (int s = threadIdx.x; s < NSLOT; s += 64 * WPB) {
+        const bool v = s < p.nslot;
+        slb[s] = v ? (double)p.s_lb[s] : -1e30;
+        sub[s] = v ? (double)p.s_ub[s] : 1e30;
+        sse[s] = v ? p.s_e[s] : -1;
+        ssrc[s] = v ? p.s_src[s] : -1;
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ> &L = lds_all[wave];
     const int gw = blockIdx.x * WPB + wave, nw = gridDim.x * WPB;
-    const int N = p.N, ne = p.ne;
+    const SlotView<EPL> sv{slb, sub, sse, ssrc, lane};
 
-    // ---- per-lane slot constants (once per wavefront): element, bounds, T_x row, warm-start source
-    int se[EPL], src[EPL];
-    T lb[EPL], ub[EPL], tx[EPL][NX];
+    // ---- the slots' T_x rows in registers (once per wavefront)
+    T tx[EPL][NX];
 #pragma unroll
     for (int j = 0; j < EPL; j++) {
         const int s = j * 64 + lane;
-        const bool v = s < p.nslot;
-        se[j] = v ? p.s_e[s] : -1;
-        src[j] = v ? p.s_src[s] : -1;
-        lb[j] = v ? p.s_lb[s] : T(-1e30);
-        ub[j] = v ? p.s_ub[s] : T(1e30);
 #pragma unroll
-        for (int c = 0; c < NX; c++) tx[j][c] = v ? p.s_tx[(size_t)s * NX + c] : T(0);
+        for (int c = 0; c < NX; c++) tx[j][c] = s < p.nslot ? p.s_tx[(size_t)s * NX + c] : T(0);
     }
-    // component of each slot (states: r < NX)
-    int sr[EPL];
-#pragma unroll
-    for (int j = 0; j < EPL; j++) sr[j] = se[j] >= 0 ? se[j] % NZ : -1;
+    const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
 
     for (int inst = gw; inst < p.B; inst += nw) {
         int step = p.istep[inst];
@@ -497,72 +537,88 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
                 fl |= (f < 0 ? 1u : (f > 0 ? 2u : 0u)) << (2 * j);
             }
         }
-        const int off = p.offset[inst];
-        int t = (int)(((long long)off + step) % p.period);
+        int t = (int)(((long long)p.offset[inst] + step) % p.period);
         double cost = 0.0, aed = 0.0, nfail = 0.0, nst = 0.0;
-        int last_status = 0, last_iters = 0, last_w = 0;   // last_w: the last accepted step's set size (outputs)
-        T z[EPL];
-        T xl_[NX];   // the state the last step solved from (x0 of the outputs)
-#pragma unroll
-        for (int c = 0; c < NX; c++) xl_[c] = x[c];
-        int tl_ = t;
+        int last_status = 0, last_iters = 0;
         bool parked = false;
+        // v_t at the slots one step ahead (the step's first dependency); the reference row and the noise
+        // draw are issued at the top of the step and consumed after the solve
+        constexpr int NR = NX < 8 ? NX : 8;   // reference components of cost / AED (nmpc_closed_loop_init: <= 8)
+        T vtn[EPL];
+        auto fetch_v = [&](int tt) {
+            const T *vp = p.vb + (size_t)tt * NSLOT;
+#pragma unroll
+            for (int j = 0; j < EPL; j++) vtn[j] = vp[j * 64 + lane];
+        };
+        fetch_v(t);
         for (; step < p.target; step++) {
-            // ---- warm start: the last solution's flags shifted by one stage (slot src)
+            T vt[EPL], xr[NR];
+#pragma unroll
+            for (int j = 0; j < EPL; j++) vt[j] = vtn[j];
+            const int tn = t + 1 == p.period ? 0 : t + 1;
+            if (step + 1 < p.target) fetch_v(tn);
+            {
+                const T *xp = p.table + (size_t)t * p.table_cols;
+#pragma unroll
+                for (int i = 0; i < NR; i++) xr[i] = i < nref ? xp[i] : T(0);
+            }
+            const double w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
+            // ---- warm start: the last solution's flags shifted by one stage (slot source)
             unsigned wf = 0;
             if (__any(fl != 0)) {
 #pragma unroll
-                for (int j = 0; j < EPL; j++) {
-                    const int s = j * 64 + lane;
-                    if (s < NSLOT) L.fl[s] = (fl >> (2 * j) & 1u) ? -1 : ((fl >> (2 * j) & 2u) ? 1 : 0);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int j = 0; j < EPL; j++) L.fl[j * 64 + lane] = flag_of(fl, j);
+                CLF_SYNC();
 #pragma unroll
                 for (int j = 0; j < EPL; j++) {
-                    const signed char f = src[j] >= 0 ? L.fl[src[j]] : 0;
-                    wf |= (f < 0 ? 1u : (f > 0 ? 2u : 0u)) << (2 * j);
+                    const int sr_ = sv.src(j);
+                    wf |= bits_of(sr_ >= 0 ? L.fl[sr_] : (signed char)0) << (2 * j);
                 }
-                __builtin_amdgcn_wave_barrier();
+                CLF_SYNC();
             }
             // ---- explicit unconstrained solution at the lane's slots
-            T z0[EPL];
-            const T *vt = p.vb + (size_t)t * NSLOT;
+            T z[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
-                T s0 = vt[j * 64 + lane], s1 = 0;
+                T s0 = vt[j], s1 = 0;
 #pragma unroll
                 for (int c = 0; c + 1 < NX; c += 2) {
                     s0 = fma(tx[j][c], x[c], s0);
                     s1 = fma(tx[j][c + 1], x[c + 1], s1);
                 }
                 if (NX % 2) s0 = fma(tx[j][NX - 1], x[NX - 1], s0);
-                z0[j] = s0 + s1;
+                z[j] = s0 + s1;
             }
             bool ok = false;
-            int status = 0, iters = 1, wsteps = 0;
+            int status = 0, iters = 1, m_acc = 0;
             if (!__any(wf != 0)) {
                 bool bad = false;
 #pragma unroll
-                for (int j = 0; j < EPL; j++) {
-                    const T tl = T(1e-13) * (T(1) + fabs(lb[j])), tu = T(1e-13) * (T(1) + fabs(ub[j]));
-                    bad |= (has_b(lb[j]) && z0[j] < lb[j] - tl) || (has_b(ub[j]) && z0[j] > ub[j] + tu) || !isfinite(z0[j]);
-                }
+                for (int j = 0; j < EPL; j++) bad |= violated(z[j], (T)sv.lb(j), (T)sv.ub(j)) || !isfinite(z[j]);
                 ok = !__any(bad);
-#pragma unroll
-                for (int j = 0; j < EPL; j++) z[j] = z0[j];
-                last_w = 0;
             }
             if (!ok) {
-                // ---- active-set steps on W (rare): see wsteps_run below
-                int m_acc = 0;
-                ok = wsteps_run<T, NX, NU, EPL>(p, L, lane, se, sr, lb, ub, z0, z, wf, wsteps, m_acc);
-                last_w = ok ? m_acc : 0;
-                iters = 1 + wsteps;
-                if (!ok) {
+                // ---- active-set steps on W (rare), the set and z_0 / z through LDS
+#pragma unroll
+                for (int j = 0; j < EPL; j++) {
+                    L.zb[j * 64 + lane] = (double)z[j];
+                    L.fl[j * 64 + lane] = flag_of(wf, j);
+                }
+                CLF_SYNC();
+                const int r = wsteps_run<T, NX, NU, EPL>(p, L, sv, lane);
+                ok = (r & 1) != 0;
+                m_acc = ok ? (r >> 8) & 0xff : 0;
+                iters = 1 + (r >> 16);
+                if (ok) {
+#pragma unroll
+                    for (int j = 0; j < EPL; j++) z[j] = (T)L.zb[j * 64 + lane];
+                } else {
                     // ---- interval certificate (oracle/c/riccati_ipm.c infeasible_stage)
-                    if (certificate_infeasible<T, NX, NU>(p, L, lane, x)) {
+#pragma unroll
+                    for (int c = 0; c < NX; c++)
+                        if (lane == c) L.xs[c] = (double)x[c];
+                    CLF_SYNC();
+                    if (certificate_infeasible<T, NX, NU>(p, L, lane)) {
                         status = 4;
                         iters = 0;
                     } else {
@@ -576,49 +632,50 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
             if (status == 0) {
 #pragma unroll
                 for (int j = 0; j < EPL; j++) {
-                    const bool onl = has_b(lb[j]) && z[j] <= lb[j] + T(1e-7) * (T(1) + fabs(lb[j]));
-                    const bool onu = has_b(ub[j]) && z[j] >= ub[j] - T(1e-7) * (T(1) + fabs(ub[j]));
+                    const T l = (T)sv.lb(j), u = (T)sv.ub(j);
+                    const bool onl = has_b(l) && z[j] <= l + T(1e-7) * (T(1) + fabs(l));
+                    const bool onu = has_b(u) && z[j] >= u - T(1e-7) * (T(1) + fabs(u));
                     fl |= (onl ? 1u : (onu ? 2u : 0u)) << (2 * j);
                 }
             }
-            // ---- u0 (slots 0..nu-1: lanes 0..nu-1 of j = 0), x1 for the cost of the jerk loop
+            // ---- u0 (slots 0..nu-1: lanes 0..nu-1 of j = 0), clamped onto its bound
+            const T z0c = fmin(fmax(z[0], (T)sv.lb(0)), (T)sv.ub(0));
             double u0[NU];
 #pragma unroll
-            for (int i = 0; i < NU; i++) {
-                const T zc = fmin(fmax(z[0], lb[0]), ub[0]);   // clamped onto the bound (held bounds land on it)
-                u0[i] = status == 0 ? bcast((double)zc, i) : (double)p.uinit[i];
-            }
-            const T *xref = p.table + (size_t)t * p.table_cols;
+            for (int i = 0; i < NU; i++) u0[i] = status == 0 ? bcast((double)z0c, i) : (double)p.uinit[i];
+            // ---- cost (controller.py:40-41) at x_0 = the state, or x_1 (jerk loop), and the AED numerator
             double cc = 0.0, aa = 0.0;
-            if (p.cost_stage == 0) {
-                for (int i = 0; i < p.ncl; i++) {
-                    const double e = (double)x[i] - (double)xref[i];
+#pragma unroll
+            for (int i = 0; i < NR; i++) {
+                if (i < p.ncl) {
+                    double xo = (double)x[i];
+                    if (p.cost_stage != 0) {
+                        xo = status == 0 ? bcast((double)z0c, p.x1_slot + i) : (double)init_point(p, NX, NZ, 1, i, t, T(0));
+                    }
+                    const double e = xo - (double)xr[i];
                     cc += (double)p.wcl[i] * e * e;
                 }
-            } else {
-                for (int i = 0; i < p.ncl; i++) {
-                    const T zc = fmin(fmax(z[0], lb[0]), ub[0]);
-                    const double x1 = status == 0 ? bcast((double)zc, p.x1_slot + i) : (double)xref[i];
-                    const double e = x1 - (double)xref[i];
-                    cc += (double)p.wcl[i] * e * e;
-                }
+                if (i < p.aed_dims) aa += fabs((double)xr[i] - (double)x[i]);
             }
-            for (int i = 0; i < p.aed_dims; i++) aa += fabs((double)xref[i] - (double)x[i]);
             cost += cc;
             aed += aa;
             nfail += status != 0 ? 1.0 : 0.0;
             nst += 1.0;
             last_status = status;
             last_iters = iters;
+            // ---- the trajectory outputs of the instance's last step of the run
+            if (step + 1 == p.target) {
 #pragma unroll
-            for (int c = 0; c < NX; c++) xl_[c] = x[c];
-            tl_ = t;
+                for (int c = 0; c < NX; c++)
+                    if (lane == c) L.xs[c] = (double)x[c];
+                CLF_SYNC();
+                write_outputs<T, NX, NU, EPL>(p, L, lane, inst, t, status, m_acc);
+            }
             // ---- plant step + noise
-            const double w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
             plant_step<T, NX, NU, SP>(p, abl, cl, x, u0, w);
-            t = t + 1 == p.period ? 0 : t + 1;
+            t = tn;
         }
-        // ---- write back: state, sums, step, flags, status; the outputs at the instance's last step
+        // ---- write back: state, sums, step, flags, status
         if (lane == 0) {
 #pragma unroll
             for (int c = 0; c < NX; c++) p.state[(size_t)inst * NX + c] = x[c];
@@ -639,9 +696,8 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
 #pragma unroll
         for (int j = 0; j < EPL; j++) {
             const int s = j * 64 + lane;
-            if (s < p.nslot) p.flags[(size_t)inst * p.nslot + s] = (fl >> (2 * j) & 1u) ? -1 : ((fl >> (2 * j) & 2u) ? 1 : 0);
+            if (s < p.nslot) p.flags[(size_t)inst * p.nslot + s] = flag_of(fl, j);
         }
-        if (!parked && nst > 0.0) write_outputs<T, NX, NU, EPL>(p, L, lane, inst, xl_, tl_, last_status, last_w);
     }
 }
 
