@@ -155,8 +155,10 @@ class ClosedLoop:
     def iter_log(self):
         """Per-step solve record of the last fused launch (env NMPC_ITER_LOG set before the run):
         (finish steps, IPM iterations, status), each [steps, batch]."""
-        steps = int(self.stats()["steps"])
-        buf = np.zeros((min(steps, 64), self.batch), dtype=np.int32)
+        steps = int(self.lib.nmpc_closed_loop_iter_log(self.solver._h, None, 0))
+        if steps <= 0:
+            raise NmpcError("nmpc_closed_loop_iter_log: no log (NMPC_ITER_LOG with the fused kernels, NMPC_CL_FAST=0)")
+        buf = np.zeros((steps, self.batch), dtype=np.int32)
         rc = self.lib.nmpc_closed_loop_iter_log(self.solver._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                                 buf.size)
         if rc < 0:

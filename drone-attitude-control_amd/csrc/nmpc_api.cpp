@@ -313,8 +313,8 @@ void lqr_table(int nx, int nu, int N, const std::vector<double> &A, const std::v
                 for (int l = 0; l < j; l++) s_ -= L[i * nu + l] * L[j * nu + l];
                 L[i * nu + j] = i == j ? std::sqrt(std::max(s_, 1e-300)) : s_ / L[j * nu + j];
             }
+        std::vector<double> y(nu);
         for (int c = 0; c < nu; c++) {   // column c of F_uu^{-1}: L L' x = e_c
-            double y[64];
             for (int i = 0; i < nu; i++) {
                 double s_ = i == c ? 1.0 : 0.0;
                 for (int l = 0; l < i; l++) s_ -= L[i * nu + l] * y[l];
@@ -405,7 +405,7 @@ void lqr_wmat(int nx, int nu, int N, const std::vector<double> &A, const std::ve
         std::vector<double> x(nx, 0.0), xn(nx);
         for (int k = 0; k < N; k++) {
             const double *t = &tab[(size_t)k * nz * W];
-            double uu[64];
+            std::vector<double> uu(nu);
             for (int u = 0; u < nu; u++) {
                 double s_ = kff[(size_t)k * nu + u];
                 for (int j = 0; j < nx; j++) s_ += t[j * W + nx + u] * x[j];
@@ -631,7 +631,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     // tuning / test switches, read per launch: NMPC_LQR=0 drops the shared factorisation (every finish
     // step factors), NMPC_FAST=0 / 2 the fast finish (2: not at a launch's first step),
     // NMPC_WARM_SHIFT=0 the warm-start shift
-    const bool no_lqr = std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0';
+    const bool no_lqr = (std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0') || h->lqr_host.empty();
     p.lqr = no_lqr ? nullptr : (const T *)(m + h->off_lqr);
     p.lqrf = no_lqr ? nullptr : (const T *)(m + h->off_lqrf);
     const bool no_w = std::getenv("NMPC_WSET") && std::getenv("NMPC_WSET")[0] == '0';
@@ -975,9 +975,12 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_Ge = carve((size_t)nx * std::max(ny_e, 1));
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
-    h->off_lqr = carve((size_t)N * nz * lqr_words(nx, nu));
-    h->off_lqrf = carve((size_t)N * nz * lqrf_words(nx, nu));
-    h->off_lqrw = carve((size_t)(N + 1) * nz * (N + 1) * nz);
+    // the unconstrained factorisation's tables (lqr_table, lqr_wmat) serve only the exact finish's
+    // shortcuts of the stage-wise kernels: fp64 handles with the finish on (polish_mu > 0)
+    const bool lqr_on = !h->cond && f64 && h->polish_mu > 0;
+    h->off_lqr = carve(lqr_on ? (size_t)N * nz * lqr_words(nx, nu) : 0);
+    h->off_lqrf = carve(lqr_on ? (size_t)N * nz * lqrf_words(nx, nu) : 0);
+    h->off_lqrw = carve(lqr_on ? (size_t)(N + 1) * nz * (N + 1) * nz : 0);
     const size_t model_bytes = off;
     if (h->cond) {
         if (!nmpc::cond_build(nx, nu, N, ny, ny_e, h->A, h->B, h->c, h->H, h->G, h->He, h->Ge, h->lbnd, h->ubnd, h->ch)) {
@@ -1057,7 +1060,7 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     put(h->off_Ge, h->Ge);
     put(h->off_lb, h->lbnd);
     put(h->off_ub, h->ubnd);
-    {
+    if (lqr_on) {
         std::vector<double> &lqr = h->lqr_host, lqrf;
         lqr_table(nx, nu, N, h->A, h->B, h->c, h->H, h->He, lqr, lqrf);
         put(h->off_lqr, lqr);
@@ -1823,6 +1826,7 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
         h->cl_events.push_back(e);
     }
     h->out_valid = false;
+    h->iter_log_steps = 0;   // the log describes the last fused launch of this run only
     int launches = 0;
     const char *fused_env = std::getenv("NMPC_CL_FUSED");
     if (h->clf && steps > 0 && !(fused_env && fused_env[0] == '0')) {
@@ -1890,7 +1894,8 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
 
 int nmpc_closed_loop_iter_log(nmpc_solver *h, int32_t *out, size_t count)
 {
-    if (!h || !out) return NMPC_EINVAL;
+    if (!h) return NMPC_EINVAL;
+    if (!out) return h->d_iter_log ? h->iter_log_steps : 0;   // query: steps in the log
     if (!h->d_iter_log || h->iter_log_steps <= 0)
         return h->fail(NMPC_ESTATE, "nmpc_closed_loop_iter_log: no log (set NMPC_ITER_LOG and run a fused closed loop)");
     const size_t n = (size_t)h->iter_log_steps * h->batch;

@@ -106,7 +106,7 @@ __device__ __forceinline__ bool violated(T z, T l, T u)
 // the solver's initial point at element (k, r) (the lane-per-component kernel's failure output):
 // x_0 pinned, states at the reference projected 1 % inside their box, inputs mid-box
 template <typename T>
-__device__ __noinline__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, int t, T x0r)
+__device__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, int t, T x0r)
 {
     const int ty = k == 0 ? 0 : (k == p.N ? 2 : 1);
     const T lb = p.lbnd[ty * nz + r], ub = p.ubnd[ty * nz + r];
@@ -137,7 +137,7 @@ __device__ __noinline__ T init_point(const ClFastParams<T> &p, int nx, int nz, i
 // set restarts from z_0 (one round). false: set larger than WSMAX, W_SS not positive definite, or no
 // acceptance in polish_steps rounds.
 template <typename T, int NX, int NU, int EPL, class LdsT>
-__device__ __noinline__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane)
+__device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane)
 {
     constexpr int NZ = NX + NU;
     const int ne = p.ne;
@@ -328,7 +328,7 @@ __device__ __noinline__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const 
 // X_k in midpoint / radius form, X_{k+1} = hull([A B] X_k x U + c) meets the state box of stage
 // k + 1; an empty intersection proves the QP infeasible
 template <typename T, int NX, int NU, class LdsT>
-__device__ __noinline__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, int lane)
+__device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, int lane)
 {
     // x_0 in L.xs (the caller's copy)
     constexpr int NZ = NX + NU;
@@ -441,7 +441,7 @@ __device__ __forceinline__ void plant_step(const ClFastParams<T> &p, const doubl
 // full tables plus the accepted active-set step (LDS), held bounds exact, bounded elements clamped;
 // a failed last step (status 4) outputs the initial point
 template <typename T, int NX, int NU, int EPL, class LdsT>
-__device__ __noinline__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int inst, int t, int status, int m)
+__device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int inst, int t, int status, int m)
 {
     // x_0 in L.xs (the caller's copy)
     constexpr int NZ = NX + NU;
@@ -496,6 +496,18 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
     // workgroup constants: [A B], c (plant), the slots' bounds, elements and warm-start sources
     __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT];
     __shared__ int sse[NSLOT], ssrc[NSLOT];
+    // the slots' T_x rows, component-major (txl[c][s]: lanes read consecutive words, no bank conflicts),
+    // shared by the workgroup's wavefronts — registers stay free for occupancy
+    // pairs of components per 16-byte word (txl[c / 2][s] = (T_x(s, c), T_x(s, c + 1))): one ds_read_b128
+    // per slot and pair
+    constexpr int NXP = (NX + 1) / 2;
+    __shared__ double2 txl[NXP][NSLOT];
+    for (int e = threadIdx.x; e < NXP * NSLOT; e += 64 * WPB) {
+        const int c = e / NSLOT, s_ = e % NSLOT;
+        const bool v = s_ < p.nslot;
+        txl[c][s_] = make_double2(v ? (double)p.s_tx[(size_t)s_ * NX + 2 * c] : 0.0,
+                                  v && 2 * c + 1 < NX ? (double)p.s_tx[(size_t)s_ * NX + 2 * c + 1] : 0.0);
+    }
     for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) abl[e] = (double)p.AB[e];
     for (int e = threadIdx.x; e < NX; e += 64 * WPB) cl[e] = (double)p.c[e];
     for (int s = threadIdx.x; s < NSLOT; s += 64 * WPB) {
@@ -511,14 +523,6 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
     const int gw = blockIdx.x * WPB + wave, nw = gridDim.x * WPB;
     const SlotView<EPL> sv{slb, sub, sse, ssrc, lane};
 
-    // ---- the slots' T_x rows in registers (once per wavefront)
-    T tx[EPL][NX];
-#pragma unroll
-    for (int j = 0; j < EPL; j++) {
-        const int s = j * 64 + lane;
-#pragma unroll
-        for (int c = 0; c < NX; c++) tx[j][c] = s < p.nslot ? p.s_tx[(size_t)s * NX + c] : T(0);
-    }
     const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
 
     for (int inst = gw; inst < p.B; inst += nw) {
@@ -577,18 +581,30 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
                 CLF_SYNC();
             }
             // ---- explicit unconstrained solution at the lane's slots
-            T z[EPL];
+            T z[EPL], z1[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
-                T s0 = vt[j], s1 = 0;
-#pragma unroll
-                for (int c = 0; c + 1 < NX; c += 2) {
-                    s0 = fma(tx[j][c], x[c], s0);
-                    s1 = fma(tx[j][c + 1], x[c + 1], s1);
-                }
-                if (NX % 2) s0 = fma(tx[j][NX - 1], x[NX - 1], s0);
-                z[j] = s0 + s1;
+                z[j] = vt[j];
+                z1[j] = T(0);
             }
+            // x in LDS for the rolled pair loop (its component pair is wave-uniform)
+#pragma unroll
+            for (int c = 0; c < NX; c++)
+                if (lane == c) L.xs[c] = (double)x[c];
+            if (lane == NX) L.xs[NX] = 0.0;
+            CLF_SYNC();
+#pragma unroll 1
+            for (int c = 0; c < NXP; c++) {
+                const double xa = L.xs[2 * c], xb = L.xs[2 * c + 1];
+#pragma unroll
+                for (int j = 0; j < EPL; j++) {
+                    const double2 tt = txl[c][j * 64 + lane];
+                    z[j] = fma((T)tt.x, (T)xa, z[j]);
+                    z1[j] = fma((T)tt.y, (T)xb, z1[j]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < EPL; j++) z[j] += z1[j];
             bool ok = false;
             int status = 0, iters = 1, m_acc = 0;
             if (!__any(wf != 0)) {

@@ -236,8 +236,10 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n);
 /* per-instance accumulators, batch*4: [cost sum, AED numerator, failed solves, steps] of each
  * instance (the Monte-Carlo distribution behind nmpc_closed_loop_stats' sums) */
 int nmpc_closed_loop_instance_stats(nmpc_solver *h, double *out, size_t count);
-/* tuning aid: with env NMPC_ITER_LOG set, the per-step solve record of the last fused launch,
- * steps*batch values [step][instance] = finish steps | IPM iterations << 8 | status << 16; returns the step count */
+/* tuning aid: with env NMPC_ITER_LOG set, the per-step solve record of the last fused launch of the
+ * fused lane-per-component / wavefront kernels (not the lean loop: NMPC_CL_FAST=0), steps*batch values
+ * [step][instance] = finish steps | IPM iterations << 8 | status << 16; returns the step count.
+ * out = NULL: returns the step count only (0: no log) */
 int nmpc_closed_loop_iter_log(nmpc_solver *h, int32_t *out, size_t count);
 /* current closed-loop states, batch*nx */
 int nmpc_closed_loop_get_state(nmpc_solver *h, double *out, size_t count);
