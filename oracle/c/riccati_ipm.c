@@ -779,10 +779,12 @@ typedef struct {
     unsigned long long seed;
     long long inst_base;
     const long long *inst_ids;   /* optional [batch] global instance ids of the Philox stream (else inst_base + b) */
+    int wsmax;              /* largest active set of mode 1's fast finish (the device's per model: nmpc_cl_fast.hip
+                               cl_fast_wsmax; 0 = 8, at most WSMAX) */
 } cl_ref_desc;
 
 #ifndef WSMAX
-#define WSMAX 8
+#define WSMAX 64
 #endif
 
 
@@ -996,7 +998,7 @@ static int valid_el(int nx, int N, int k, int i) { return !(k == 0 && i < nx) &&
  * infeasible QP), -4 polish_steps rounds without acceptance. Counts the active-set steps and the
  * FP64 work. */
 static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double *x0, int t, signed char *wf,
-                       double *z0, double *z, int *wsteps, double *flops)
+                       double *z0, double *z, int *wsteps, double *flops, int wsmax)
 {
     const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
     const double *vt = f->v + (size_t)t * ne;
@@ -1049,7 +1051,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
                 }
             continue;
         }
-        if (m > WSMAX) return -2;
+        if (m > wsmax) return -2;
         double L[WSMAX][WSMAX], nu_[WSMAX], lt[WSMAX], wd[WSMAX];
         for (int i = 0; i < m; i++) {
             const int k = S[i] / nz, c = S[i] % nz;
@@ -1365,6 +1367,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
         return -1;
     fast_tables *f = mode == 1 ? fast_init(d, c) : NULL;
     const double fi = f_iter(nx, nu, N);
+    const int wsmax = c->wsmax > 0 ? (c->wsmax < WSMAX ? c->wsmax : WSMAX) : 8;
     double cnt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int nfail = 0;
 #ifdef _OPENMP
@@ -1405,7 +1408,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                     if (d->polish_mu > 0.0) {
                         int wst = 0, nw = 0;
                         for (int e = 0; e < ne; e++) nw += wf[e] != 0;
-                        ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6]) > 0;
+                        ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax) > 0;
                         cnt[3] += wst;
                         if (ok) {
                             path = (nw == 0 && wst == 0) ? 0 : 1;
