@@ -153,11 +153,12 @@ class ClosedLoop:
         return out
 
     def iter_log(self):
-        """Per-step solve record of the last fused launch (env NMPC_ITER_LOG set before the run):
-        (finish steps, IPM iterations, status), each [steps, batch]."""
+        """Per-step solve record (env NMPC_ITER_LOG set before the run), each [steps, batch]: the fused
+        kernels' last launch (NMPC_CL_FAST=0): (finish steps, IPM iterations, status); the lean loop's
+        last run (nmpc_cl_fast.hip): (active-set steps, status, clock cycles / 64 of the step)."""
         steps = int(self.lib.nmpc_closed_loop_iter_log(self.solver._h, None, 0))
         if steps <= 0:
-            raise NmpcError("nmpc_closed_loop_iter_log: no log (NMPC_ITER_LOG with the fused kernels, NMPC_CL_FAST=0)")
+            raise NmpcError("nmpc_closed_loop_iter_log: no log (set NMPC_ITER_LOG before the run)")
         buf = np.zeros((steps, self.batch), dtype=np.int32)
         rc = self.lib.nmpc_closed_loop_iter_log(self.solver._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                                 buf.size)

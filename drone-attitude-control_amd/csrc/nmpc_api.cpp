@@ -219,6 +219,8 @@ struct nmpc_solver {
     // lean closed loop (nmpc_cl_fast.hip): slot tables, per-instance step / flags, park list
     bool clf = false;
     int clf_nslot = 0, clf_epl = 0, clf_x1slot = 0, clf_sid = 0;
+    int clf_kidx = -1;                     // list-mode fallback kernel (lane per component)
+    void *d_clf_scratch = nullptr;         // its scratch when the handle's own family is another
     void *d_fsT = nullptr;                 // typed: s_lb, s_ub, s_tx, vb, uinit
     size_t fso[5] = {0, 0, 0, 0, 0};
     int *d_fsI = nullptr;                  // s_e, s_src, eslot
@@ -236,7 +238,8 @@ struct nmpc_solver {
     int cl_step = 0, cl_last_launches = 0, cl_last_steps = 0;
     double *d_fnoise = nullptr;   // fused closed loop: noise draws of a launch's steps [B][64]
     int *d_iter_log = nullptr;    // fused closed loop, env NMPC_ITER_LOG: per-step finish steps | IPM iterations << 8 | status << 16 [64][B]
-    int iter_log_steps = 0;       // steps in the log (the last fused launch)
+    int iter_log_steps = 0;       // steps in the log (the last fused launch; the lean loop: the last run)
+    size_t iter_log_cap = 0;      // capacity of d_iter_log (ints)
     std::vector<hipEvent_t> cl_events;
     double cl_last_ms = 0.0;
     double cost_s = 1.0;  // stage cost factor (time step or 1)
@@ -490,7 +493,7 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
                     (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
-                    (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags})
+                    (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -574,8 +577,12 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
 {
     if (h->cond) return launch_cond<T>(h, e0, e1);
     nmpc::IpmParams<T> p{};
+    int kidx = h->kidx;
+    void *scratch = h->d_scratch;
     p.cl_steps = cl_steps;
     if (la) {
+        kidx = h->clf_kidx;
+        if (h->d_clf_scratch) scratch = h->d_clf_scratch;
         p.cl_list = h->d_park + 1;
         p.cl_count = la->count;
         p.cl_istep = h->d_istep;
@@ -592,6 +599,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
         if (iter_log && !h->d_iter_log &&
             hipMalloc((void **)&h->d_iter_log, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(int)) != hipSuccess)
             h->d_iter_log = nullptr;
+        if (h->d_iter_log && h->iter_log_cap < (size_t)h->batch * CL_FUSED_CHUNK) h->iter_log_cap = (size_t)h->batch * CL_FUSED_CHUNK;
         p.iter_log = iter_log && !la ? h->d_iter_log : nullptr;
         const bool no_expl = std::getenv("NMPC_EXPLICIT") && std::getenv("NMPC_EXPLICIT")[0] == '0';
         p.cl_tx = no_expl ? nullptr : (const T *)h->d_cltx;
@@ -642,7 +650,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     p.uout = (T *)h->d_u;
     p.status = h->d_status;
     p.iters = h->d_iters;
-    p.scratch = (T *)h->d_scratch;
+    p.scratch = (T *)scratch;
     p.ipw = h->ipw;
     p.lpi_stride = ((long long)h->batch + h->ipw - 1) / h->ipw * h->ipw;
     p.cycles = nullptr;
@@ -653,7 +661,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
         p.cycles = h->d_cycles;
     }
     hipEventRecord(e0 ? e0 : h->ev0, h->stream);
-    hipError_t e = nmpc::ipm_launch<T>(h->kidx, p, h->stream);
+    hipError_t e = nmpc::ipm_launch<T>(kidx, p, h->stream);
     hipEventRecord(e1 ? e1 : h->ev1, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "ipm kernel launch");
     if (sweep_cycles && h->d_cycles) {
@@ -1490,10 +1498,10 @@ hipError_t put_typed(void *dst, const double *src, size_t n, bool f64)
     return hipMemcpy(dst, t.data(), n * sizeof(float), hipMemcpyHostToDevice);
 }
 
-// The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, the
-// lane-per-component family (its list mode is the fallback), a compiled slot layout for (nx, nu);
-// on by default for quad13 and jerk, NMPC_CL_FAST=1 for any compiled shape (force: its input
-// saturation sets exceed the fast path's 8 bounds, the fused kernel stays faster), =0 off.
+// The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, a compiled slot
+// layout for (nx, nu) (quad13, jerk, force: on by default; NMPC_CL_FAST=0 off). Its fallback is the
+// lane-per-component kernel's list mode: a handle of the wavefront family (small models at small
+// batches) gets that family's kernel and scratch as well.
 // Slots: the bounded elements of z in stage-major order (stage 0's inputs first), their bounds,
 // T_x rows, v_t columns and warm-start sources (the element one stage later; stage N - 1's inputs
 // keep their own flag, as the fused kernel's mirror of stage N).
@@ -1501,11 +1509,21 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
 {
     const int nx = h->nx, nu = h->nu, nz = nx + nu, N = h->N, ne = (N + 1) * nz, P_ = d.ref_period;
     const char *env = std::getenv("NMPC_CL_FAST");
-    const bool want = env ? env[0] != '0' : ((nx == 13 && nu == 4) || (nx == 6 && nu == 2));
-    const int kind = nmpc::ipm_kind<double>(h->kidx);
+    const bool want = !env || env[0] != '0';
     const int epl = nmpc::cl_fast_epl(nx, nu);
-    if (!want || h->precision != NMPC_FP64 || !(h->polish_mu > 0) || !h->g_diag || h->cond || kind != 1 || epl <= 0)
+    if (!want || h->precision != NMPC_FP64 || !(h->polish_mu > 0) || !h->g_diag || h->cond || epl <= 0)
         return 0;
+    int fk = h->kidx;
+    if (nmpc::ipm_kind<double>(h->kidx) != 1) {
+        fk = nmpc::ipm_find_family<double>(nx, nu, 1);
+        if (fk < 0) return 0;
+        std::vector<double> ABh((size_t)nx * nz);
+        for (int r = 0; r < nx; r++) {
+            for (int q = 0; q < nx; q++) ABh[r * nz + q] = h->A[r * nx + q];
+            for (int q = 0; q < nu; q++) ABh[r * nz + nx + q] = h->B[r * nu + q];
+        }
+        fk = nmpc::ipm_refine<double>(fk, ABh.data(), h->H.data(), h->He.data());
+    }
     std::vector<int> el;
     std::vector<double> lb, ub;
     for (int k = 0; k <= N; k++)
@@ -1562,7 +1580,8 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         h->fsi[i] = itot;
         itot += (ip[i]->size() + 63) & ~(size_t)63;
     }
-    for (void **q : {&h->d_fsT, (void **)&h->d_fsI, (void **)&h->d_istep, (void **)&h->d_park, (void **)&h->d_flags})
+    for (void **q : {&h->d_fsT, (void **)&h->d_fsI, (void **)&h->d_istep, (void **)&h->d_park, (void **)&h->d_flags,
+                     &h->d_clf_scratch})
         if (*q) {
             hipFree(*q);
             *q = nullptr;
@@ -1572,6 +1591,8 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
               hipMalloc((void **)&h->d_istep, (size_t)h->batch * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_park, (size_t)(h->batch + 1) * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_flags, (size_t)h->batch * nslot) == hipSuccess;
+    if (ok && fk != h->kidx)
+        ok = hipMalloc(&h->d_clf_scratch, nmpc::ipm_scratch_elems<double>(fk, h->batch, N) * sizeof(double)) == hipSuccess;
     if (!ok) return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: lean closed-loop tables");
     hipError_t e = hipSuccess;
     for (int i = 0; i < 5 && e == hipSuccess; i++)
@@ -1585,7 +1606,8 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     h->clf_nslot = nslot;
     h->clf_epl = epl;
     h->clf_x1slot = x1slot;
-    h->clf_sid = nmpc::ipm_structure<double>(h->kidx);
+    h->clf_sid = nmpc::ipm_structure<double>(fk);
+    h->clf_kidx = fk;
     return 0;
 }
 
@@ -1678,7 +1700,19 @@ int clf_run(nmpc_solver *h, int steps)
     nmpc::ClParams<double> cp = cl_params<double>(h);
     hipError_t e = nmpc::cl_noise_launch<double>(cp, h->cl_step, steps, h->d_fnoise, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
-    const nmpc::ClFastParams<double> fp = clf_params(h, target, h->cl_step, steps);
+    nmpc::ClFastParams<double> fp = clf_params(h, target, h->cl_step, steps);
+    // env NMPC_ITER_LOG: the per-step record of the run (tuning aid, nmpc_closed_loop_iter_log)
+    static const bool iter_log = std::getenv("NMPC_ITER_LOG") != nullptr;
+    if (iter_log) {
+        if (h->iter_log_cap < need) {
+            if (h->d_iter_log) hipFree(h->d_iter_log);
+            h->d_iter_log = nullptr;
+            h->iter_log_cap = 0;
+            if (hipMalloc((void **)&h->d_iter_log, need * sizeof(int)) == hipSuccess) h->iter_log_cap = need;
+        }
+        fp.iter_log = h->d_iter_log;
+        h->iter_log_steps = h->d_iter_log ? steps : 0;
+    }
     int launches = 0;
     // one wavefront per instance at a time: at most 8 per SIMD resident, the rest stride
     const int waves = std::min(h->batch, 8192);
@@ -1703,6 +1737,15 @@ int clf_run(nmpc_solver *h, int steps)
         if (r < 0) return r;
         if (dbg && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "lean closed loop (list-mode fallback)");
     }
+    static const bool dbg = std::getenv("NMPC_CLF_DEBUG") != nullptr;
+    if (dbg && hipStreamSynchronize(h->stream) == hipSuccess)
+        for (int i = 0; i < launches; i++) {
+            float ms = 0.f, gap = 0.f;
+            hipEventElapsedTime(&ms, cl_event(h, 2 * i), cl_event(h, 2 * i + 1));
+            if (i + 1 < launches) hipEventElapsedTime(&gap, cl_event(h, 2 * i + 1), cl_event(h, 2 * i + 2));
+            std::fprintf(stderr, "[nmpc clf] steps %d..%d launch %d (%s): %.4f ms, then %.4f ms to the next\n", h->cl_step,
+                         target, i, i % 2 ? "list-mode full solve" : "fast", ms, gap);
+        }
     h->cl_step = target;
     return launches;
 }

@@ -11,7 +11,7 @@
 //     row t the window starts at (tables built at nmpc_closed_loop_init);
 //   * if the previous solution touched no bound and z_0 satisfies every bound (1e-13), it is the
 //     solution; otherwise primal-dual active-set steps on the projected inverse Hessian W of the
-//     unconstrained problem (z = z_0 + W[:, S] nu, W_SS nu = b_S - z_0,S, sets of <= WSMAX bounds,
+//     unconstrained problem (z = z_0 + W[:, S] nu, W_SS nu = b_S - z_0,S, sets of <= WSM bounds,
 //     KKT acceptance with the multiplier signs measured as displacements nu_i W_ii);
 //   * a QP the interval certificate proves infeasible returns status 4 with the initial point's
 //     inputs (the lane-per-component kernel's failure output);
@@ -20,14 +20,19 @@
 //
 // Layout: only the bounded elements of z matter for the test (quad13: 251 of 357), so the wavefront's
 // 64 lanes own them in "slots" s = j * 64 + lane (j < EPL, stage-major order: stage 0's inputs are
-// slots 0..nu-1, stage 1's bounded elements follow). Each lane keeps its slots' T_x rows, bounds and
-// element indices in registers for the whole launch (loaded once per wavefront), so a step costs one
-// coalesced load of the window's v_t slots, EPL x nx FMAs per lane and a few wave reductions; the
-// state, the plant step and the sums are wave-uniform. No per-step stores: the solution's active flags
-// stay in a register mask, the trajectory outputs are written once, at the instance's last step.
-// The unbounded elements (quaternions, the terminal stage) are formed only for those outputs.
+// slots 0..nu-1, stage 1's bounded elements follow). The slots' T_x rows, bounds and test thresholds
+// sit in the workgroup's LDS (shared by its wavefronts). The closed-loop state is lane-distributed:
+// lane i < nx holds x_i, so the plant step is one dense row per lane ([A B] row from LDS, x from a
+// broadcast LDS copy, u0 by readlane) and the cost / AED terms are per-lane partial sums reduced once,
+// when the instance's launch ends. A step costs one coalesced load of the window's v_t slots (one step
+// ahead), EPL x nx FMAs per lane, one wave vote, the plant row and the per-lane sums. No per-step
+// stores: the solution's active flags stay in a register mask, the trajectory outputs are written once,
+// at the instance's last step.
 
 #include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdlib>
 
 #include "nmpc_cl_device.h"
 #include "nmpc_internal.h"
@@ -36,8 +41,8 @@
 namespace nmpc {
 namespace clf {
 
-constexpr int WSMAX = 8;   // largest active set of the fast path (the lane-per-component kernel's)
-constexpr int WPB = 4;     // wavefronts per workgroup
+
+constexpr int PDAS_ROUNDS = 6;   // rounds of the first PDAS run before the fallback (oracle: fast_finish's cap)
 
 template <typename T>
 __device__ __forceinline__ bool has_b(T b)
@@ -53,30 +58,55 @@ __device__ __forceinline__ double bcast(double v, int l)
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
-__device__ __forceinline__ unsigned long long ballot(bool b) { return __ballot(b); }
+// sum / max / min over the wavefront's lanes (butterfly)
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
 
 // per-wavefront LDS: active flags by slot (the warm-start shift), the set of an active-set step
-// (element, sign, target b - z_0, multiplier), the per-component argmax of the violated states, and
-// the certificate's stage exchange
-template <int NSLOT, int NZ>
+// (element, sign, target b - z_0, multiplier), W_SS and its Cholesky factor, the per-component argmax
+// of the violated states, the certificate's stage exchange and the state copy
+template <int NSLOT, int NZ, int WSM>
 struct Lds {
-    double zb[NSLOT];          // z_0 into / z out of the active-set steps
-    signed char fl[NSLOT];     // flags: the warm-start shift buffer; the active-set steps' set
-    double se_t[WSMAX], se_nu[WSMAX], wdg[WSMAX], wss[WSMAX][WSMAX];
-    int se_e[WSMAX], se_s[WSMAX];
+    alignas(16) double xs[32];   // x (lane i writes x_i; x_nx.. stay 0): explicit form, plant rows, rare paths
+    signed char fl[NSLOT];       // the warm-start shift buffer
+    double se_t[WSM], se_nu[WSM], wdg[WSM], wss[WSM][WSM + 1];
+    int se_e[WSM], se_s[WSM], gi_slot[WSM];
     unsigned long long vmax[NZ];
     int vslot[NZ];
-    double cm[32], cr[32], xs[32];   // certificate exchange; x_0 for the certificate and the outputs
+    double cm[32], cr[32];       // certificate exchange
 };
 
-// the workgroup's slot constants (LDS), seen from one lane: slot j of this lane is j * 64 + lane
+// the workgroup's slot constants (LDS), seen from one lane: slot j of this lane is j * 64 + lane.
+// lo / hi: violation thresholds of the fast path (z < lo or z > hi: a bound violated beyond 1e-13
+// relative to 1 + |b|; -/+DBL_MAX without a bound); onl / onu: on-bound thresholds of the warm-start
+// flags (z <= onl: on the lower bound to 1e-7, z >= onu: on the upper)
 template <int EPL>
 struct SlotView {
-    const double *lb_, *ub_;
+    const double *lb_, *ub_, *lo_, *hi_, *onl_, *onu_;
     const int *e_, *src_;
     int lane;
     __device__ double lb(int j) const { return lb_[j * 64 + lane]; }
     __device__ double ub(int j) const { return ub_[j * 64 + lane]; }
+    __device__ double lo(int j) const { return lo_[j * 64 + lane]; }
+    __device__ double hi(int j) const { return hi_[j * 64 + lane]; }
+    __device__ double onl(int j) const { return onl_[j * 64 + lane]; }
+    __device__ double onu(int j) const { return onu_[j * 64 + lane]; }
     __device__ int e(int j) const { return e_[j * 64 + lane]; }
     __device__ int src(int j) const { return src_[j * 64 + lane]; }
 };
@@ -88,13 +118,6 @@ __device__ __forceinline__ signed char flag_of(unsigned m, int j)
     return b == 1u ? (signed char)-1 : (b == 2u ? (signed char)1 : (signed char)0);
 }
 __device__ __forceinline__ unsigned bits_of(signed char f) { return f < 0 ? 1u : (f > 0 ? 2u : 0u); }
-
-// a bound violated beyond the fast path's 1e-13 (relative to 1 + |b|)
-template <typename T>
-__device__ __forceinline__ bool violated(T z, T l, T u)
-{
-    return (has_b(l) && z < l - T(1e-13) * (T(1) + fabs(l))) || (has_b(u) && z > u + T(1e-13) * (T(1) + fabs(u)));
-}
 
 #define CLF_SYNC()                                               \
     do {                                                         \
@@ -127,38 +150,143 @@ __device__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, 
     return v;
 }
 
-// Primal-dual active-set steps on W (oracle/c/riccati_ipm.c fast_finish; the lane-per-component
-// kernel's W steps): wf holds the set (warm start, or empty: the first set from z_0's violations —
-// the violated inputs and each state component's most violated stage). Each round solves
-// W_SS nu = b_S - z_0,S (Cholesky on every lane, the set broadcast through LDS, W_SS by wave-uniform
-// loads), sets z = z_0 + W[:, S] nu at the lane's slots and accepts when the held bounds are met
-// (1e-9), no other bound is violated (1e-13) and every multiplier has its sign (displacement nu_i W_ii
-// to 1e-10 (1 + |b - z_0|)); otherwise removals and additions as the finish's PDAS rule. An emptied
-// set restarts from z_0 (one round). false: set larger than WSMAX, W_SS not positive definite, or no
-// acceptance in polish_steps rounds.
-template <typename T, int NX, int NU, int EPL, class LdsT>
-__device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane)
+// Cholesky of W_SS for the m elements in L.se_e (W_SS gathered over 8 x 8 lane tiles into the lower
+// triangle of L.wss, its diagonal into L.wdg; right-looking: column c scaled by its lanes, then the
+// trailing update over lane tiles). A pivot below 1e-9 of its diagonal W_ii (a bound linearly dependent
+// on the ones before it) is regularised to 1e-6 W_ii: that bound is held by a penalty (oracle/c/
+// riccati_ipm.c fast_finish / gi_factor). false: a non-positive W_ii.
+template <typename T, class LdsT>
+__device__ bool factor_set(const ClFastParams<T> &p, LdsT &L, int m, int lane)
 {
-    constexpr int NZ = NX + NU;
+    const int ne = p.ne, ti_ = lane >> 3, tj_ = lane & 7;
+    for (int a = 0; a * 8 < m; a++)
+        for (int b = 0; b <= a; b++) {
+            const int i = a * 8 + ti_, j = b * 8 + tj_;
+            if (i < m && j <= i) {
+                const double wij = (double)p.W[(size_t)L.se_e[j] * ne + L.se_e[i]];
+                L.wss[i][j] = wij;
+                if (i == j) L.wdg[i] = wij;
+            }
+        }
+    CLF_SYNC();
+    bool pd = true;
+    for (int c = 0; c < m; c++) {
+        const double d = L.wss[c][c], wcc = L.wdg[c];
+        pd = pd && wcc > 0.0;
+        const double lcc = d > 1e-9 * wcc ? sqrt(d) : sqrt(fmax(d, 0.0) + 1e-6 * wcc);
+        const int i = c + lane;
+        if (i < m) L.wss[i][c] = i == c ? lcc : L.wss[i][c] / lcc;   // the diagonal read above precedes this write
+        CLF_SYNC();
+        const int r0 = c + 1;
+        for (int a = 0; r0 + a * 8 < m; a++)
+            for (int b = 0; b <= a; b++) {
+                const int ii = r0 + a * 8 + ti_, jj = r0 + b * 8 + tj_;
+                if (ii < m && jj <= ii) L.wss[ii][jj] = fma(-L.wss[ii][c], L.wss[jj][c], L.wss[ii][jj]);
+            }
+        CLF_SYNC();
+    }
+    return pd;
+}
+
+// y = L^-1 y (forward) or L^-T y (backward) for the factor in L.wss, the vector lane-distributed (lane
+// i holds y_i, i < m; the pivot of each column broadcast by readlane)
+template <class LdsT>
+__device__ double solve_lower(LdsT &L, int m, int lane, double y)
+{
+    const double dg = lane < m ? L.wss[lane][lane] : 1.0;
+    for (int c = 0; c < m; c++) {
+        const double yc = bcast(y, c) / bcast(dg, c);
+        if (lane == c) y = yc;
+        else if (lane > c && lane < m) y = fma(-L.wss[lane][c], yc, y);
+    }
+    return y;
+}
+template <class LdsT>
+__device__ double solve_upper(LdsT &L, int m, int lane, double y)
+{
+    const double dg = lane < m ? L.wss[lane][lane] : 1.0;
+    for (int c = m - 1; c >= 0; c--) {
+        const double xc = bcast(y, c) / bcast(dg, c);
+        if (lane == c) y = xc;
+        else if (lane < c) y = fma(-L.wss[c][lane], xc, y);
+    }
+    return y;
+}
+
+// sum_i W[e_i][e] c_i over the m elements in L.se_e with coefficients in cf (LDS), loads 8 at a time
+template <typename T, class LdsT>
+__device__ T w_combo(const ClFastParams<T> &p, LdsT &L, const double *cf, int m, int e, T acc)
+{
     const int ne = p.ne;
-    int se[EPL], sr[EPL], wsteps = 0;
-    T lb[EPL], ub[EPL], z0[EPL], z[EPL];
-    unsigned wf = 0;
+    for (int i0 = 0; i0 < m; i0 += 8) {
+        T w[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) w[q] = i0 + q < m ? p.W[(size_t)L.se_e[i0 + q] * ne + e] : T(0);
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (i0 + q < m) acc = fma(w[q], (T)cf[i0 + q], acc);
+    }
+    return acc;
+}
+
+// the set of flag bits wf in LDS in slot order (= element order): element, sign (-1 lower, 1 upper),
+// b - z_0, slot; pos[j] = the held slot's position in the set. Returns the set size (not written when
+// larger than WSM).
+template <typename T, int EPL, int WSM, class LdsT>
+__device__ int load_set(LdsT &L, const SlotView<EPL> sv, int lane, unsigned wf, const T (&z0)[EPL], int (&pos)[EPL])
+{
+    unsigned long long bal[EPL];
+    int m = 0;
 #pragma unroll
     for (int j = 0; j < EPL; j++) {
-        se[j] = sv.e(j);
-        sr[j] = se[j] >= 0 ? se[j] % NZ : -1;
-        lb[j] = (T)sv.lb(j);
-        ub[j] = (T)sv.ub(j);
-        z0[j] = (T)L.zb[j * 64 + lane];
-        wf |= bits_of(L.fl[j * 64 + lane]) << (2 * j);
+        bal[j] = __ballot(((wf >> (2 * j)) & 3u) != 0);
+        m += __popcll(bal[j]);
     }
-    auto done = [&](int m) {   // accepted: z to LDS; result word ok | m << 8 | steps << 16
+    int base = 0;
 #pragma unroll
-        for (int j = 0; j < EPL; j++) L.zb[j * 64 + lane] = (double)z[j];
-        CLF_SYNC();
-        return 1 | (m << 8) | (wsteps << 16);
+    for (int j = 0; j < EPL; j++) {
+        const unsigned f = (wf >> (2 * j)) & 3u;
+        pos[j] = -1;
+        if (f && m <= WSM) {
+            pos[j] = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal[j], 0u));
+            L.se_e[pos[j]] = sv.e(j);
+            L.se_s[pos[j]] = f == 1u ? -1 : 1;
+            L.se_t[pos[j]] = (double)((f == 1u ? (T)sv.lb(j) : (T)sv.ub(j)) - z0[j]);
+            L.gi_slot[pos[j]] = j * 64 + lane;
+        }
+        base += __popcll(bal[j]);
+    }
+    CLF_SYNC();
+    return m;
+}
+
+// Primal-dual active-set steps on W (oracle/c/riccati_ipm.c fast_finish): wf holds the set (warm
+// start, or empty: the first set from z_0's violations — the violated inputs and each state
+// component's most violated stage), z z_0 at the lane's slots. Each round solves W_SS nu = b_S - z_0,S: W_SS gathered
+// into LDS over 8 x 8 lane tiles, a right-looking Cholesky (column scaling by lanes, trailing update
+// over lane tiles), the two triangular solves with the right-hand side lane-distributed (lane i holds
+// row i, the pivot broadcast by readlane); then z = z_0 + W[:, S] nu at the lane's slots, accepted
+// when the held bounds are met (1e-9), no other bound is violated (1e-13) and every multiplier has its
+// sign (displacement nu_i W_ii to 1e-10 (1 + |b - z_0|)); otherwise removals and additions as the
+// finish's PDAS rule. An emptied set restarts from z_0 (one round). Result: ok | m << 8 | steps << 16
+// (z in L.zb, the set in L.se_*); not ok: a set larger than WSM, W_SS not positive definite, or no
+// acceptance in polish_steps rounds. z: z_0 in, the solution out (when accepted).
+template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
+__device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, T (&z)[EPL], unsigned wf,
+                          int rounds)
+{
+    constexpr int NZ = NX + NU;
+    static_assert(WSM <= 64, "active sets are lane-distributed");
+    const int ne = p.ne;
+    int wsteps = 0;
+    T z0[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; j++) z0[j] = z[j];
+    auto comp = [&](int j) {   // the slot's component r (or -1: padding slot)
+        const int e = sv.e(j);
+        return e >= 0 ? e % NZ : -1;
     };
+    auto done = [&](int m) { return 1 | (m << 8) | (wsteps << 16); };
     // per state component: the most violated slot (argmax by LDS atomics, ties to the first stage)
     auto argmax_states = [&](const double (&v)[EPL]) {
         if (lane < NZ) {
@@ -167,23 +295,32 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         }
         CLF_SYNC();
 #pragma unroll
-        for (int j = 0; j < EPL; j++)
-            if (sr[j] >= 0 && sr[j] < NX && v[j] > 0.0) atomicMax(&L.vmax[sr[j]], __builtin_bit_cast(unsigned long long, v[j]));
+        for (int j = 0; j < EPL; j++) {
+            const int r = comp(j);
+            if (r >= 0 && r < NX && v[j] > 0.0) atomicMax(&L.vmax[r], __builtin_bit_cast(unsigned long long, v[j]));
+        }
         CLF_SYNC();
-#pragma unroll
-        for (int j = 0; j < EPL; j++)
-            if (sr[j] >= 0 && sr[j] < NX && v[j] > 0.0 && __builtin_bit_cast(unsigned long long, v[j]) == L.vmax[sr[j]])
-                atomicMin(&L.vslot[sr[j]], se[j]);
-        CLF_SYNC();
-    };
-    for (int ws = 0, first = 1; ws < p.polish_steps; first = 0) {
-        unsigned long long bal[EPL];
-        int m = 0;
 #pragma unroll
         for (int j = 0; j < EPL; j++) {
-            bal[j] = __ballot(((wf >> (2 * j)) & 3u) != 0);
-            m += __popcll(bal[j]);
+            const int r = comp(j);
+            if (r >= 0 && r < NX && v[j] > 0.0 && __builtin_bit_cast(unsigned long long, v[j]) == L.vmax[r])
+                atomicMin(&L.vslot[r], sv.e(j));
         }
+        CLF_SYNC();
+    };
+    auto add_states = [&](const double (&v)[EPL], unsigned sgn, unsigned &w) {
+        argmax_states(v);
+#pragma unroll
+        for (int j = 0; j < EPL; j++) {
+            const int r = comp(j);
+            if (r >= 0 && r < NX && v[j] > 0.0 && L.vslot[r] == sv.e(j)) w |= ((sgn >> (2 * j)) & 3u) << (2 * j);
+        }
+        CLF_SYNC();
+    };
+    for (int ws = 0, first = 1; ws < rounds; first = 0) {
+        int m = 0;
+#pragma unroll
+        for (int j = 0; j < EPL; j++) m += __popcll(__ballot(((wf >> (2 * j)) & 3u) != 0));
         if (m == 0) {
             // no bound held: the iterate is z_0 — accepted if feasible, else the set from its violations
             if (!first) ws++;
@@ -192,93 +329,39 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
             unsigned sgn = 0;
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
-                const T tl = T(1e-13) * (T(1) + fabs(lb[j])), tu = T(1e-13) * (T(1) + fabs(ub[j]));
-                const bool lo = has_b(lb[j]) && z0[j] < lb[j] - tl, hi = has_b(ub[j]) && z0[j] > ub[j] + tu;
-                bad |= lo || hi || (se[j] >= 0 && !isfinite(z0[j]));
-                v[j] = lo ? (double)(lb[j] - z0[j]) : (hi ? (double)(z0[j] - ub[j]) : 0.0);
+                const bool lo = z0[j] < (T)sv.lo(j), hi = z0[j] > (T)sv.hi(j);
+                bad |= lo || hi || !isfinite(z0[j]);
+                v[j] = lo ? (double)((T)sv.lb(j) - z0[j]) : (hi ? (double)(z0[j] - (T)sv.ub(j)) : 0.0);
                 sgn |= (lo ? 1u : (hi ? 2u : 0u)) << (2 * j);
-                if (sr[j] >= NX && (lo || hi)) wf |= (lo ? 1u : 2u) << (2 * j);   // inputs join at once
+                if (comp(j) >= NX && (lo || hi)) wf |= (lo ? 1u : 2u) << (2 * j);   // inputs join at once
             }
             if (!__any(bad)) {
 #pragma unroll
-                for (int j = 0; j < EPL; j++) z[j] = z0[j];
+                for (int j = 0; j < EPL; j++) z[j] = z0[j];   // (a restart: z holds the last round's trial)
                 return done(0);
             }
-            argmax_states(v);
-#pragma unroll
-            for (int j = 0; j < EPL; j++)
-                if (sr[j] >= 0 && sr[j] < NX && v[j] > 0.0 && L.vslot[sr[j]] == se[j]) wf |= ((sgn >> (2 * j)) & 3u) << (2 * j);
-            CLF_SYNC();
+            add_states(v, sgn, wf);
             continue;
         }
-        if (m > WSMAX) return wsteps << 16;
-        // the set in LDS: element, sign, b - z_0
-        int base = 0;
-#pragma unroll
-        for (int j = 0; j < EPL; j++) {
-            const unsigned f = (wf >> (2 * j)) & 3u;
-            if (f) {
-                const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal[j], 0u));
-                L.se_e[pos] = se[j];
-                L.se_s[pos] = f == 1u ? -1 : 1;
-                L.se_t[pos] = (double)((f == 1u ? lb[j] : ub[j]) - z0[j]);
-            }
-            base += __popcll(bal[j]);
+        if (m > WSM) break;
+        int pos[EPL];
+        load_set<T, EPL, WSM>(L, sv, lane, wf, z0, pos);
+        if (!factor_set(p, L, m, lane)) break;
+        // nu = L^-T L^-1 (b - z_0)_S, lane i holding row i
+        const double y = solve_upper(L, m, lane, solve_lower(L, m, lane, lane < m ? L.se_t[lane] : 0.0));
+        // multiplier signs as displacements nu_i W_ii (lower: >= 0, upper: <= 0) to 1e-10 (1 + |b - z_0|)
+        bool rmv = false;
+        if (lane < m) {
+            L.se_nu[lane] = y;
+            const double tol = 1e-10 * (1.0 + fabs(L.se_t[lane])), dsp = y * L.wdg[lane];
+            const int sg = L.se_s[lane];
+            rmv = (sg < 0 && dsp < -tol) || (sg > 0 && dsp > tol) || !isfinite(y);
         }
+        const unsigned long long remm = __ballot(rmv);
         CLF_SYNC();
-        // W_SS in LDS, entry (i, j) on lane 8 i + j; right-looking Cholesky (the lower triangle), then
-        // the triangular solves for nu on every lane from LDS (wave-uniform reads)
-        {
-            const int i = lane >> 3, j = lane & 7;
-            const bool in = i < m && j < m && j <= i;
-            const double wij = in ? (double)p.W[(size_t)L.se_e[j] * ne + L.se_e[i]] : 0.0;
-            L.wss[i][j] = wij;
-            if (in && i == j) L.wdg[i] = wij;
-        }
-        CLF_SYNC();
-        bool pd = true;
-        for (int c = 0; c < m; c++) {
-            const double d = L.wss[c][c];
-            pd = pd && d > 0.0;
-            const double lcc = d > 0.0 ? sqrt(d) : 1.0;
-            const int i = lane >> 3, j = lane & 7;
-            CLF_SYNC();
-            if (j == c && i >= c && i < m) L.wss[i][c] = i == c ? lcc : L.wss[i][c] / lcc;
-            CLF_SYNC();
-            if (j > c && j <= i && i < m) L.wss[i][j] -= L.wss[i][c] * L.wss[j][c];
-            CLF_SYNC();
-        }
-        if (!pd) return wsteps << 16;
-        // nu = L^-T L^-1 (b - z_0)_S into L.se_nu (lane 0 writes, every lane reads; m <= WSMAX rows)
-#pragma unroll 1
-        for (int i = 0; i < m; i++) {
-            double s_ = L.se_t[i];
-#pragma unroll 1
-            for (int l = 0; l < i; l++) s_ = fma(-L.wss[i][l], L.se_nu[l], s_);
-            CLF_SYNC();
-            if (lane == 0) L.se_nu[i] = s_ / L.wss[i][i];
-            CLF_SYNC();
-        }
-#pragma unroll 1
-        for (int i = m - 1; i >= 0; i--) {
-            double s_ = L.se_nu[i];
-#pragma unroll 1
-            for (int l = i + 1; l < m; l++) s_ = fma(-L.wss[l][i], L.se_nu[l], s_);
-            CLF_SYNC();
-            if (lane == 0) L.se_nu[i] = s_ / L.wss[i][i];
-            CLF_SYNC();
-        }
         const int round = ws++;
         wsteps++;
-        // multiplier signs as displacements nu_i W_ii (lower: >= 0, upper: <= 0) to 1e-10 (1 + |b - z_0|)
-        unsigned remm = 0;
-#pragma unroll 1
-        for (int i = 0; i < m; i++) {
-            const double nui = L.se_nu[i], tol = 1e-10 * (1.0 + fabs(L.se_t[i])), dsp = nui * L.wdg[i];
-            const int sg = L.se_s[i];
-            if ((sg < 0 && dsp < -tol) || (sg > 0 && dsp > tol) || !isfinite(nui)) remm |= 1u << i;
-        }
-        const int nrem = __popc(remm);
+        const int nrem = __popcll(remm);
         const bool addok = round == 0 || nrem == 0;
         bool bad = nrem > 0;
         double v[EPL];
@@ -286,177 +369,321 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
 #pragma unroll
         for (int j = 0; j < EPL; j++) {
             v[j] = 0.0;
-            if (se[j] < 0) {
+            const int e = sv.e(j);
+            if (e < 0) {
                 z[j] = z0[j];
                 continue;
             }
-            T zz = z0[j];
-#pragma unroll 1
-            for (int i = 0; i < m; i++) zz = fma(p.W[(size_t)L.se_e[i] * ne + se[j]], (T)L.se_nu[i], zz);
+            T zz = w_combo(p, L, L.se_nu, m, e, z0[j]);
             const unsigned f = (wf >> (2 * j)) & 3u;
             if (f) {
-                const T bb = f == 1u ? lb[j] : ub[j];
+                const T bb = f == 1u ? (T)sv.lb(j) : (T)sv.ub(j);
                 bad |= !(fabs(zz - bb) <= T(1e-9) * (T(1) + fabs(bb)));
                 zz = bb;
-#pragma unroll 1
-                for (int i = 0; i < m; i++)
-                    if (((remm >> i) & 1u) && L.se_e[i] == se[j]) nwf &= ~(3u << (2 * j));
+                if ((remm >> pos[j]) & 1ull) nwf &= ~(3u << (2 * j));
             } else {
-                const T tl = T(1e-13) * (T(1) + fabs(lb[j])), tu = T(1e-13) * (T(1) + fabs(ub[j]));
-                const bool lo = has_b(lb[j]) && zz < lb[j] - tl, hi = has_b(ub[j]) && zz > ub[j] + tu;
+                const bool lo = zz < (T)sv.lo(j), hi = zz > (T)sv.hi(j);
                 bad |= lo || hi || !isfinite(zz);
-                v[j] = lo ? (double)(lb[j] - zz) : (hi ? (double)(zz - ub[j]) : 0.0);
+                v[j] = lo ? (double)((T)sv.lb(j) - zz) : (hi ? (double)(zz - (T)sv.ub(j)) : 0.0);
                 sgn |= (lo ? 1u : (hi ? 2u : 0u)) << (2 * j);
-                if (sr[j] >= NX && (lo || hi)) nwf |= (lo ? 1u : 2u) << (2 * j);   // inputs join at once
+                if (e % NZ >= NX && (lo || hi)) nwf |= (lo ? 1u : 2u) << (2 * j);   // inputs join at once
             }
             z[j] = zz;
         }
         if (!__any(bad)) return done(m);
-        if (addok) {
-            argmax_states(v);
-#pragma unroll
-            for (int j = 0; j < EPL; j++)
-                if (sr[j] >= 0 && sr[j] < NX && v[j] > 0.0 && L.vslot[sr[j]] == se[j]) nwf |= ((sgn >> (2 * j)) & 3u) << (2 * j);
-        }
+        if (addok) add_states(v, sgn, nwf);
         wf = nwf;
         CLF_SYNC();
     }
+#pragma unroll
+    for (int j = 0; j < EPL; j++) z[j] = z0[j];   // not accepted: z_0 back to the caller
     return wsteps << 16;
+}
+
+// The fast path's fallback when the PDAS rounds do not settle — degenerate sets, cycling
+// (oracle/c/riccati_ipm.c gi_set): the Goldfarb-Idnani dual active-set method on W, which converges for
+// any strictly convex QP. Bounds are constraints n_i^T z >= b_i, n_i = +e (lower) / -e (upper), sign
+// sg_i. From z = z_0 and an empty set the most violated inactive bound p enters (ties: the first slot):
+// l' = L^-1 W[S][p] (the unsigned factor of W_SS in L.wss), theta = W_pp - |l'|^2, the multipliers'
+// rate r_i = sg_p sg_i (L^-T l')_i, dz = sg_p (W[:, p] - W[:, S] L^-T l'); the full step
+// t2 = -sg_p (z_p - b_p) / theta makes p active (the factor grows by the row l', sqrt(theta)), the
+// partial step t1 = min u_i / r_i (r_i > 0) drops the bound whose multiplier reaches zero first
+// (refactored); z += t dz, u -= t r, u_p += t. theta ~ 0 (p dependent on the set) only drops; no
+// blocking bound then: infeasible. The set lives in L.se_e / L.se_s (+ slot), the multipliers on lanes
+// i < m. true: no inactive bound violated beyond 1e-13, the set in wf (per-lane flag bits), for
+// wsteps_run to solve exactly and check. z_0 is not modified.
+template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
+__device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, const T (&z0)[EPL],
+                       unsigned w0, unsigned &wf, int &iters)
+{
+    const int ne = p.ne;
+    T z[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; j++) z[j] = z0[j];
+    int m = 0, ps = -1, sp = 0, ep = 0;   // the entering bound: slot, sign (+1 lower, -1 upper), element
+    double u = 0.0, up = 0.0;             // lane i < m: the multiplier u_i; up: the entering bound's
+    // warm start: the set the PDAS rounds started from (w0), made dual feasible — its equality-constrained
+    // solution nu = W_SS^-1 (b - z_0)_S, u_i = sg_i nu_i; the negative ones leave, re-solved until none
+    // is left — and z = z_0 + W[:, S] nu
+    {
+        int pos[EPL];
+        m = load_set<T, EPL, WSM>(L, sv, lane, w0, z0, pos);
+        wf = m <= WSM ? w0 : 0u;
+        if (m > WSM) m = 0;
+        double nu = 0.0;
+        while (m > 0) {
+            factor_set(p, L, m, lane);
+            nu = solve_upper(L, m, lane, solve_lower(L, m, lane, lane < m ? L.se_t[lane] : 0.0));
+            u = lane < m ? (double)(-L.se_s[lane]) * nu : 0.0;
+            const bool keep = lane < m && !(u < 0.0);
+            const unsigned long long km = __ballot(keep);
+            if (__popcll(km) == m) break;
+            // compact: the kept entries to their new positions, the dropped slots' flags cleared
+            const int to = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
+            int e_ = 0, s_ = 0, sl_ = 0;
+            double t_ = 0.0;
+            if (lane < m) {
+                e_ = L.se_e[lane];
+                s_ = L.se_s[lane];
+                sl_ = L.gi_slot[lane];
+                t_ = L.se_t[lane];
+            }
+            CLF_SYNC();
+            if (keep) {
+                L.se_e[to] = e_;
+                L.se_s[to] = s_;
+                L.gi_slot[to] = sl_;
+                L.se_t[to] = t_;
+            }
+            const unsigned long long dm = __ballot(lane < m && !keep);
+            for (unsigned long long d_ = dm; d_; d_ &= d_ - 1) {
+                const int sk = __shfl(sl_, (int)__builtin_ctzll(d_));
+                if (lane == (sk & 63)) wf &= ~(3u << (2 * (sk >> 6)));
+            }
+            m = __popcll(km);
+            CLF_SYNC();
+        }
+        if (m > 0) {
+            if (lane < m) L.se_nu[lane] = nu;
+            CLF_SYNC();
+#pragma unroll
+            for (int j = 0; j < EPL; j++) {
+                const int e = sv.e(j);
+                if (e >= 0) z[j] = w_combo(p, L, L.se_nu, m, e, z[j]);
+            }
+            CLF_SYNC();
+        }
+    }
+    const int cap = 3 * WSM + 16;
+    int it = 0;
+    for (; it < cap; it++) {
+        if (ps < 0) {
+            double v[EPL], vm = 0.0;
+#pragma unroll
+            for (int j = 0; j < EPL; j++) {
+                const bool held = ((wf >> (2 * j)) & 3u) != 0;
+                const bool lo = !held && z[j] < (T)sv.lo(j), hi = !held && z[j] > (T)sv.hi(j);
+                v[j] = lo ? (double)((T)sv.lb(j) - z[j]) : (hi ? (double)(z[j] - (T)sv.ub(j)) : 0.0);
+                vm = fmax(vm, v[j]);
+            }
+            vm = wave_max(vm);
+            if (!(vm > 0.0)) break;
+#pragma unroll
+            for (int j = EPL - 1; j >= 0; j--) {
+                const unsigned long long bal = __ballot(v[j] == vm);
+                if (bal) ps = j * 64 + (int)__builtin_ctzll(bal);
+            }
+            ep = sv.e_[ps];
+            up = 0.0;
+        }
+        double zc = 0.0;
+#pragma unroll
+        for (int j = 0; j < EPL; j++)
+            if (j == (ps >> 6)) zc = (double)z[j];
+        const double zp = bcast(zc, ps & 63);
+        if (up == 0.0) sp = zp < sv.lo_[ps] ? 1 : -1;   // entering: the violated side
+        const double bp = sp > 0 ? sv.lb_[ps] : sv.ub_[ps];
+        const double wpp = (double)p.W[(size_t)ep * ne + ep];
+        const double l_ = solve_lower(L, m, lane, lane < m ? (double)p.W[(size_t)L.se_e[lane] * ne + ep] : 0.0);
+        const double theta = wpp - wave_sum(lane < m ? l_ * l_ : 0.0);
+        const double r_ = solve_upper(L, m, lane, l_);
+        const double ri = lane < m ? (double)sp * (double)(-L.se_s[lane]) * r_ : 0.0;
+        const double q = (lane < m && ri > 0.0) ? u / ri : INFINITY;
+        const double t1 = wave_min(q);
+        const double t2 = theta > 1e-12 * wpp ? -(double)sp * (zp - bp) / theta : INFINITY;
+        if (t1 == INFINITY && t2 == INFINITY) break;   // infeasible
+        const bool full = t2 <= t1;
+        const double t = full ? t2 : t1;
+        if (t2 < INFINITY) {
+            if (lane < m) L.se_nu[lane] = r_;
+            CLF_SYNC();
+#pragma unroll
+            for (int j = 0; j < EPL; j++) {
+                const int e = sv.e(j);
+                if (e >= 0) z[j] = fma((T)t, (T)sp * (p.W[(size_t)ep * ne + e] - w_combo(p, L, L.se_nu, m, e, T(0))), z[j]);
+            }
+            CLF_SYNC();
+        }
+        if (lane < m) u = fma(-t, ri, u);
+        up += t;
+        if (full) {
+            if (m >= WSM) break;
+            if (lane < m) L.wss[m][lane] = l_;
+            if (lane == m) {
+                L.wss[m][m] = sqrt(theta);
+                L.se_e[m] = ep;
+                L.se_s[m] = sp > 0 ? -1 : 1;
+                L.gi_slot[m] = ps;
+                u = up;
+            }
+            if (lane == (ps & 63)) wf |= (sp > 0 ? 1u : 2u) << (2 * (ps >> 6));
+            m++;
+            ps = -1;
+            CLF_SYNC();
+        } else {
+            const unsigned long long kb = __ballot(lane < m && ri > 0.0 && q == t1);
+            const int kk = (int)__builtin_ctzll(kb);
+            const int sk = L.gi_slot[kk];
+            if (lane == (sk & 63)) wf &= ~(3u << (2 * (sk >> 6)));
+            const int src = lane >= kk ? lane + 1 : lane;
+            int e_ = 0, s_ = 0, sl_ = 0;
+            if (lane + 1 < m) {
+                e_ = L.se_e[src];
+                s_ = L.se_s[src];
+                sl_ = L.gi_slot[src];
+            }
+            u = __shfl(u, src & 63);
+            CLF_SYNC();
+            if (lane + 1 < m) {
+                L.se_e[lane] = e_;
+                L.se_s[lane] = s_;
+                L.gi_slot[lane] = sl_;
+            }
+            m--;
+            CLF_SYNC();
+            factor_set(p, L, m, lane);
+        }
+    }
+    iters = it;
+    return ps < 0 && it < cap;
 }
 
 // interval certificate (oracle/c/riccati_ipm.c infeasible_stage): lane i < NX carries state i of
 // X_k in midpoint / radius form, X_{k+1} = hull([A B] X_k x U + c) meets the state box of stage
-// k + 1; an empty intersection proves the QP infeasible
+// k + 1; an empty intersection proves the QP infeasible. x_0 in L.xs; [A B], c from the workgroup's
+// LDS copy (the model's own values: zero outside its structure); the stage exchange by readlane.
 template <typename T, int NX, int NU, class LdsT>
-__device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, int lane)
+__device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, const double *abl, const double *cl, int lane)
 {
-    // x_0 in L.xs (the caller's copy)
     constexpr int NZ = NX + NU;
-    T m = lane < NX ? (T)L.xs[lane] : T(0), r = 0;
-    T mu[NU], ru[NU];
-#pragma unroll
-    for (int j = 0; j < NU; j++) {
-        const T l = p.lbnd[NX + j], h = p.ubnd[NX + j];
-        const bool bb = has_b(l) && has_b(h);
-        mu[j] = bb ? T(0.5) * (l + h) : T(0);
-        ru[j] = bb ? T(0.5) * (h - l) : T(INFINITY);
-    }
-    bool infeas = false;
     const int i = lane < NX ? lane : 0;
+    double m = lane < NX ? L.xs[lane] : 0.0, r = 0.0;
+    double a[NX];
+#pragma unroll
+    for (int j = 0; j < NX; j++) a[j] = abl[i * NZ + j];
+    bool infeas = false;
     for (int k = 0; k < p.N; k++) {
-        if (lane < NX) {
-            L.cm[lane] = (double)m;
-            L.cr[lane] = (double)r;
-        }
-        CLF_SYNC();
-        T s = p.c[i], tr = 0;
+        double s = cl[i], tr = 0.0;
 #pragma unroll
         for (int j = 0; j < NX; j++) {
-            const T a = p.AB[i * NZ + j];
-            s = fma(a, (T)L.cm[j], s);
-            if (a != T(0)) tr = fma(fabs(a), (T)L.cr[j], tr);
+            const double mj = bcast(m, j), rj = bcast(r, j);
+            s = fma(a[j], mj, s);
+            if (a[j] != 0.0) tr = fma(fabs(a[j]), rj, tr);
         }
 #pragma unroll
         for (int j = 0; j < NU; j++) {
-            const T b = p.AB[i * NZ + NX + j];
-            s = fma(b, mu[j], s);
-            if (b != T(0)) tr = fma(fabs(b), ru[j], tr);
+            const double b = abl[i * NZ + NX + j], l = p.lbnd[NX + j], h = p.ubnd[NX + j];
+            const bool bb = has_b(l) && has_b(h);
+            s = fma(b, bb ? 0.5 * (l + h) : 0.0, s);
+            if (b != 0.0) tr = fma(fabs(b), bb ? 0.5 * (h - l) : (double)INFINITY, tr);
         }
-        CLF_SYNC();
         const int ty = k + 1 == p.N ? 2 : 1;
-        const T lb = p.lbnd[ty * NZ + i], ub = p.ubnd[ty * NZ + i];
-        T lo = s - tr, hi = s + tr;
+        const double lb = p.lbnd[ty * NZ + i], ub = p.ubnd[ty * NZ + i];
+        double lo = s - tr, hi = s + tr;
         if (has_b(lb) && lb > lo) lo = lb;
         if (has_b(ub) && ub < hi) hi = ub;
-        infeas |= lane < NX && lo > hi + T(1e-9) * (T(1) + fabs(hi));
+        infeas |= lane < NX && lo > hi + 1e-9 * (1.0 + fabs(hi));
         const bool fin = isfinite(lo) && isfinite(hi);
-        m = fin ? T(0.5) * (lo + hi) : s;
-        r = fin ? T(0.5) * (hi - lo) : tr;
+        m = fin ? 0.5 * (lo + hi) : s;
+        r = fin ? 0.5 * (hi - lo) : tr;
     }
     return __any(infeas);
 }
 
-// plant step + noise on the wave-uniform state (nmpc_cl_device.h cl_advance_group's arithmetic):
-// plant 0 the controller's own discrete model [A B] (structure SP), 1 / 2 the Crazyflie plant with
-// the force / jerk converter
+// plant step + noise, lane-distributed: lane i < NX returns x_i after the step (nmpc_cl_device.h
+// cl_advance_group's arithmetic). Plant 0: the controller's own discrete model, row i of [A B] from the
+// workgroup's LDS copy (the structure's nonzeros, in column order), x from L.xs, u0 wave-uniform;
+// plants 1 / 2: the Crazyflie plant with the force / jerk converter, evaluated wave-uniformly.
 template <typename T, int NX, int NU, class SP>
-__device__ __forceinline__ void plant_step(const ClFastParams<T> &p, const double *abl, const double *cl, T (&x)[NX],
-                                           const double (&u0)[NU], double w)
+__device__ __forceinline__ double plant_step(const ClFastParams<T> &p, const double *abl, const double *cl,
+                                             const double *xs, double xl, const double (&u0)[NU], double w, int lane)
 {
     constexpr int NZ = NX + NU;
     if (p.plant == 0) {
-        // [A B] and c from the workgroup's LDS copy (wave-uniform reads; kept out of SGPRs)
-        T xn[NX];
+        const int i = lane < NX ? lane : 0;
+        double s = cl[i];
 #pragma unroll
-        for (int i = 0; i < NX; i++) {
-            double s = cl[i];
+        for (int j = 0; j < NX; j++) s = fma(abl[i * NZ + j], xs[j], s);
 #pragma unroll
-            for (int j = 0; j < NX; j++)
-                if (SP::ab(i, j)) s += abl[i * NZ + j] * (double)x[j];
-#pragma unroll
-            for (int j = 0; j < NU; j++)
-                if (SP::ab(i, NX + j)) s += abl[i * NZ + NX + j] * u0[j];
-            xn[i] = (T)(s + (i < p.noise_dims ? w : 0.0));
-        }
-#pragma unroll
-        for (int i = 0; i < NX; i++) x[i] = xn[i];
+        for (int j = 0; j < NU; j++) s = fma(abl[i * NZ + NX + j], u0[j], s);
+        return lane < NX ? s + (lane < p.noise_dims ? w : 0.0) : 0.0;
     } else if constexpr ((NX == 4 && NU == 2) || (NX == 6 && NU == 2)) {
-        double xs[4], f[4];
+        double x4[4], f[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) xs[i] = (double)x[i];
+        for (int i = 0; i < 4; i++) x4[i] = xs[i];
         const double inv_m = 1.0 / p.mass;
+        double xn = xl;
         if (NX == 4) {
             const double Fx = u0[0], Fz = u0[1];
             const double th = atan2(Fx, Fz), Fd = sqrt(Fx * Fx + Fz * Fz);
             const double s_ = sin(th), c_ = cos(th), h = p.dt;
             double k1[4], k2[4], k3[4], k4[4], tt[4];
-            crazyflie_rhs(xs, s_, c_, Fd, inv_m, p.g, k1);
-            for (int i = 0; i < 4; i++) tt[i] = xs[i] + 0.5 * h * k1[i];
+            crazyflie_rhs(x4, s_, c_, Fd, inv_m, p.g, k1);
+            for (int i = 0; i < 4; i++) tt[i] = x4[i] + 0.5 * h * k1[i];
             crazyflie_rhs(tt, s_, c_, Fd, inv_m, p.g, k2);
-            for (int i = 0; i < 4; i++) tt[i] = xs[i] + 0.5 * h * k2[i];
+            for (int i = 0; i < 4; i++) tt[i] = x4[i] + 0.5 * h * k2[i];
             crazyflie_rhs(tt, s_, c_, Fd, inv_m, p.g, k3);
-            for (int i = 0; i < 4; i++) tt[i] = xs[i] + h * k3[i];
+            for (int i = 0; i < 4; i++) tt[i] = x4[i] + h * k3[i];
             crazyflie_rhs(tt, s_, c_, Fd, inv_m, p.g, k4);
-            for (int i = 0; i < 4; i++) xs[i] += h / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
-            for (int i = 0; i < 4; i++) x[i] = (T)(xs[i] + w);
+            for (int i = 0; i < 4; i++) x4[i] += h / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (lane == i) xn = x4[i] + w;
         } else {
-            double a0 = (double)x[4 % NX], a1 = (double)x[5 % NX];
+            double a0 = xs[4 % NX], a1 = xs[5 % NX];
             const double h0 = u0[0], h1 = u0[1];
             for (int j = 0; j < p.substeps; j++) {
                 a0 = a0 + h0 * p.dt_conv;
                 a1 = a1 + h1 * p.dt_conv;
                 const double Fx = p.mass * a0, Fz = p.mass * a1;
                 const double th = atan2(Fx, Fz), Fd = sqrt(Fx * Fx + Fz * Fz);
-                crazyflie_rhs(xs, sin(th), cos(th), Fd, inv_m, p.g, f);
-                for (int i = 0; i < 4; i++) xs[i] += p.dt_conv * f[i];
+                crazyflie_rhs(x4, sin(th), cos(th), Fd, inv_m, p.g, f);
+                for (int i = 0; i < 4; i++) x4[i] += p.dt_conv * f[i];
             }
-            for (int i = 0; i < 4; i++) x[i] = (T)(xs[i] + w);
-            x[4 % NX] = (T)a0;
-            x[5 % NX] = (T)a1;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (lane == i) xn = x4[i] + w;
+            if (lane == 4 % NX) xn = a0;
+            if (lane == 5 % NX) xn = a1;
         }
+        return xn;
     }
+    return xl;
 }
 
 // trajectory outputs of an instance's last solve (lanes over the (N+1) nz elements): z_0 from the
 // full tables plus the accepted active-set step (LDS), held bounds exact, bounded elements clamped;
-// a failed last step (status 4) outputs the initial point
+// a failed last step (status 4) outputs the initial point. x_0 in L.xs.
 template <typename T, int NX, int NU, int EPL, class LdsT>
 __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int inst, int t, int status, int m)
 {
-    // x_0 in L.xs (the caller's copy)
     constexpr int NZ = NX + NU;
     const int N = p.N, ne = p.ne;
-    T x0[NX];
-#pragma unroll
-    for (int c = 0; c < NX; c++) x0[c] = (T)L.xs[c];
 #pragma unroll 1
     for (int e = lane; e < ne; e += 64) {
         const int k = e / NZ, r = e % NZ;
         if (k == N && r >= NX) continue;
-        T x0r = 0;
-#pragma unroll
-        for (int c = 0; c < NX; c++)
-            if (c == r) x0r = x0[c];
+        const T x0r = r < NX ? (T)L.xs[r] : T(0);
         const int ty = k == 0 ? 0 : (k == N ? 2 : 1);
         const T lb = p.lbnd[ty * NZ + r], ub = p.ubnd[ty * NZ + r];
         T z;
@@ -467,12 +694,12 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int i
         } else {
             const T *tr = p.txfull + (size_t)e * NX;
             T s0 = p.vfull[(size_t)t * ne + e], s1 = 0;
-#pragma unroll
+#pragma unroll 1
             for (int c = 0; c + 1 < NX; c += 2) {
-                s0 = fma(tr[c], x0[c], s0);
-                s1 = fma(tr[c + 1], x0[c + 1], s1);
+                s0 = fma(tr[c], (T)L.xs[c], s0);
+                s1 = fma(tr[c + 1], (T)L.xs[c + 1], s1);
             }
-            if (NX % 2) s0 = fma(tr[NX - 1], x0[NX - 1], s0);
+            if (NX % 2) s0 = fma(tr[NX - 1], (T)L.xs[NX - 1], s0);
             z = s0 + s1;
             int held = 0;
             for (int i = 0; i < m; i++) {
@@ -488,18 +715,19 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int i
     }
 }
 
-template <typename T, int NX, int NU, int EPL, class SP>
-__global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
+// WPB wavefronts per workgroup (the slot tables in LDS are shared by them), MW the occupancy target
+// (waves per SIMD; 0: none)
+template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0 ? MW : 1, 8))) void cl_fast_kernel(ClFastParams<T> p)
 {
     constexpr int NZ = NX + NU, NSLOT = EPL * 64;
-    __shared__ Lds<NSLOT, NZ> lds_all[WPB];
-    // workgroup constants: [A B], c (plant), the slots' bounds, elements and warm-start sources
-    __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT];
+    static_assert(NX < 32 && NZ <= 64, "lane-distributed state");
+    __shared__ Lds<NSLOT, NZ, WSM> lds_all[WPB];
+    // workgroup constants: [A B], c (plant), the slots' bounds, thresholds, elements and warm-start sources
+    __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT], slo[NSLOT], shi[NSLOT], sol[NSLOT], sou[NSLOT];
     __shared__ int sse[NSLOT], ssrc[NSLOT];
-    // the slots' T_x rows, component-major (txl[c][s]: lanes read consecutive words, no bank conflicts),
-    // shared by the workgroup's wavefronts — registers stay free for occupancy
-    // pairs of components per 16-byte word (txl[c / 2][s] = (T_x(s, c), T_x(s, c + 1))): one ds_read_b128
-    // per slot and pair
+    // the slots' T_x rows, pairs of components per 16-byte word (txl[c][s] = (T_x(s, 2c), T_x(s, 2c + 1))):
+    // lanes read consecutive words, one ds_read_b128 per slot and pair
     constexpr int NXP = (NX + 1) / 2;
     __shared__ double2 txl[NXP][NSLOT];
     for (int e = threadIdx.x; e < NXP * NSLOT; e += 64 * WPB) {
@@ -508,29 +736,39 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
         txl[c][s_] = make_double2(v ? (double)p.s_tx[(size_t)s_ * NX + 2 * c] : 0.0,
                                   v && 2 * c + 1 < NX ? (double)p.s_tx[(size_t)s_ * NX + 2 * c + 1] : 0.0);
     }
-    for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) abl[e] = (double)p.AB[e];
+    for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) {
+        const int i = e / NZ, j = e % NZ;
+        abl[e] = SP::ab(i, j) ? (double)p.AB[e] : 0.0;   // the plant rows: the structure's nonzeros
+    }
     for (int e = threadIdx.x; e < NX; e += 64 * WPB) cl[e] = (double)p.c[e];
     for (int s = threadIdx.x; s < NSLOT; s += 64 * WPB) {
         const bool v = s < p.nslot;
-        slb[s] = v ? (double)p.s_lb[s] : -1e30;
-        sub[s] = v ? (double)p.s_ub[s] : 1e30;
+        const double l = v ? (double)p.s_lb[s] : -1e30, u = v ? (double)p.s_ub[s] : 1e30;
+        const bool hl = has_b(l), hu = has_b(u);
+        slb[s] = l;
+        sub[s] = u;
+        slo[s] = hl ? l - 1e-13 * (1.0 + fabs(l)) : -DBL_MAX;
+        shi[s] = hu ? u + 1e-13 * (1.0 + fabs(u)) : DBL_MAX;
+        sol[s] = hl ? l + 1e-7 * (1.0 + fabs(l)) : -DBL_MAX;
+        sou[s] = hu ? u - 1e-7 * (1.0 + fabs(u)) : DBL_MAX;
         sse[s] = v ? p.s_e[s] : -1;
         ssrc[s] = v ? p.s_src[s] : -1;
     }
-    __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    Lds<NSLOT, NZ> &L = lds_all[wave];
+    Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
+    if (lane < 32) L.xs[lane] = 0.0;
+    __syncthreads();
     const int gw = blockIdx.x * WPB + wave, nw = gridDim.x * WPB;
-    const SlotView<EPL> sv{slb, sub, sse, ssrc, lane};
+    const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
 
     const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
+    const double wl = lane < p.ncl ? (double)p.wcl[lane] : 0.0;   // this lane's cost weight
 
     for (int inst = gw; inst < p.B; inst += nw) {
         int step = p.istep[inst];
         if (step >= p.target) continue;
-        T x[NX];
-#pragma unroll
-        for (int c = 0; c < NX; c++) x[c] = p.state[(size_t)inst * NX + c];
+        // lane-distributed state: lane i < NX holds x_i
+        double xl = lane < NX ? (double)p.state[(size_t)inst * NX + lane] : 0.0;
         // active flags of the last solution by slot: bit 2j lower, 2j+1 upper
         unsigned fl = 0;
         if (step > 0) {
@@ -542,12 +780,12 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
             }
         }
         int t = (int)(((long long)p.offset[inst] + step) % p.period);
-        double cost = 0.0, aed = 0.0, nfail = 0.0, nst = 0.0;
-        int last_status = 0, last_iters = 0;
+        double cost = 0.0, aed = 0.0;   // this lane's terms (component lane), summed over the wave at the end
+        int nfail = 0, nst = 0;
+        int last_status = step > 0 ? p.status[inst] : 0, last_iters = 0;
         bool parked = false;
-        // v_t at the slots one step ahead (the step's first dependency); the reference row and the noise
-        // draw are issued at the top of the step and consumed after the solve
-        constexpr int NR = NX < 8 ? NX : 8;   // reference components of cost / AED (nmpc_closed_loop_init: <= 8)
+        // v_t at the slots one step ahead (the step's first dependency); the reference component and the
+        // noise draw are issued at the top of the step and consumed after the solve
         T vtn[EPL];
         auto fetch_v = [&](int tt) {
             const T *vp = p.vb + (size_t)tt * NSLOT;
@@ -556,17 +794,15 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
         };
         fetch_v(t);
         for (; step < p.target; step++) {
-            T vt[EPL], xr[NR];
+            const long long clk0 = p.iter_log ? clock64() : 0;
+            T vt[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) vt[j] = vtn[j];
             const int tn = t + 1 == p.period ? 0 : t + 1;
             if (step + 1 < p.target) fetch_v(tn);
-            {
-                const T *xp = p.table + (size_t)t * p.table_cols;
-#pragma unroll
-                for (int i = 0; i < NR; i++) xr[i] = i < nref ? xp[i] : T(0);
-            }
+            const double xr = lane < nref ? (double)p.table[(size_t)t * p.table_cols + lane] : 0.0;
             const double w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
+            if (lane < NX) L.xs[lane] = xl;
             // ---- warm start: the last solution's flags shifted by one stage (slot source)
             unsigned wf = 0;
             if (__any(fl != 0)) {
@@ -578,29 +814,23 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
                     const int sr_ = sv.src(j);
                     wf |= bits_of(sr_ >= 0 ? L.fl[sr_] : (signed char)0) << (2 * j);
                 }
-                CLF_SYNC();
             }
-            // ---- explicit unconstrained solution at the lane's slots
+            CLF_SYNC();
+            // ---- explicit unconstrained solution at the lane's slots (x pairs broadcast from LDS)
             T z[EPL], z1[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 z[j] = vt[j];
                 z1[j] = T(0);
             }
-            // x in LDS for the rolled pair loop (its component pair is wave-uniform)
-#pragma unroll
-            for (int c = 0; c < NX; c++)
-                if (lane == c) L.xs[c] = (double)x[c];
-            if (lane == NX) L.xs[NX] = 0.0;
-            CLF_SYNC();
 #pragma unroll 1
             for (int c = 0; c < NXP; c++) {
-                const double xa = L.xs[2 * c], xb = L.xs[2 * c + 1];
+                const double2 xx = *reinterpret_cast<const double2 *>(&L.xs[2 * c]);
 #pragma unroll
                 for (int j = 0; j < EPL; j++) {
                     const double2 tt = txl[c][j * 64 + lane];
-                    z[j] = fma((T)tt.x, (T)xa, z[j]);
-                    z1[j] = fma((T)tt.y, (T)xb, z1[j]);
+                    z[j] = fma((T)tt.x, (T)xx.x, z[j]);
+                    z1[j] = fma((T)tt.y, (T)xx.y, z1[j]);
                 }
             }
 #pragma unroll
@@ -610,96 +840,91 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
             if (!__any(wf != 0)) {
                 bool bad = false;
 #pragma unroll
-                for (int j = 0; j < EPL; j++) bad |= violated(z[j], (T)sv.lb(j), (T)sv.ub(j)) || !isfinite(z[j]);
+                for (int j = 0; j < EPL; j++) bad |= !(z[j] >= (T)sv.lo(j) && z[j] <= (T)sv.hi(j));   // NaN: bad
                 ok = !__any(bad);
             }
             if (!ok) {
-                // ---- active-set steps on W (rare), the set and z_0 / z through LDS
-#pragma unroll
-                for (int j = 0; j < EPL; j++) {
-                    L.zb[j * 64 + lane] = (double)z[j];
-                    L.fl[j * 64 + lane] = flag_of(wf, j);
-                }
-                CLF_SYNC();
-                const int r = wsteps_run<T, NX, NU, EPL>(p, L, sv, lane);
-                ok = (r & 1) != 0;
-                m_acc = ok ? (r >> 8) & 0xff : 0;
-                iters = 1 + (r >> 16);
-                if (ok) {
-#pragma unroll
-                    for (int j = 0; j < EPL; j++) z[j] = (T)L.zb[j * 64 + lane];
-                } else {
-                    // ---- interval certificate (oracle/c/riccati_ipm.c infeasible_stage)
-#pragma unroll
-                    for (int c = 0; c < NX; c++)
-                        if (lane == c) L.xs[c] = (double)x[c];
-                    CLF_SYNC();
-                    if (certificate_infeasible<T, NX, NU>(p, L, lane)) {
+                // ---- active-set steps on W (rare)
+                // PDAS rounds from the warm set; if they do not settle: the interval certificate (oracle/c/
+                // riccati_ipm.c infeasible_stage: status 4), else the dual active-set fallback finds the set
+                // and one more PDAS run solves and checks it; else the instance parks
+                // (an instance whose last solve failed tries the certificate first: infeasible QPs come in runs).
+                // The first PDAS run takes at most PDAS_ROUNDS rounds (its long runs are cycles, which the
+                // fallback resolves in a few steps), the run after the fallback polish_steps.
+                int r = 0, steps_ = 0;
+                unsigned wset = wf;
+                const bool cert_first = last_status == 4;
+                if (cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) status = 4;
+                for (int pass = 0; pass < 2 && status != 4; pass++) {
+                    r = wsteps_run<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, pass == 0 ? min(p.polish_steps, PDAS_ROUNDS) : p.polish_steps);
+                    steps_ += r >> 16;
+                    if ((r & 1) || pass == 1) break;
+                    if (!cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) {
                         status = 4;
-                        iters = 0;
-                    } else {
-                        parked = true;
                         break;
                     }
+                    int git = 0;
+                    const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git);
+                    steps_ += git;
+                    if (!found) break;
+                }
+                ok = (r & 1) != 0;
+                m_acc = ok ? (r >> 8) & 0xff : 0;
+                iters = status == 4 ? 0 : 1 + steps_;
+                if (!ok && status != 4) {
+                    parked = true;
+                    break;
                 }
             }
             // ---- the solution's active flags (z on a bound to 1e-7): the next step's warm start
             fl = 0;
             if (status == 0) {
 #pragma unroll
-                for (int j = 0; j < EPL; j++) {
-                    const T l = (T)sv.lb(j), u = (T)sv.ub(j);
-                    const bool onl = has_b(l) && z[j] <= l + T(1e-7) * (T(1) + fabs(l));
-                    const bool onu = has_b(u) && z[j] >= u - T(1e-7) * (T(1) + fabs(u));
-                    fl |= (onl ? 1u : (onu ? 2u : 0u)) << (2 * j);
-                }
+                for (int j = 0; j < EPL; j++)
+                    fl |= (z[j] <= (T)sv.onl(j) ? 1u : (z[j] >= (T)sv.onu(j) ? 2u : 0u)) << (2 * j);
             }
             // ---- u0 (slots 0..nu-1: lanes 0..nu-1 of j = 0), clamped onto its bound
             const T z0c = fmin(fmax(z[0], (T)sv.lb(0)), (T)sv.ub(0));
             double u0[NU];
 #pragma unroll
             for (int i = 0; i < NU; i++) u0[i] = status == 0 ? bcast((double)z0c, i) : (double)p.uinit[i];
-            // ---- cost (controller.py:40-41) at x_0 = the state, or x_1 (jerk loop), and the AED numerator
-            double cc = 0.0, aa = 0.0;
-#pragma unroll
-            for (int i = 0; i < NR; i++) {
-                if (i < p.ncl) {
-                    double xo = (double)x[i];
-                    if (p.cost_stage != 0) {
-                        xo = status == 0 ? bcast((double)z0c, p.x1_slot + i) : (double)init_point(p, NX, NZ, 1, i, t, T(0));
-                    }
-                    const double e = xo - (double)xr[i];
-                    cc += (double)p.wcl[i] * e * e;
+            // ---- cost (controller.py:40-41) at x_0 = the state, or x_1 (jerk loop), and the AED numerator:
+            // lane i adds component i
+            {
+                double xo = xl;
+                if (p.cost_stage != 0) {
+                    const double x1 = __shfl((double)z0c, p.x1_slot + lane);
+                    xo = status == 0 ? x1 : (lane < NX ? (double)init_point(p, NX, NZ, 1, lane, t, T(0)) : 0.0);
                 }
-                if (i < p.aed_dims) aa += fabs((double)xr[i] - (double)x[i]);
+                const double e = xo - xr;
+                if (lane < p.ncl) cost = fma(wl * e, e, cost);
+                if (lane < p.aed_dims) aed += fabs(xr - xl);
             }
-            cost += cc;
-            aed += aa;
-            nfail += status != 0 ? 1.0 : 0.0;
-            nst += 1.0;
+            nfail += status != 0;
+            nst++;
+            if (p.iter_log && lane == 0) {
+                const long long kc = (clock64() - clk0) >> 6;
+                p.iter_log[(size_t)(step - p.step0) * p.B + inst] =
+                    (iters < 255 ? iters : 255) | (status << 8) | ((int)(kc < 32767 ? kc : 32767) << 16);
+            }
             last_status = status;
             last_iters = iters;
             // ---- the trajectory outputs of the instance's last step of the run
-            if (step + 1 == p.target) {
-#pragma unroll
-                for (int c = 0; c < NX; c++)
-                    if (lane == c) L.xs[c] = (double)x[c];
-                CLF_SYNC();
-                write_outputs<T, NX, NU, EPL>(p, L, lane, inst, t, status, m_acc);
-            }
+            if (step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, lane, inst, t, status, m_acc);
             // ---- plant step + noise
-            plant_step<T, NX, NU, SP>(p, abl, cl, x, u0, w);
+            xl = plant_step<T, NX, NU, SP>(p, abl, cl, L.xs, xl, u0, w, lane);
             t = tn;
         }
         // ---- write back: state, sums, step, flags, status
+        cost = wave_sum(cost);
+        aed = wave_sum(aed);
+        if (lane < NX) p.state[(size_t)inst * NX + lane] = (T)xl;
         if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < NX; c++) p.state[(size_t)inst * NX + c] = x[c];
             double *a = p.acc + (size_t)inst * 4;
             a[0] += cost;
             a[1] += aed;
-            a[2] += nfail;
-            a[3] += nst;
+            a[2] += (double)nfail;
+            a[3] += (double)nst;
             p.istep[inst] = step;
             if (parked) {
                 const int pos = atomicAdd(p.park_count, 1);
@@ -714,6 +939,7 @@ __global__ __launch_bounds__(64 * WPB) void cl_fast_kernel(ClFastParams<T> p)
             const int s = j * 64 + lane;
             if (s < p.nslot) p.flags[(size_t)inst * p.nslot + s] = flag_of(fl, j);
         }
+        CLF_SYNC();   // L.xs / L.fl of this instance are read before the next one overwrites them
     }
 }
 
@@ -727,20 +953,39 @@ int cl_fast_epl(int nx, int nu)
     return 0;
 }
 
+// largest active set of the fast path per shape (oracle/cref.py WSMAX restates it): the saturating
+// force model rides input bounds over long arcs (its closed loop needs up to ~20), quad13 and jerk 16
+// (the dual active-set fallback's sets on the bench workloads)
+int cl_fast_wsmax(int nx, int nu)
+{
+    return (nx == 4 && nu == 2) ? 32 : 16;
+}
+
+template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
+static void launch_one(const ClFastParams<T> &p, int waves, hipStream_t s)
+{
+    const int blocks = (waves + WPB - 1) / WPB;
+    hipLaunchKernelGGL((clf::cl_fast_kernel<T, NX, NU, EPL, WSM, WPB, MW, SP>), dim3(blocks), dim3(64 * WPB), 0, s, p);
+}
+
+// NMPC_CLF_VARIANT=1 (tuning): quad13 with an occupancy target of 4 waves per SIMD (spills; measured
+// 10 % slower than the default without a target)
 template <typename T>
 hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, hipStream_t s)
 {
-    const int blocks = (waves + clf::WPB - 1) / clf::WPB;
-    if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id)
-        hipLaunchKernelGGL((clf::cl_fast_kernel<T, 13, 4, 4, lpc::Quad13Structure>), dim3(blocks), dim3(64 * clf::WPB), 0, s, p);
-    else if (nx == 13 && nu == 4)
-        hipLaunchKernelGGL((clf::cl_fast_kernel<T, 13, 4, 4, lpc::DenseStructure<13, 4>>), dim3(blocks), dim3(64 * clf::WPB), 0, s, p);
-    else if (nx == 6 && nu == 2)
-        hipLaunchKernelGGL((clf::cl_fast_kernel<T, 6, 2, 5, lpc::DenseStructure<6, 2>>), dim3(blocks), dim3(64 * clf::WPB), 0, s, p);
-    else if (nx == 4 && nu == 2)
-        hipLaunchKernelGGL((clf::cl_fast_kernel<T, 4, 2, 2, lpc::DenseStructure<4, 2>>), dim3(blocks), dim3(64 * clf::WPB), 0, s, p);
-    else
+    static const int var = std::getenv("NMPC_CLF_VARIANT") ? std::atoi(std::getenv("NMPC_CLF_VARIANT")) : 0;
+    if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) {
+        if (var == 1) launch_one<T, 13, 4, 4, 16, 8, 4, lpc::Quad13Structure>(p, waves, s);
+        else launch_one<T, 13, 4, 4, 16, 8, 0, lpc::Quad13Structure>(p, waves, s);
+    } else if (nx == 13 && nu == 4) {
+        launch_one<T, 13, 4, 4, 16, 8, 0, lpc::DenseStructure<13, 4>>(p, waves, s);
+    } else if (nx == 6 && nu == 2) {
+        launch_one<T, 6, 2, 5, 16, 8, 0, lpc::DenseStructure<6, 2>>(p, waves, s);
+    } else if (nx == 4 && nu == 2) {
+        launch_one<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>(p, waves, s);
+    } else {
         return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

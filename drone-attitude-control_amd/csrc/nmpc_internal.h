@@ -129,9 +129,12 @@ struct ClFastParams {
     T *xout, *uout;               // trajectories of the last solve (written at the last step)
     int *status, *iters;
     int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
+    int *iter_log;                // optional [steps][B]: active-set steps (<= 255) | status << 8 | clock / 64 (<= 32767) << 16
 };
 // compiled fast kernels: EPL slots per lane (0 if none for this shape)
 int cl_fast_epl(int nx, int nu);
+// largest active set of the fast path for the shape (oracle/cref.py WSMAX)
+int cl_fast_wsmax(int nx, int nu);
 template <typename T>
 hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, hipStream_t s);
 
@@ -144,6 +147,9 @@ template <typename T>
 int ipm_find(int nx, int nu, int ipw_req, int batch, int *ipw_out, int *lds_out, int *wpb_out);
 template <typename T>
 hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s);
+// first dense compiled entry of family `kind` (0 wavefront, 1 lane per component) for (nx, nu), or -1
+template <typename T>
+int ipm_find_family(int nx, int nu, int kind);
 // scratch elements (of T) the kernel `idx` needs for a batch of B instances, horizon N
 template <typename T>
 size_t ipm_scratch_elems(int idx, int B, int N);

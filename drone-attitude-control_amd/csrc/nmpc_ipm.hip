@@ -1343,6 +1343,21 @@ int ipm_find(int nx, int nu, int ipw_req, int batch, int *ipw_out, int *lds_out,
     return best;
 }
 
+// the first compiled dense entry of family `kind` for (nx, nu), or -1 (the lean closed loop's list-mode
+// fallback runs the lane-per-component family whatever the handle's own family is)
+template <typename T>
+int ipm_find_family(int nx, int nu, int kind)
+{
+    int n;
+    const IpmEntry<T> *t = table<T>(&n);
+    for (int i = 0; i < n; i++)
+        if (t[i].nx == nx && t[i].nu == nu && t[i].kind == kind && !t[i].sid) return i;
+    return -1;
+}
+
+template int ipm_find_family<double>(int, int, int);
+template int ipm_find_family<float>(int, int, int);
+
 template <typename T>
 hipError_t ipm_launch(int idx, const IpmParams<T> &p, hipStream_t s)
 {

@@ -786,6 +786,7 @@ typedef struct {
 #ifndef WSMAX
 #define WSMAX 64
 #endif
+#define PDAS_ROUNDS 6   /* rounds of the first PDAS run before the dual fallback (nmpc_cl_fast.hip) */
 
 
 /* Philox4x32-10 + Box-Muller: the device's noise stream (nmpc_cl_device.h philox_normal_dev) */
@@ -994,11 +995,11 @@ static int valid_el(int nx, int N, int k, int i) { return !(k == 0 && i < nx) &&
 
 /* The fast finish of one step (mode 1). wf: the warm set (shifted flags, in), the set reached
  * (out). Returns 1 and the solution in z (clamped onto the bounds) when accepted, else why not:
- * -2 a set larger than WSMAX, -3 W_SS not positive definite (linearly dependent bounds: an
- * infeasible QP), -4 polish_steps rounds without acceptance. Counts the active-set steps and the
+ * -2 a set larger than WSMAX, -3 a non-positive diagonal of W (never for a decision variable), -4
+ * polish_steps rounds without acceptance. Counts the active-set steps and the
  * FP64 work. */
 static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double *x0, int t, signed char *wf,
-                       double *z0, double *z, int *wsteps, double *flops, int wsmax)
+                       double *z0, double *z, int *wsteps, double *flops, int wsmax, int rounds)
 {
     const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
     const double *vt = f->v + (size_t)t * ne;
@@ -1014,7 +1015,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
             z0[e] = s;
             *flops += 2.0 * nx;
         }
-    for (int ws = 0, first = 1; ws < d->polish_steps; first = 0) {
+    for (int ws = 0, first = 1; ws < rounds; first = 0) {
         int S[WSMAX], m = 0;
         for (int e = 0; e < ne; e++)
             if (wf[e]) { if (m < WSMAX) S[m] = e; m++; }
@@ -1058,17 +1059,20 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
             lt[i] = (wf[S[i]] < 0 ? LBk(d, k, c) : UBk(d, k, c)) - z0[S[i]];
             nu_[i] = lt[i];
         }
+        /* Cholesky of W_SS; a bound whose pivot falls below 1e-9 of its diagonal W_ii is linearly
+         * dependent on the bounds before it in the set (an input on its bound and the state it drives on
+         * its own one stage later): its pivot is regularised to 1e-6 W_ii, i.e. it is held by a penalty,
+         * so the others' multipliers show which of them has to leave (the exact finish's penalty rule) */
+        for (int i = 0; i < m; i++) {
+            wd[i] = f->W[(size_t)S[i] * ne + S[i]];
+            if (!(wd[i] > 0.0)) return -3;
+        }
         for (int i = 0; i < m; i++)
             for (int j = 0; j <= i; j++) {
                 double s = f->W[(size_t)S[j] * ne + S[i]];
-                if (i == j) wd[i] = s;
                 for (int l = 0; l < j; l++) s -= L[i][l] * L[j][l];
-                if (i == j) {
-                    if (!(s > 0.0)) return -3;
-                    L[i][i] = sqrt(s);
-                } else {
-                    L[i][j] = s / L[j][j];
-                }
+                if (i == j) L[i][i] = s > 1e-9 * wd[i] ? sqrt(s) : sqrt((s > 0.0 ? s : 0.0) + 1e-6 * wd[i]);
+                else L[i][j] = s / L[j][j];
             }
         for (int i = 0; i < m; i++) {
             double s = nu_[i];
@@ -1142,6 +1146,152 @@ accept:
             if (has(ub) && z[e] > ub) z[e] = ub;
         }
     return 1;
+}
+
+/* Cholesky of the signed W_AA (entries sg_i sg_j W[A_i][A_j]) with fast_finish's regularised pivots */
+static void gi_factor(const fast_tables *f, const int *A, const int *sg, int m, double L[WSMAX][WSMAX])
+{
+    const int ne = f->ne;
+    for (int i = 0; i < m; i++)
+        for (int j = 0; j <= i; j++) {
+            double s = sg[i] * sg[j] * f->W[(size_t)A[j] * ne + A[i]];
+            for (int l = 0; l < j; l++) s -= L[i][l] * L[j][l];
+            if (i == j) {
+                const double wii = f->W[(size_t)A[i] * ne + A[i]];
+                L[i][i] = s > 1e-9 * wii ? sqrt(s) : sqrt((s > 0.0 ? s : 0.0) + 1e-6 * wii);
+            } else {
+                L[i][j] = s / L[j][j];
+            }
+        }
+}
+
+/* The fast path's fallback when the PDAS rounds do not settle (degenerate sets, cycling): the
+ * Goldfarb-Idnani dual active-set method on W (Goldfarb & Idnani, Math. Prog. 27 (1983)), which
+ * converges for any strictly convex QP. The bounds are the constraints n_i^T z >= b_i with n_i = +e
+ * (lower) or -e (upper); from z = z_0 and an empty set the most violated inactive bound p enters:
+ * with the set's multipliers u >= 0, l = L^-1 N_A^T W n_p, r = L^-T l (the multipliers' rate),
+ * theta = n_p^T W n_p - |l|^2 (the curvature along p), dz = W n_p - W N_A r; the full step
+ * t2 = -(n_p^T z - b_p) / theta makes p active, the partial step t1 = min u_i / r_i (r_i > 0) drops the
+ * bound whose multiplier reaches zero first; z += t dz, u -= t r, u_p += t. A dependent p (theta ~ 0)
+ * only drops; no blocking bound and theta ~ 0: infeasible. Returns 1 with the set in wf (flags) when no
+ * inactive bound is violated beyond 1e-13, < 0 otherwise (-5 infeasible, -6 set larger than wsmax,
+ * -7 iteration cap). fast_finish then solves that set exactly and checks its KKT conditions. */
+static int gi_set(const ocp_ref_desc *d, const fast_tables *f, const double *z0, const signed char *w0, signed char *wf,
+                  int wsmax, int *iters, double *flops)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
+    int A[WSMAX], sg[WSMAX], m = 0, p = -1, sp = 0, it;
+    double u[WSMAX], l[WSMAX], r[WSMAX], up = 0.0, z[NZMAX * 64];
+    static double L[WSMAX][WSMAX];
+#pragma omp threadprivate(L)
+    memset(wf, 0, (size_t)ne);
+    memcpy(z, z0, sizeof(double) * ne);
+    /* warm start: the set the PDAS rounds started from, made dual feasible (its equality-constrained
+     * solution's multipliers u = (N_A^T W N_A)^-1 sg (b_A - z_0,A); the negative ones leave, re-solved
+     * until none is left), z = z_0 + W N_A u */
+    if (w0) {
+        for (int e = 0; e < ne && m <= wsmax; e++)
+            if (w0[e]) { if (m < wsmax) { A[m] = e; sg[m] = w0[e] < 0 ? 1 : -1; } m++; }
+        if (m > wsmax) m = 0;
+        while (m > 0) {
+            gi_factor(f, A, sg, m, L);
+            for (int i = 0; i < m; i++) {
+                const int k = A[i] / nz, c = A[i] % nz;
+                double s = sg[i] * ((sg[i] > 0 ? LBk(d, k, c) : UBk(d, k, c)) - z0[A[i]]);
+                for (int q = 0; q < i; q++) s -= L[i][q] * u[q];
+                u[i] = s / L[i][i];
+            }
+            for (int i = m - 1; i >= 0; i--) {
+                double s = u[i];
+                for (int q = i + 1; q < m; q++) s -= L[q][i] * u[q];
+                u[i] = s / L[i][i];
+            }
+            *flops += m * m * m / 3.0 + 2.0 * m * m;
+            int k = 0;
+            for (int i = 0; i < m; i++)
+                if (!(u[i] < 0.0)) { A[k] = A[i]; sg[k] = sg[i]; u[k] = u[i]; k++; }
+            if (k == m) break;
+            m = k;
+        }
+        for (int q = 0; q < m; q++) {
+            wf[A[q]] = sg[q] > 0 ? -1 : 1;
+            for (int e = 0; e < ne; e++) z[e] += sg[q] * u[q] * f->W[(size_t)A[q] * ne + e];
+        }
+        *flops += 2.0 * ne * m;
+    }
+    const int cap = 3 * wsmax + 16;
+    for (it = 0; it < cap; it++) {
+        if (p < 0) {   /* the most violated inactive bound (ties: the first element) */
+            double vmax = 0.0;
+            for (int k = 0; k <= N; k++)
+                for (int i = 0; i < nz; i++) {
+                    if (!valid_el(nx, N, k, i)) continue;
+                    const int e = k * nz + i;
+                    if (wf[e]) continue;
+                    const double lb = LBk(d, k, i), ub = UBk(d, k, i);
+                    const int lo = has(lb) && z[e] < lb - 1e-13 * (1.0 + fabs(lb)), hi = has(ub) && z[e] > ub + 1e-13 * (1.0 + fabs(ub));
+                    const double v = lo ? lb - z[e] : (hi ? z[e] - ub : 0.0);
+                    if (v > vmax) { vmax = v; p = e; sp = lo ? 1 : -1; }
+                }
+            if (p < 0) break;
+            up = 0.0;
+        }
+        const double wpp = f->W[(size_t)p * ne + p];
+        for (int i = 0; i < m; i++) l[i] = sg[i] * sp * f->W[(size_t)A[i] * ne + p];
+        double ll = 0.0;
+        for (int i = 0; i < m; i++) {
+            double s = l[i];
+            for (int q = 0; q < i; q++) s -= L[i][q] * l[q];
+            l[i] = s / L[i][i];
+            ll += l[i] * l[i];
+        }
+        for (int i = m - 1; i >= 0; i--) {
+            double s = l[i];
+            for (int q = i + 1; q < m; q++) s -= L[q][i] * r[q];
+            r[i] = s / L[i][i];
+        }
+        const double theta = wpp - ll;
+        double t1 = INFINITY;
+        int kk = -1;
+        for (int i = 0; i < m; i++)
+            if (r[i] > 0.0 && u[i] / r[i] < t1) { t1 = u[i] / r[i]; kk = i; }
+        const int kp = p / nz, ip = p % nz;
+        const double cp = sp * (z[p] - (sp > 0 ? LBk(d, kp, ip) : UBk(d, kp, ip)));
+        const double t2 = theta > 1e-12 * wpp ? -cp / theta : INFINITY;
+        *flops += 2.0 * m * m + 2.0 * m;
+        if (t1 == INFINITY && t2 == INFINITY) return -5;
+        const int full = t2 <= t1;
+        const double t = full ? t2 : t1;
+        if (t2 < INFINITY) {
+            for (int k = 0; k <= N; k++)
+                for (int i = 0; i < nz; i++) {
+                    if (!valid_el(nx, N, k, i)) continue;
+                    const int e = k * nz + i;
+                    double dz = sp * f->W[(size_t)p * ne + e];
+                    for (int q = 0; q < m; q++) dz -= sg[q] * f->W[(size_t)A[q] * ne + e] * r[q];
+                    z[e] += t * dz;
+                }
+            *flops += 2.0 * ne * (m + 1);
+        }
+        for (int i = 0; i < m; i++) u[i] -= t * r[i];
+        up += t;
+        if (full) {
+            if (m >= wsmax) return -6;
+            for (int q = 0; q < m; q++) L[m][q] = l[q];
+            L[m][m] = sqrt(theta);
+            A[m] = p; sg[m] = sp; u[m] = up; m++;
+            wf[p] = sp > 0 ? -1 : 1;
+            p = -1;
+        } else {
+            wf[A[kk]] = 0;
+            for (int i = kk; i + 1 < m; i++) { A[i] = A[i + 1]; sg[i] = sg[i + 1]; u[i] = u[i + 1]; }
+            m--;
+            gi_factor(f, A, sg, m, L);
+            *flops += m * m * m / 3.0;
+        }
+    }
+    *iters = it;
+    return p < 0 ? 1 : -7;
 }
 
 static void crazyflie_rhs_ref(const double x[4], double st, double ct, double Fd, double inv_m, double g, double f[4])
@@ -1389,7 +1539,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
         double *yref = (double *)malloc(sizeof(double) * ((size_t)N * ny + nye));
         double *xo = (double *)malloc(sizeof(double) * (N + 1) * nx), *uo = (double *)malloc(sizeof(double) * N * nu);
         double *z0 = (double *)malloc(sizeof(double) * ne), *zf = (double *)malloc(sizeof(double) * ne);
-        signed char *wf = (signed char *)malloc(ne);
+        signed char *wf = (signed char *)malloc(ne), *w0 = (signed char *)malloc(ne);
 #pragma omp for schedule(dynamic, 4)
         for (int b = 0; b < batch; b++) {
             double *st = state + (size_t)b * nx;
@@ -1408,8 +1558,25 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                     if (d->polish_mu > 0.0) {
                         int wst = 0, nw = 0;
                         for (int e = 0; e < ne; e++) nw += wf[e] != 0;
-                        ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax) > 0;
+                        memcpy(w0, wf, (size_t)ne);   /* the warm set (the fallback's start) */
+                        /* an instance whose last solve failed tries the certificate first (solve_one returns
+                         * status 4 for it); the first PDAS run takes at most PDAS_ROUNDS rounds */
+                        const int cert_first = failed && failed[b];
+                        if (!(cert_first && infeasible_stage(d, st) > 0))
+                            ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax,
+                                             d->polish_steps < PDAS_ROUNDS ? d->polish_steps : PDAS_ROUNDS) > 0;
                         cnt[3] += wst;
+                        /* not settled: unless the interval certificate proves the QP infeasible (solve_one
+                         * returns that), the dual active-set fallback, its set then solved and checked by
+                         * fast_finish */
+                        if (!ok && infeasible_stage(d, st) == 0) {
+                            int git = 0;
+                            if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
+                                ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
+                                cnt[3] += wst;
+                            }
+                            cnt[3] += git;
+                        }
                         if (ok) {
                             path = (nw == 0 && wst == 0) ? 0 : 1;
                             cnt[path == 0 ? 1 : 2] += 1;
@@ -1459,7 +1626,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                 if (path_log) path_log[(size_t)b * steps + s] = path;
             }
         }
-        free(buf); free(yref); free(xo); free(uo); free(z0); free(zf); free(wf);
+        free(buf); free(yref); free(xo); free(uo); free(z0); free(zf); free(wf); free(w0);
     }
     fast_free(f);
     if (counters)

@@ -140,8 +140,13 @@ class _ClDesc(ctypes.Structure):
         ("mass", ctypes.c_double), ("g", ctypes.c_double), ("dt", ctypes.c_double), ("dt_conv", ctypes.c_double),
         ("noise", ctypes.c_void_p), ("noise_len", ctypes.c_int),
         ("noise_std", ctypes.c_double), ("seed", ctypes.c_ulonglong), ("inst_base", ctypes.c_longlong),
-        ("inst_ids", ctypes.c_void_p),
+        ("inst_ids", ctypes.c_void_p), ("wsmax", ctypes.c_int),
     ]
+
+
+# largest active set of the device's lean closed loop per model (nmpc_cl_fast.hip cl_fast_wsmax):
+# mode 1 restates the same cap
+WSMAX = {"quad13": 16, "jerk": 16, "force": 32}
 
 
 class ClosedLoopRef:
@@ -199,6 +204,7 @@ class ClosedLoopRef:
             d.noise, d.noise_len = keep["noise"].ctypes.data, keep["noise"].shape[1]
         d.noise_std = P.NOISE if noise_std is None else float(noise_std)
         d.seed, d.inst_base = int(seed), int(instance_base)
+        d.wsmax = WSMAX.get(model, 8)
         if instance_ids is not None:   # global ids of a subset of instances (Philox stream)
             keep["ids"] = np.ascontiguousarray(instance_ids, dtype=np.int64)
             d.inst_ids = keep["ids"].ctypes.data

@@ -81,28 +81,33 @@ def test_bench_closed_loop_matches_oracle(golden, model, N, B):
 
 @pytest.mark.timeout(300)
 def test_force_fused_loop_families_agree():
-    """The two kernel families of the force model — lane per component (LPC, the fused fast finish;
-    the default from B = 8192 in fp64) and wavefront per instance block (below it) — run the same
-    fused closed loop on a ragged batch of 2049 over 70 steps (two launches, 64 + 6): states and
-    per-instance sums agree to 1e-9, failure counts exactly, and both match the oracle."""
+    """The force model's three closed-loop paths — the lean loop (nmpc_cl_fast.hip, the default, with
+    its list-mode fallback on the lane-per-component kernel), and the fused loops of the two kernel
+    families (NMPC_CL_FAST=0: lane per component, LPC; wavefront per instance block) — on a ragged
+    batch of 2049 over 70 steps (two launches, 64 + 6): states and per-instance sums agree to 1e-9,
+    failure counts exactly, and all match the oracle."""
     from drone_attitude_control_amd.batched import ClosedLoop, workload
     from oracle import cref, models
 
     def run(kernel):
-        os.environ["NMPC_KERNEL"] = kernel
+        env = {"NMPC_KERNEL": kernel, "NMPC_CL_FAST": "0"} if kernel else {}
+        os.environ.update(env)
         try:
             cl = ClosedLoop("force", 2049, N=20, seed=5)
-            assert cl.solver.launch_info()["kernel"] == {"lpc": "ipm_lpc_kernel", "wave": "ipm_kernel"}[kernel]
+            if kernel:
+                assert cl.solver.launch_info()["kernel"] == {"lpc": "ipm_lpc_kernel", "wave": "ipm_kernel"}[kernel]
             cl.run(70)
             return cl.state(), cl.instance_stats()
         finally:
-            os.environ.pop("NMPC_KERNEL", None)
+            for k in env:
+                os.environ.pop(k, None)
 
     xl, sl = run("lpc")
-    xw, sw = run("wave")
-    assert np.array_equal(sl[:, 2:], sw[:, 2:])
-    assert np.allclose(xl, xw, rtol=1e-9, atol=1e-9), np.abs(xl - xw).max()
-    assert np.allclose(sl[:, :2], sw[:, :2], rtol=1e-9, atol=1e-12)
+    for other in ("wave", None):
+        xw, sw = run(other)
+        assert np.array_equal(sl[:, 2:], sw[:, 2:]), other
+        assert np.allclose(xl, xw, rtol=1e-9, atol=1e-9), (other, np.abs(xl - xw).max())
+        assert np.allclose(sl[:, :2], sw[:, :2], rtol=1e-9, atol=1e-12), other
     table, off, x = workload("force", 20, 2049, 5)
     ref = cref.ClosedLoopRef(models.force_model(20), "force", table, off, x, mode=0, seed=5)
     ref.run(70)
