@@ -236,7 +236,8 @@ def main():
         achieved = fl_launch / (kernel_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.precision]
         info = cl.solver.launch_info()
-        pmc = load_pmc(model, N, B, args.precision, info["kernel"])
+        kernel = info["closed_loop_kernel"] if info["closed_loop_kernel"] != "fused" else info["kernel"]
+        pmc = load_pmc(model, N, B, args.precision, kernel)
         headline = model == "quad13" and N == 20
         metric = ("NMPC steps/sec (batched trajectories), N=20 nx=13 nu=4, 1/2/4/8 MI355X" if headline else
                   f"NMPC steps/sec (batched trajectories), N={N} nx={nx} nu={nu} ({model}), 1/2/4/8 MI355X")
@@ -268,7 +269,7 @@ def main():
             "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32",
                          "pipe": ("FP64 FMA on the VALU" if args.precision == "fp64" else "FP32 FMA on the VALU")
                          + " (MI355X: FP64 matrix peak = FP64 vector peak; FP32 matrix peak = FP32 vector peak)",
-                         "kernel": info["kernel"], "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "kernel": kernel, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak,
                          "credit": "FP64 flops per instance-step of the CPU baseline's run of the same algorithm on "
                                    "the same steps (oracle closed loop mode 1, counted per path: explicit solution "

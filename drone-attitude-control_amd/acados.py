@@ -416,11 +416,13 @@ class AcadosOcpSolver:
         return self._check(self.lib.nmpc_set_stream(self._h, ctypes.c_void_p(stream_ptr)), "set_stream")
 
     def launch_info(self):
-        out = (ctypes.c_int * 6)()
-        self._check(self.lib.nmpc_get_launch_info(self._h, out, 6), "launch_info")
+        out = (ctypes.c_int * 8)()
+        self._check(self.lib.nmpc_get_launch_info(self._h, out, 8), "launch_info")
         return {"instances_per_wave": out[0], "workgroups": out[1], "threads": out[2], "lds_bytes": out[3],
                 "kernel": {0: "ipm_kernel", 1: "ipm_lpc_kernel", 2: "cond_ipm_kernel", 3: "ipm_lpi_kernel"}.get(out[4], str(out[4])),
-                "structure": {0: "dense", 1: "force", 2: "jerk", 3: "quad13"}.get(out[5], str(out[5]))}
+                "structure": {0: "dense", 1: "force", 2: "jerk", 3: "quad13"}.get(out[5], str(out[5])),
+                "closed_loop_kernel": "cl_fast_kernel" if out[6] else "fused",
+                "active_set_max": out[7]}
 
     def discrete_model(self):
         A = np.zeros((self.nx, self.nx))

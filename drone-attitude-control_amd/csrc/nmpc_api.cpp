@@ -1371,8 +1371,9 @@ int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
     const bool f64 = h->precision == NMPC_FP64;
     const int kind = h->cond ? 2 : f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
     const int sid = h->cond ? 0 : f64 ? nmpc::ipm_structure<double>(h->kidx) : nmpc::ipm_structure<float>(h->kidx);
-    const int v[6] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid};
-    for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
+    const int v[8] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid, h->clf ? 1 : 0,
+                      h->clf ? nmpc::cl_fast_wsmax(h->nx, h->nu) : 0};
+    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
     return 0;
 }
 

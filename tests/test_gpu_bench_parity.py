@@ -1,6 +1,7 @@
-"""GPU parity of the exact path bench.py times: the default fused closed loop (steps inside the
-solve kernel, warm-started active sets, the fast finish with its explicit unconstrained
-solution and active-set steps on the shared factorisation) at the BASELINE sizes, on the bench's
+"""GPU parity of the exact path bench.py times: the default closed loop — the lean loop
+(nmpc_cl_fast.hip: explicit unconstrained solution, warm-started PDAS steps on the projected inverse
+Hessian, the dual active-set fallback, the interval certificate, the list-mode full solve for what
+is left) — at the BASELINE sizes, on the bench's
 own seed-42 workload (batched.workload: start rows, initial states, Philox noise keyed by the
 global instance id) and launch boundaries (3 warm-up steps, then 10 regions of 20), against
 
@@ -48,7 +49,9 @@ def test_bench_closed_loop_matches_oracle(golden, model, N, B):
     sel = golden[f"{key}_sel"]
     assert list(golden["checkpoints"]) == list(np.cumsum(REGIONS))
     loop = ClosedLoop(model, B, N=N, seed=42)             # bench.py's workload and defaults
-    assert loop.solver.launch_info()["kernel"] in ("ipm_lpc_kernel", "ipm_kernel")
+    info = loop.solver.launch_info()
+    assert info["kernel"] in ("ipm_lpc_kernel", "ipm_kernel")
+    assert info["closed_loop_kernel"] == "cl_fast_kernel"   # the lean loop bench.py times
     states, sums = [], []
     for n in REGIONS:
         loop.run(n)

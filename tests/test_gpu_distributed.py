@@ -26,13 +26,13 @@ def _port():
     return p
 
 
-def _bench(args, world):
+def _bench(args, world, **env_extra):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
     if world > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
                *args, "--dist-backend", "gloo"]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **env_extra)
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
     assert out.returncode == 0, out.stderr[-3000:]
     return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
@@ -40,36 +40,39 @@ def _bench(args, world):
 
 @pytest.mark.timeout(300)
 def test_force_two_ranks_reduce_equals_one_process():
-    """Split across the kernel-family crossover: each rank's 4096 instances run the wavefront
-    family, the single process's 8192 the lane-per-component family (fp64 force crossover at
-    B = 8192, nmpc_ipm.hip kernel_kind) — sharding must not change the statistics either way.
-    Across the families the sums agree to the solvers' precision (1e-8 relative; both families
-    return the exact QP solutions, by different paths), not bit for bit (a family bug that moved a
-    solution showed as 7e-7 relative in round 2)."""
+    """Two ranks x 4096 against one process over 8192, both ways the force closed loop can run:
+    the lean loop (the default: one wavefront per instance, so sharding changes nothing but the
+    summation order of the statistics — 1e-10) and the fused kernel families (NMPC_CL_FAST=0): each
+    rank's 4096 instances then run the wavefront family, the single process's 8192 the
+    lane-per-component family (fp64 force crossover at B = 8192, nmpc_ipm.hip kernel_kind), which
+    agree to the solvers' precision (1e-8 relative; both return the exact QP solutions, by different
+    paths), not bit for bit (a family bug that moved a solution showed as 7e-7 relative in round 2)."""
     common = ["--model", "force", "--steps", "4", "--warmup", "2", "--repeats", "2", "--no-cpu-baseline"]
-    two = _bench(common + ["--gpus", "2", "--batch", "4096"], 2)
-    one = _bench(common + ["--gpus", "1", "--batch", "8192"], 1)
-    assert two["roofline"]["kernel"] == "ipm_kernel" and one["roofline"]["kernel"] == "ipm_lpc_kernel"
-    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == one["config"]["global_batch"] == 8192
-    a, b = two["closed_loop"], one["closed_loop"]
-    assert a["instance_steps"] == b["instance_steps"] == 8192 * (2 + 2 * 4)
-    assert a["failed_solves"] == b["failed_solves"]
-    assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=1e-8)
-    assert a["aed"] == pytest.approx(b["aed"], rel=1e-8)
-    assert two["value"] > 0 and len(two["timing"]["region_ms"]) == 2
+    for env, kernels, rel in (({}, ("cl_fast_kernel", "cl_fast_kernel"), 1e-10),
+                              ({"NMPC_CL_FAST": "0"}, ("ipm_kernel", "ipm_lpc_kernel"), 1e-8)):
+        two = _bench(common + ["--gpus", "2", "--batch", "4096"], 2, **env)
+        one = _bench(common + ["--gpus", "1", "--batch", "8192"], 1, **env)
+        assert (two["roofline"]["kernel"], one["roofline"]["kernel"]) == kernels
+        assert two["n_gpus"] == 2 and two["config"]["global_batch"] == one["config"]["global_batch"] == 8192
+        a, b = two["closed_loop"], one["closed_loop"]
+        assert a["instance_steps"] == b["instance_steps"] == 8192 * (2 + 2 * 4)
+        assert a["failed_solves"] == b["failed_solves"]
+        assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=rel)
+        assert a["aed"] == pytest.approx(b["aed"], rel=rel)
+        assert two["value"] > 0 and len(two["timing"]["region_ms"]) == 2
 
 
 @pytest.mark.timeout(600)
 def test_config4_eight_ranks_reduce_equals_one_process():
     """BASELINE config 4 at its size, rehearsed on the one-GPU box: 65,536 force instances as 8
-    ranks x 8,192 (gloo; every rank on the same GPU, each running the lane-per-component fused
-    loop on its shard) against one process over all 65,536 — the reduced cost / AED / failure /
+    ranks x 8,192 (gloo; every rank on the same GPU, each running the lean closed loop on its shard)
+    against one process over all 65,536 — the reduced cost / AED / failure /
     step statistics agree to 1e-10 (force_model/controller.py:40-41,54; store_results.py:233-236)."""
     common = ["--model", "force", "--steps", "4", "--warmup", "2", "--repeats", "1", "--no-cpu-baseline"]
     eight = _bench(common + ["--gpus", "8", "--batch", "8192"], 8)
     one = _bench(common + ["--gpus", "1", "--batch", "65536"], 1)
     assert eight["n_gpus"] == 8 and eight["config"]["global_batch"] == one["config"]["global_batch"] == 65536
-    assert eight["roofline"]["kernel"] == one["roofline"]["kernel"] == "ipm_lpc_kernel"
+    assert eight["roofline"]["kernel"] == one["roofline"]["kernel"] == "cl_fast_kernel"
     a, b = eight["closed_loop"], one["closed_loop"]
     assert a["instance_steps"] == b["instance_steps"] == 65536 * (2 + 4)
     assert a["failed_solves"] == b["failed_solves"]

@@ -76,7 +76,7 @@ def main():
                      "flops as the hardware counts them, idle lanes included)")
         key = (model, int(N), int(batch), prec)
         d["entries"] = [e for e in d["entries"] if (e["model"], e["N"], e["batch"], e["precision"]) != key]
-        d["entries"].append({"model": model, "N": int(N), "batch": int(batch), "precision": prec,
+        d["entries"].append({"model": model, "N": int(N), "batch": int(batch), "precision": prec, "kernel": a.kernel,
                              "hbm_bytes_per_launch": res["traffic_bytes_per_launch"],
                              "steps_per_launch": a.steps_per_launch,
                              "hbm_bytes_per_step": res["traffic_bytes_per_launch"] / a.steps_per_launch,
