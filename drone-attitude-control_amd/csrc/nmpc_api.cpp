@@ -225,7 +225,7 @@ struct nmpc_solver {
     size_t fso[5] = {0, 0, 0, 0, 0};
     int *d_fsI = nullptr;                  // s_e, s_src, eslot
     size_t fsi[3] = {0, 0, 0};
-    int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count + list [1 + B]
+    int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
     std::vector<float> tmp_x0f, tmp_yf;
@@ -583,7 +583,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     if (la) {
         kidx = h->clf_kidx;
         if (h->d_clf_scratch) scratch = h->d_clf_scratch;
-        p.cl_list = h->d_park + 1;
+        p.cl_list = h->d_park + 2;
         p.cl_count = la->count;
         p.cl_istep = h->d_istep;
         p.cl_noise_ld = la->noise_ld;
@@ -1590,7 +1590,7 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     bool ok = hipMalloc(&h->d_fsT, tot * sizeof(double)) == hipSuccess &&
               hipMalloc((void **)&h->d_fsI, itot * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_istep, (size_t)h->batch * sizeof(int)) == hipSuccess &&
-              hipMalloc((void **)&h->d_park, (size_t)(h->batch + 1) * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_park, (size_t)(h->batch + 2) * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_flags, (size_t)h->batch * nslot) == hipSuccess;
     if (ok && fk != h->kidx)
         ok = hipMalloc(&h->d_clf_scratch, nmpc::ipm_scratch_elems<double>(fk, h->batch, N) * sizeof(double)) == hipSuccess;
@@ -1669,7 +1669,8 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     p.status = h->d_status;
     p.iters = h->d_iters;
     p.park_count = h->d_park;
-    p.park_list = h->d_park + 1;
+    p.work = h->d_park + 1;
+    p.park_list = h->d_park + 2;
     return p;
 }
 
@@ -1715,10 +1716,10 @@ int clf_run(nmpc_solver *h, int steps)
         h->iter_log_steps = h->d_iter_log ? steps : 0;
     }
     int launches = 0;
-    // one wavefront per instance at a time: at most 8 per SIMD resident, the rest stride
-    const int waves = std::min(h->batch, 8192);
+    // one wavefront per instance at a time, as many as the device holds (persistent, cl_fast_launch)
+    const int waves = h->batch;
     for (int round = 0; round <= steps; round++) {
-        if ((e = hipMemsetAsync(h->d_park, 0, sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
+        if ((e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
         hipEventRecord(cl_event(h, 2 * launches), h->stream);
         e = nmpc::cl_fast_launch<double>(h->nx, h->nu, h->clf_sid, fp, waves, h->stream);
         hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <algorithm>
 #include <cstdlib>
 
 #include "nmpc_cl_device.h"
@@ -758,13 +759,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
     if (lane < 32) L.xs[lane] = 0.0;
     __syncthreads();
-    const int gw = blockIdx.x * WPB + wave, nw = gridDim.x * WPB;
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
 
     const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
     const double wl = lane < p.ncl ? (double)p.wcl[lane] : 0.0;   // this lane's cost weight
 
-    for (int inst = gw; inst < p.B; inst += nw) {
+    // persistent wavefronts: each takes the next instance from the launch's work counter until none is
+    // left (every wavefront reaches the exit; an instance's cost varies 10x with its active sets)
+    for (;;) {
+        int inst = 0;
+        if (lane == 0) inst = atomicAdd(p.work, 1);
+        inst = __builtin_amdgcn_readfirstlane(inst);
+        if (inst >= p.B) break;
         int step = p.istep[inst];
         if (step >= p.target) continue;
         // lane-distributed state: lane i < NX holds x_i
@@ -961,10 +967,22 @@ int cl_fast_wsmax(int nx, int nu)
     return (nx == 4 && nu == 2) ? 32 : 16;
 }
 
+// grid: the workgroups the device holds at once (persistent wavefronts), at most one wavefront per instance
 template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
 static void launch_one(const ClFastParams<T> &p, int waves, hipStream_t s)
 {
-    const int blocks = (waves + WPB - 1) / WPB;
+    static int resident = 0;
+    if (resident == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, clf::cl_fast_kernel<T, NX, NU, EPL, WSM, WPB, MW, SP>,
+                                                         64 * WPB, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus < 1)
+            cus = 256;
+        resident = per_cu * cus;
+    }
+    const int blocks = std::min((waves + WPB - 1) / WPB, resident);
     hipLaunchKernelGGL((clf::cl_fast_kernel<T, NX, NU, EPL, WSM, WPB, MW, SP>), dim3(blocks), dim3(64 * WPB), 0, s, p);
 }
 
