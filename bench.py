@@ -7,18 +7,19 @@ Workload (BASELINE.json metric "NMPC steps/sec (batched trajectories), N=20 nx=1
 the synthetic quad13 OCP (nx=13, nu=4, horizon N=20, no reference counterpart: SURVEY §0),
 B = 8192 independent closed-loop trajectories per GPU (weak scaling), fp64. One step = for
 every instance: build the yref window + pin x0 (set_up_ocp, ocp.py:117-122), solve the OCP
-(AcadosOcpSolver.solve, controller.py:32) to its exact solution (the warm-started exact finish:
-explicit unconstrained solution, primal-dual active-set steps, full IPM + finish where those
-fail), advance the plant with Philox noise and accumulate cost/AED — all resident
-in HBM. value = instances x steps / wall time (max over ranks) for all ranks together. Ranks
+(AcadosOcpSolver.solve, controller.py:32) to its exact solution (the lean closed loop,
+cl_fast_kernel: explicit unconstrained solution, warm-started primal-dual active-set steps, the
+dual active-set fallback, KKT-checked; full IPM + finish for what is left), advance
+the plant with Philox noise and accumulate cost/AED — all resident in HBM. value = instances x steps / wall time (max over ranks) for all ranks together. Ranks
 exchange nothing during the run; RCCL (torch.distributed "nccl") reduces the cost/AED/failure
 statistics once at the end.
 
 Also reported (one JSON line on rank 0):
-  roofline — the solve kernel (the dominant kernel), bound "valu_fp64": achieved = the FP64 flops
-    per instance-step that the CPU baseline executes on the same closed loop (the same algorithm,
-    counted per path it takes: explicit solution 2 nx per element, active-set steps
-    m^3/3 + 2 m^2 + 2 ne m, full solves SURVEY §8d's F_iter per Newton system, plant 2 nx nz)
+  roofline — the closed-loop kernel (the dominant kernel: cl_fast_kernel, or the fused solve kernel
+    with NMPC_CL_FAST=0), bound "valu_fp64": achieved = the FP64 flops per instance-step that the CPU
+    baseline executes on the same closed loop (the same algorithm, counted per path it takes:
+    explicit solution 2 nx per element, active-set steps m^3/3 + 2 m^2 + 2 ne m, the dual fallback's
+    iterations, full solves SURVEY §8d's F_iter per Newton system, plant 2 nx nz)
     x B / the kernel's mean duration per step from HIP events around each launch; peak = MI355X
     FP64 78.6 TFLOP/s (the FP64 vector and matrix peaks are equal). executed_frac = the FP64 flops
     the kernel really issues (SQ_INSTS_VALU_FLOPS_FP64 of the committed rocprofv3 PMC pass, idle

@@ -224,7 +224,8 @@ struct nmpc_solver {
     void *d_fsT = nullptr;                 // typed: s_lb, s_ub, s_tx, vb, uinit
     size_t fso[5] = {0, 0, 0, 0, 0};
     int *d_fsI = nullptr;                  // s_e, s_src, eslot
-    size_t fsi[3] = {0, 0, 0};
+    size_t fsi[4] = {0, 0, 0, 0};
+    int clf_nfree = 0;
     int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
@@ -1525,14 +1526,17 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         }
         fk = nmpc::ipm_refine<double>(fk, ABh.data(), h->H.data(), h->He.data());
     }
-    std::vector<int> el;
+    std::vector<int> el, fr;
     std::vector<double> lb, ub;
     for (int k = 0; k <= N; k++)
         for (int r = 0; r < nz; r++) {
             if ((k == 0 && r < nx) || (k == N && r >= nx)) continue;
             const int ty = k == 0 ? 0 : (k == N ? 2 : 1);
             const double l = h->lbnd[ty * nz + r], u_ = h->ubnd[ty * nz + r];
-            if (!has_bound(l) && !has_bound(u_)) continue;
+            if (!has_bound(l) && !has_bound(u_)) {
+                fr.push_back(k * nz + r);
+                continue;
+            }
             el.push_back(k * nz + r);
             lb.push_back(l);
             ub.push_back(u_);
@@ -1575,9 +1579,9 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         h->fso[i] = tot;
         tot += (parts[i]->size() + 31) & ~(size_t)31;
     }
-    const std::vector<int> *ip[3] = {&el, &src, &eslot};
+    const std::vector<int> *ip[4] = {&el, &src, &eslot, &fr};
     size_t itot = 0;
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < 4; i++) {
         h->fsi[i] = itot;
         itot += (ip[i]->size() + 63) & ~(size_t)63;
     }
@@ -1598,13 +1602,15 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     hipError_t e = hipSuccess;
     for (int i = 0; i < 5 && e == hipSuccess; i++)
         e = hipMemcpy((double *)h->d_fsT + h->fso[i], parts[i]->data(), parts[i]->size() * sizeof(double), hipMemcpyHostToDevice);
-    for (int i = 0; i < 3 && e == hipSuccess; i++)
-        e = hipMemcpy(h->d_fsI + h->fsi[i], ip[i]->data(), ip[i]->size() * sizeof(int), hipMemcpyHostToDevice);
+    for (int i = 0; i < 4 && e == hipSuccess; i++)
+        if (!ip[i]->empty())
+            e = hipMemcpy(h->d_fsI + h->fsi[i], ip[i]->data(), ip[i]->size() * sizeof(int), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(h->d_istep, 0, (size_t)h->batch * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * nslot);
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init lean tables");
     h->clf = true;
     h->clf_nslot = nslot;
+    h->clf_nfree = (int)fr.size();
     h->clf_epl = epl;
     h->clf_x1slot = x1slot;
     h->clf_sid = nmpc::ipm_structure<double>(fk);
@@ -1655,6 +1661,8 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     p.uinit = fT + h->fso[4];
     p.s_e = h->d_fsI + h->fsi[0];
     p.s_src = h->d_fsI + h->fsi[1];
+    p.s_free = h->d_fsI + h->fsi[3];
+    p.nfree = h->clf_nfree;
     p.vfull = (const double *)h->d_clv;
     p.txfull = (const double *)h->d_cltx;
     const char *m = (const char *)h->d_model;

@@ -672,47 +672,50 @@ __device__ __forceinline__ double plant_step(const ClFastParams<T> &p, const dou
     return xl;
 }
 
-// trajectory outputs of an instance's last solve (lanes over the (N+1) nz elements): z_0 from the
-// full tables plus the accepted active-set step (LDS), held bounds exact, bounded elements clamped;
-// a failed last step (status 4) outputs the initial point. x_0 in L.xs.
+// trajectory outputs of an instance's last solve: x_0 the state, the bounded elements the lane's slots
+// (z of the accepted solve — held bounds exact — clamped onto the bounds), the unbounded decision
+// elements (p.s_free) z_0 from the full tables plus the accepted active-set step W[:, S] nu; a failed
+// last step (status 4) outputs the initial point for every element. x_0 in L.xs.
 template <typename T, int NX, int NU, int EPL, class LdsT>
-__device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, int lane, int inst, int t, int status, int m)
+__device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, int inst, int t,
+                              int status, int m, const T (&zs)[EPL])
 {
     constexpr int NZ = NX + NU;
     const int N = p.N, ne = p.ne;
-#pragma unroll 1
-    for (int e = lane; e < ne; e += 64) {
+    auto put = [&](int e, T z) {
         const int k = e / NZ, r = e % NZ;
-        if (k == N && r >= NX) continue;
-        const T x0r = r < NX ? (T)L.xs[r] : T(0);
-        const int ty = k == 0 ? 0 : (k == N ? 2 : 1);
-        const T lb = p.lbnd[ty * NZ + r], ub = p.ubnd[ty * NZ + r];
-        T z;
-        if (status != 0) {
-            z = init_point(p, NX, NZ, k, r, t, x0r);
-        } else if (k == 0 && r < NX) {
-            z = x0r;
-        } else {
-            const T *tr = p.txfull + (size_t)e * NX;
-            T s0 = p.vfull[(size_t)t * ne + e], s1 = 0;
-#pragma unroll 1
-            for (int c = 0; c + 1 < NX; c += 2) {
-                s0 = fma(tr[c], (T)L.xs[c], s0);
-                s1 = fma(tr[c + 1], (T)L.xs[c + 1], s1);
-            }
-            if (NX % 2) s0 = fma(tr[NX - 1], (T)L.xs[NX - 1], s0);
-            z = s0 + s1;
-            int held = 0;
-            for (int i = 0; i < m; i++) {
-                z = fma(p.W[(size_t)L.se_e[i] * ne + e], (T)L.se_nu[i], z);
-                if (L.se_e[i] == e) held = L.se_s[i];
-            }
-            if (held) z = held < 0 ? lb : ub;
-            if (has_b(lb)) z = fmax(z, lb);
-            if (has_b(ub)) z = fmin(z, ub);
-        }
         if (r < NX) p.xout[((size_t)inst * (N + 1) + k) * NX + r] = z;
         else p.uout[((size_t)inst * N + k) * NU + (r - NX)] = z;
+    };
+    if (status != 0) {
+#pragma unroll 1
+        for (int e = lane; e < ne; e += 64) {
+            const int k = e / NZ, r = e % NZ;
+            if (k == N && r >= NX) continue;
+            put(e, init_point(p, NX, NZ, k, r, t, r < NX ? (T)L.xs[r] : T(0)));
+        }
+        return;
+    }
+    if (lane < NX) put(lane, (T)L.xs[lane]);
+#pragma unroll
+    for (int j = 0; j < EPL; j++) {
+        const int e = sv.e(j);
+        if (e >= 0) put(e, fmin(fmax(zs[j], (T)sv.lb(j)), (T)sv.ub(j)));
+    }
+#pragma unroll 1
+    for (int q = lane; q < p.nfree; q += 64) {
+        const int e = p.s_free[q];
+        const T *tr = p.txfull + (size_t)e * NX;
+        T s0 = p.vfull[(size_t)t * ne + e], s1 = 0;
+#pragma unroll
+        for (int c = 0; c + 1 < NX; c += 2) {
+            s0 = fma(tr[c], (T)L.xs[c], s0);
+            s1 = fma(tr[c + 1], (T)L.xs[c + 1], s1);
+        }
+        if (NX % 2) s0 = fma(tr[NX - 1], (T)L.xs[NX - 1], s0);
+        T z = s0 + s1;
+        for (int i = 0; i < m; i++) z = fma(p.W[(size_t)L.se_e[i] * ne + e], (T)L.se_nu[i], z);
+        put(e, z);
     }
 }
 
@@ -763,6 +766,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 
     const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
     const double wl = lane < p.ncl ? (double)p.wcl[lane] : 0.0;   // this lane's cost weight
+    double uin[NU];                                                // inputs of a failed step (mid-box)
+#pragma unroll
+    for (int i = 0; i < NU; i++) uin[i] = (double)p.uinit[i];
 
     // persistent wavefronts: each takes the next instance from the launch's work counter until none is
     // left (every wavefront reaches the exit; an instance's cost varies 10x with its active sets)
@@ -785,7 +791,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 fl |= (f < 0 ? 1u : (f > 0 ? 2u : 0u)) << (2 * j);
             }
         }
-        int t = (int)(((long long)p.offset[inst] + step) % p.period);
+        int t = (int)(((unsigned)p.offset[inst] % (unsigned)p.period + (unsigned)step % (unsigned)p.period) % (unsigned)p.period);
         double cost = 0.0, aed = 0.0;   // this lane's terms (component lane), summed over the wave at the end
         int nfail = 0, nst = 0;
         int last_status = step > 0 ? p.status[inst] : 0, last_iters = 0;
@@ -829,7 +835,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 z[j] = vt[j];
                 z1[j] = T(0);
             }
-#pragma unroll 1
+#pragma unroll
             for (int c = 0; c < NXP; c++) {
                 const double2 xx = *reinterpret_cast<const double2 *>(&L.xs[2 * c]);
 #pragma unroll
@@ -893,7 +899,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             const T z0c = fmin(fmax(z[0], (T)sv.lb(0)), (T)sv.ub(0));
             double u0[NU];
 #pragma unroll
-            for (int i = 0; i < NU; i++) u0[i] = status == 0 ? bcast((double)z0c, i) : (double)p.uinit[i];
+            for (int i = 0; i < NU; i++) u0[i] = status == 0 ? bcast((double)z0c, i) : uin[i];
             // ---- cost (controller.py:40-41) at x_0 = the state, or x_1 (jerk loop), and the AED numerator:
             // lane i adds component i
             {
@@ -916,7 +922,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             last_status = status;
             last_iters = iters;
             // ---- the trajectory outputs of the instance's last step of the run
-            if (step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, lane, inst, t, status, m_acc);
+            if (step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, t, status, m_acc, z);
             // ---- plant step + noise
             xl = plant_step<T, NX, NU, SP>(p, abl, cl, L.xs, xl, u0, w, lane);
             t = tn;

@@ -116,6 +116,8 @@ struct ClFastParams {
     signed char *flags;           // [B][nslot] the last solution's active flags (-1 lower, 1 upper)
     const double *noise;          // [B][noise_ld]
     const int *s_e, *s_src;       // [nslot] element index k nz + r; warm-start source slot (or -1)
+    const int *s_free;            // [nfree] the decision elements without a bound (outputs only)
+    int nfree;
     const T *s_lb, *s_ub;         // [nslot]
     const T *s_tx;                // [nslot][nx] rows of T_x
     const T *vb;                  // [period][EPL * 64] v_t at the slots
