@@ -155,7 +155,8 @@ class ClosedLoop:
     def iter_log(self):
         """Per-step solve record (env NMPC_ITER_LOG set before the run), each [steps, batch]: the fused
         kernels' last launch (NMPC_CL_FAST=0): (finish steps, IPM iterations, status); the lean loop's
-        last run (nmpc_cl_fast.hip): (active-set steps, status, clock cycles / 64 of the step)."""
+        last run (nmpc_cl_fast.hip): (active-set steps, status, wall-clock ticks of the step: wall_clock64,
+        100 MHz on MI355X)."""
         steps = int(self.lib.nmpc_closed_loop_iter_log(self.solver._h, None, 0))
         if steps <= 0:
             raise NmpcError("nmpc_closed_loop_iter_log: no log (set NMPC_ITER_LOG before the run)")

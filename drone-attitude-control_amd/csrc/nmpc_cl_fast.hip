@@ -777,6 +777,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         if (lane == 0) inst = atomicAdd(p.work, 1);
         inst = __builtin_amdgcn_readfirstlane(inst);
         if (inst >= p.B) break;
+        const long long inst_t0 = p.iter_log ? wall_clock64() : 0;
         int step = p.istep[inst];
         if (step >= p.target) continue;
         // lane-distributed state: lane i < NX holds x_i
@@ -806,7 +807,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         };
         fetch_v(t);
         for (; step < p.target; step++) {
-            const long long clk0 = p.iter_log ? clock64() : 0;
+            const long long clk0 = p.iter_log ? wall_clock64() : 0;
             T vt[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) vt[j] = vtn[j];
@@ -914,11 +915,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             }
             nfail += status != 0;
             nst++;
-            if (p.iter_log && lane == 0) {
-                const long long kc = (clock64() - clk0) >> 6;
-                p.iter_log[(size_t)(step - p.step0) * p.B + inst] =
-                    (iters < 255 ? iters : 255) | (status << 8) | ((int)(kc < 32767 ? kc : 32767) << 16);
-            }
             last_status = status;
             last_iters = iters;
             // ---- the trajectory outputs of the instance's last step of the run
@@ -926,6 +922,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             // ---- plant step + noise
             xl = plant_step<T, NX, NU, SP>(p, abl, cl, L.xs, xl, u0, w, lane);
             t = tn;
+            if (p.iter_log && lane == 0) {
+                const long long kc = wall_clock64() - clk0;   // constant-rate ticks (hipDeviceAttributeWallClockRate)
+                p.iter_log[(size_t)(step - p.step0) * p.B + inst] =
+                    (iters < 255 ? iters : 255) | (status << 8) | ((int)(kc < 32767 ? kc : 32767) << 16);
+            }
         }
         // ---- write back: state, sums, step, flags, status
         cost = wave_sum(cost);
@@ -950,6 +951,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         for (int j = 0; j < EPL; j++) {
             const int s = j * 64 + lane;
             if (s < p.nslot) p.flags[(size_t)inst * p.nslot + s] = flag_of(fl, j);
+        }
+        if (p.iter_log && lane == 0) {   // the instance's whole time in this launch (row p.target - p.step0)
+            const long long kc = wall_clock64() - inst_t0;
+            p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(kc < 0x7fffffff ? kc : 0x7fffffff);
         }
         CLF_SYNC();   // L.xs / L.fl of this instance are read before the next one overwrites them
     }

@@ -1,5 +1,5 @@
 """Lean closed loop step record (tuning aid, needs a GPU): runs the bench workload with NMPC_ITER_LOG and
-prints the distribution of per-step clock cycles and active-set steps, and the per-instance totals that
+prints the distribution of per-step wall time (ns) and active-set steps, and the per-instance totals that
 set a launch's time (the slowest wavefront).
 
     python tools/clf_steps.py --model force --batch 1024 --steps 20
@@ -32,14 +32,17 @@ def main():
     for _ in range(args.regions):
         cl.run(args.steps)
         it, st, kc = cl.iter_log()
-        cyc = kc.astype(np.int64) * 64
+        life = (it[-1].astype(np.int64) | (st[-1].astype(np.int64) << 8) | (kc[-1].astype(np.int64) << 16)) * 10
+        it, st, kc = it[:-1], st[:-1], kc[:-1]   # the last row: each instance's whole time in the launch
+        cyc = kc.astype(np.int64) * 10   # ns (wall_clock64 ticks at 100 MHz)
         tot = cyc.sum(0)
         worst = int(tot.argmax())
         q = lambda a: [float(np.percentile(a, x)) for x in (50, 90, 99, 99.9, 100)]
         out.append({"kernel_ms_per_step": cl.stats()["solve_kernel_ms"] / args.steps,
-                    "step_cycles_p50_90_99_999_max": q(cyc.ravel()),
-                    "instance_total_cycles_p50_90_99_max": q(tot)[:3] + [int(tot.max())],
-                    "worst_instance": worst, "worst_steps_cycles": cyc[:, worst].tolist(),
+                    "step_ns_p50_90_99_999_max": q(cyc.ravel()),
+                    "instance_total_ns_p50_90_99_max": q(tot)[:3] + [int(tot.max())],
+                    "instance_launch_ns_p50_90_99_max": q(life)[:3] + [int(life.max())],
+                    "worst_instance": worst, "worst_steps_ns": cyc[:, worst].tolist(),
                     "worst_steps_iters": it[:, worst].tolist(),
                     "iters_hist": np.bincount(np.minimum(it.ravel(), 40)).tolist()})
     print(json.dumps(out))
