@@ -634,10 +634,13 @@ __device__ __forceinline__ double plant_step(const ClFastParams<T> &p, const dou
         for (int i = 0; i < 4; i++) x4[i] = xs[i];
         const double inv_m = 1.0 / p.mass;
         double xn = xl;
+        // the converter hands the plant theta = atan2(Fx, Fz) and F_d = |F| (force_model/ocp.py:106-115,
+        // jerk_model/ocp.py:106-116) and the plant uses F_d sin(theta), F_d cos(theta)
+        // (force_model/dynamics.py:54-79): the composition is (Fx, Fz) itself, so the kernel passes the
+        // components with F_d = 1 (no atan2 / sin / cos; the oracle keeps the reference's operations, which
+        // agree to rounding)
         if (NX == 4) {
-            const double Fx = u0[0], Fz = u0[1];
-            const double th = atan2(Fx, Fz), Fd = sqrt(Fx * Fx + Fz * Fz);
-            const double s_ = sin(th), c_ = cos(th), h = p.dt;
+            const double s_ = u0[0], c_ = u0[1], Fd = 1.0, h = p.dt;
             double k1[4], k2[4], k3[4], k4[4], tt[4];
             crazyflie_rhs(x4, s_, c_, Fd, inv_m, p.g, k1);
             for (int i = 0; i < 4; i++) tt[i] = x4[i] + 0.5 * h * k1[i];
@@ -656,9 +659,7 @@ __device__ __forceinline__ double plant_step(const ClFastParams<T> &p, const dou
             for (int j = 0; j < p.substeps; j++) {
                 a0 = a0 + h0 * p.dt_conv;
                 a1 = a1 + h1 * p.dt_conv;
-                const double Fx = p.mass * a0, Fz = p.mass * a1;
-                const double th = atan2(Fx, Fz), Fd = sqrt(Fx * Fx + Fz * Fz);
-                crazyflie_rhs(x4, sin(th), cos(th), Fd, inv_m, p.g, f);
+                crazyflie_rhs(x4, p.mass * a0, p.mass * a1, 1.0, inv_m, p.g, f);
                 for (int i = 0; i < 4; i++) x4[i] += p.dt_conv * f[i];
             }
 #pragma unroll
