@@ -1714,7 +1714,7 @@ int clf_run(nmpc_solver *h, int steps)
     // env NMPC_ITER_LOG: the per-step record of the run (tuning aid, nmpc_closed_loop_iter_log)
     static const bool iter_log = std::getenv("NMPC_ITER_LOG") != nullptr;
     if (iter_log) {
-        const size_t cap = need + h->batch;   // + one row: each instance's time in the launch
+        const size_t cap = need + 2 * (size_t)h->batch;   // + two rows: each instance's start and end
         if (h->iter_log_cap < cap) {
             if (h->d_iter_log) hipFree(h->d_iter_log);
             h->d_iter_log = nullptr;
@@ -1722,7 +1722,7 @@ int clf_run(nmpc_solver *h, int steps)
             if (hipMalloc((void **)&h->d_iter_log, cap * sizeof(int)) == hipSuccess) h->iter_log_cap = cap;
         }
         fp.iter_log = h->d_iter_log;
-        h->iter_log_steps = h->d_iter_log ? steps + 1 : 0;   // + the instance-time row
+        h->iter_log_steps = h->d_iter_log ? steps + 2 : 0;   // + the instance start / end rows
     }
     int launches = 0;
     // one wavefront per instance at a time, as many as the device holds (persistent, cl_fast_launch)

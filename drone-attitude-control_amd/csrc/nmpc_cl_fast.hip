@@ -189,6 +189,47 @@ __device__ bool factor_set(const ClFastParams<T> &p, LdsT &L, int m, int lane)
     return pd;
 }
 
+// W_SS nu = t for the m elements in L.se_e by Gauss-Jordan elimination in registers: lane i holds row i
+// of W_SS (gathered with all its loads in flight) and t_i; pivot c's row reaches the other lanes by
+// readlane, every other row eliminates column c, so at the end nu_i = t_i / (row i's pivot). Pivots get
+// factor_set's regularisation (below 1e-9 of W_ii: + 1e-6 W_ii), i.e. the same regularised system the
+// Cholesky path solves. The diagonal W_ii goes to L.wdg (the multiplier test). pd: every W_ii > 0.
+template <typename T, int WSM, class LdsT>
+__device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, int m, int lane, double t, bool &pd)
+{
+    const int ne = p.ne;
+    double row[WSM];
+    const int ei = lane < m ? L.se_e[lane] : 0;
+#pragma unroll
+    for (int j = 0; j < WSM; j++) row[j] = (j < m && lane < m) ? (double)p.W[(size_t)L.se_e[j] * ne + ei] : 0.0;
+    double wii = 1.0;
+#pragma unroll
+    for (int j = 0; j < WSM; j++)
+        if (j == lane) wii = row[j];
+    if (lane < m) L.wdg[lane] = wii;
+    pd = true;
+#pragma unroll
+    for (int c = 0; c < WSM; c++) {
+        if (c >= m) break;
+        const double d0 = bcast(row[c], c), wcc = bcast(wii, c), tc = bcast(t, c);
+        pd = pd && wcc > 0.0;
+        const double d = d0 > 1e-9 * wcc ? d0 : fmax(d0, 0.0) + 1e-6 * wcc;
+        const double f = lane != c ? row[c] / d : 0.0;
+#pragma unroll
+        for (int j = c + 1; j < WSM; j++) {
+            if (j >= m) break;
+            row[j] = fma(-f, bcast(row[j], c), row[j]);
+        }
+        t = fma(-f, tc, t);
+        if (lane == c) row[c] = d;
+    }
+    double dd = 1.0;
+#pragma unroll
+    for (int j = 0; j < WSM; j++)
+        if (j == lane) dd = row[j];
+    return lane < m ? t / dd : 0.0;
+}
+
 // y = L^-1 y (forward) or L^-T y (backward) for the factor in L.wss, the vector lane-distributed (lane
 // i holds y_i, i < m; the pivot of each column broadcast by readlane)
 template <class LdsT>
@@ -347,9 +388,17 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         if (m > WSM) break;
         int pos[EPL];
         load_set<T, EPL, WSM>(L, sv, lane, wf, z0, pos);
-        if (!factor_set(p, L, m, lane)) break;
-        // nu = L^-T L^-1 (b - z_0)_S, lane i holding row i
-        const double y = solve_upper(L, m, lane, solve_lower(L, m, lane, lane < m ? L.se_t[lane] : 0.0));
+        // nu = W_SS^-1 (b - z_0)_S, lane i holding row i: Gauss-Jordan in registers for sets of up to 16,
+        // the LDS Cholesky beyond (the force model's sets up to 32: register rows of 32 would go to scratch)
+        bool pd = true;
+        double y;
+        if (WSM <= 16 || m <= 16) {
+            y = solve_set_gj<T, (WSM < 16 ? WSM : 16)>(p, L, m, lane, lane < m ? L.se_t[lane] : 0.0, pd);
+        } else {
+            pd = factor_set(p, L, m, lane);
+            y = solve_upper(L, m, lane, solve_lower(L, m, lane, lane < m ? L.se_t[lane] : 0.0));
+        }
+        if (!pd) break;
         // multiplier signs as displacements nu_i W_ii (lower: >= 0, upper: <= 0) to 1e-10 (1 + |b - z_0|)
         bool rmv = false;
         if (lane < m) {
@@ -953,9 +1002,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             const int s = j * 64 + lane;
             if (s < p.nslot) p.flags[(size_t)inst * p.nslot + s] = flag_of(fl, j);
         }
-        if (p.iter_log && lane == 0) {   // the instance's whole time in this launch (row p.target - p.step0)
-            const long long kc = wall_clock64() - inst_t0;
-            p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(kc < 0x7fffffff ? kc : 0x7fffffff);
+        if (p.iter_log && lane == 0) {   // the instance's start and end in this launch (rows target - step0 + 0 / 1,
+            // wall-clock ticks, low 31 bits)
+            p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(inst_t0 & 0x7fffffff);
+            p.iter_log[(size_t)(p.target - p.step0 + 1) * p.B + inst] = (int)(wall_clock64() & 0x7fffffff);
         }
         CLF_SYNC();   // L.xs / L.fl of this instance are read before the next one overwrites them
     }

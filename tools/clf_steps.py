@@ -32,8 +32,12 @@ def main():
     for _ in range(args.regions):
         cl.run(args.steps)
         it, st, kc = cl.iter_log()
-        life = (it[-1].astype(np.int64) | (st[-1].astype(np.int64) << 8) | (kc[-1].astype(np.int64) << 16)) * 10
-        it, st, kc = it[:-1], st[:-1], kc[:-1]   # the last row: each instance's whole time in the launch
+        raw = lambda r: it[r].astype(np.int64) | (st[r].astype(np.int64) << 8) | (kc[r].astype(np.int64) << 16)
+        t_start, t_end = raw(-2), raw(-1)           # the last two rows: each instance's start / end ticks
+        life = (t_end - t_start) * 10
+        rel0 = (t_start - t_start.min()) * 10
+        rel1 = (t_end - t_start.min()) * 10
+        it, st, kc = it[:-2], st[:-2], kc[:-2]
         cyc = kc.astype(np.int64) * 10   # ns (wall_clock64 ticks at 100 MHz)
         tot = cyc.sum(0)
         worst = int(tot.argmax())
@@ -42,6 +46,8 @@ def main():
                     "step_ns_p50_90_99_999_max": q(cyc.ravel()),
                     "instance_total_ns_p50_90_99_max": q(tot)[:3] + [int(tot.max())],
                     "instance_launch_ns_p50_90_99_max": q(life)[:3] + [int(life.max())],
+                    "instance_start_ns_from_first_p0_50_90_100": [float(np.percentile(rel0, x)) for x in (0, 50, 90, 100)],
+                    "instance_end_ns_from_first_p10_50_90_100": [float(np.percentile(rel1, x)) for x in (10, 50, 90, 100)],
                     "worst_instance": worst, "worst_steps_ns": cyc[:, worst].tolist(),
                     "worst_steps_iters": it[:, worst].tolist(),
                     "iters_hist": np.bincount(np.minimum(it.ravel(), 40)).tolist()})
