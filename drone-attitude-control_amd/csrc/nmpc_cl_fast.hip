@@ -271,6 +271,38 @@ __device__ T w_combo(const ClFastParams<T> &p, LdsT &L, const double *cf, int m,
     return acc;
 }
 
+// acc[j] += sum_i W[e_i][e_j] c_i at every slot j of the lane (padding slots untouched) for the m
+// elements in L.se_e with coefficients cf (LDS): the set in batches of QB, each batch's loads for all the
+// lane's slots in flight together (one memory latency per batch, not one per slot and batch); per slot
+// the sum runs in set order, as w_combo's
+template <typename T, int EPL, class LdsT>
+__device__ void w_combo_slots(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, const double *cf, int m,
+                              T (&acc)[EPL])
+{
+    constexpr int QB = EPL <= 2 ? 8 : (EPL <= 4 ? 4 : 2);
+    const int ne = p.ne;
+    int e[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; j++) e[j] = sv.e(j);
+    for (int i0 = 0; i0 < m; i0 += QB) {
+        T w[QB][EPL];
+#pragma unroll
+        for (int q = 0; q < QB; q++) {
+            const int row = i0 + q < m ? L.se_e[i0 + q] : 0;
+#pragma unroll
+            for (int j = 0; j < EPL; j++) w[q][j] = (i0 + q < m && e[j] >= 0) ? p.W[(size_t)row * ne + e[j]] : T(0);
+        }
+#pragma unroll
+        for (int q = 0; q < QB; q++)
+            if (i0 + q < m) {
+                const T c = (T)cf[i0 + q];
+#pragma unroll
+                for (int j = 0; j < EPL; j++)
+                    if (e[j] >= 0) acc[j] = fma(w[q][j], c, acc[j]);
+            }
+    }
+}
+
 // the set of flag bits wf in LDS in slot order (= element order): element, sign (-1 lower, 1 upper),
 // b - z_0, slot; pos[j] = the held slot's position in the set. Returns the set size (not written when
 // larger than WSM).
@@ -417,14 +449,14 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         double v[EPL];
         unsigned sgn = 0, nwf = wf;
 #pragma unroll
+        for (int j = 0; j < EPL; j++) z[j] = z0[j];
+        w_combo_slots<T, EPL>(p, L, sv, L.se_nu, m, z);
+#pragma unroll
         for (int j = 0; j < EPL; j++) {
             v[j] = 0.0;
             const int e = sv.e(j);
-            if (e < 0) {
-                z[j] = z0[j];
-                continue;
-            }
-            T zz = w_combo(p, L, L.se_nu, m, e, z0[j]);
+            if (e < 0) continue;
+            T zz = z[j];
             const unsigned f = (wf >> (2 * j)) & 3u;
             if (f) {
                 const T bb = f == 1u ? (T)sv.lb(j) : (T)sv.ub(j);
@@ -516,11 +548,7 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         if (m > 0) {
             if (lane < m) L.se_nu[lane] = nu;
             CLF_SYNC();
-#pragma unroll
-            for (int j = 0; j < EPL; j++) {
-                const int e = sv.e(j);
-                if (e >= 0) z[j] = w_combo(p, L, L.se_nu, m, e, z[j]);
-            }
+            w_combo_slots<T, EPL>(p, L, sv, L.se_nu, m, z);
             CLF_SYNC();
         }
     }
@@ -567,10 +595,14 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         if (t2 < INFINITY) {
             if (lane < m) L.se_nu[lane] = r_;
             CLF_SYNC();
+            T comb[EPL];
+#pragma unroll
+            for (int j = 0; j < EPL; j++) comb[j] = T(0);
+            w_combo_slots<T, EPL>(p, L, sv, L.se_nu, m, comb);
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 const int e = sv.e(j);
-                if (e >= 0) z[j] = fma((T)t, (T)sp * (p.W[(size_t)ep * ne + e] - w_combo(p, L, L.se_nu, m, e, T(0))), z[j]);
+                if (e >= 0) z[j] = fma((T)t, (T)sp * (p.W[(size_t)ep * ne + e] - comb[j]), z[j]);
             }
             CLF_SYNC();
         }
