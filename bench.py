@@ -177,7 +177,7 @@ def main():
             device = local_rank % max(1, torch.cuda.device_count())
             dist.init_process_group("gloo")
 
-    from drone_attitude_control_amd.batched import DEFAULT_N, ClosedLoop, flops_per_iter
+    from drone_attitude_control_amd.batched import DEFAULT_N, ClosedLoop
     from drone_attitude_control_amd.sharding import rank_workload, reduce_run
 
     model = args.model
@@ -290,9 +290,6 @@ def main():
                                          f"({pmc.get('source', 'none for this config')}); no x2 FETCH_SIZE "
                                          "correction: the kernel's loads are 4/8-B per lane, the guide's x2 is "
                                          "calibrated for 16-B streams; includes Infinity-Cache hits",
-                         "riccati_credit_frac": flops_per_iter(nx, nu, N) * B / (kernel_ms * 1e-3) / 1e12 / peak,
-                         "riccati_credit_note": "rounds 1-2's credit (one full Riccati factorisation, SURVEY 8d F_iter, "
-                                                "per step) for comparison only: the fast finish does not factor",
                          "gpu_mean_qp_iter": st["mean_qp_iter"]},
             "solve_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "QP solves/s",
                            "note": "solve kernel alone (median of the regions' mean launch durations, HIP events), "
