@@ -1677,7 +1677,6 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     p.status = h->d_status;
     p.iters = h->d_iters;
     p.park_count = h->d_park;
-    p.work = h->d_park + 1;
     p.park_list = h->d_park + 2;
     return p;
 }

@@ -230,6 +230,57 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, int m, int lan
     return lane < m ? t / dd : 0.0;
 }
 
+// solve_set_gj for sets of 17..32: two lanes per row — lane r < 32 holds columns 0..15 of row r, lane
+// r + 32 columns 16..31, t_r on both. Each pivot row goes through LDS (L.wss[0], free outside the
+// Cholesky path): its two lanes store it, every lane reads its half back (broadcast reads); W'(r, c)
+// comes from the lane holding that column by shuffle. The same eliminations and regularisation as
+// solve_set_gj.
+template <typename T, class LdsT>
+__device__ double solve_set_gj2(const ClFastParams<T> &p, LdsT &L, int m, int lane, double t, bool &pd)
+{
+    const int ne = p.ne, r = lane & 31, h = lane >> 5;
+    double row[16];
+    const int er = r < m ? L.se_e[r] : 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int col = 16 * h + k;
+        row[k] = (col < m && r < m) ? (double)p.W[(size_t)L.se_e[col] * ne + er] : 0.0;
+    }
+    double wv = 1.0;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if (16 * h + k == r) wv = row[k];
+    const double wii = __shfl(wv, r + 32 * (r >> 4));   // W_rr, from the half holding column r
+    if (lane < m) L.wdg[lane] = wii;
+    pd = true;
+    double piv = 1.0;
+    double *prow = &L.wss[0][0];
+#pragma unroll
+    for (int c = 0; c < 32; c++) {
+        if (c >= m) break;
+        const int pk = c & 15;
+        if (r == c) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) prow[16 * h + k] = row[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const double wrc = __shfl(row[pk], r + 32 * (c >> 4));
+        const double d0 = prow[c], wcc = bcast(wii, c), tc = bcast(t, c);
+        pd = pd && wcc > 0.0;
+        const double d = d0 > 1e-9 * wcc ? d0 : fmax(d0, 0.0) + 1e-6 * wcc;
+        const double f = (r != c && r < m) ? wrc / d : 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int col = 16 * h + k;
+            if (col > c && col < m) row[k] = fma(-f, prow[col], row[k]);
+        }
+        t = fma(-f, tc, t);
+        if (r == c) piv = d;
+        __builtin_amdgcn_wave_barrier();
+    }
+    return (h == 0 && r < m) ? t / piv : 0.0;
+}
+
 // y = L^-1 y (forward) or L^-T y (backward) for the factor in L.wss, the vector lane-distributed (lane
 // i holds y_i, i < m; the pivot of each column broadcast by readlane)
 template <class LdsT>
@@ -420,12 +471,15 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         if (m > WSM) break;
         int pos[EPL];
         load_set<T, EPL, WSM>(L, sv, lane, wf, z0, pos);
-        // nu = W_SS^-1 (b - z_0)_S, lane i holding row i: Gauss-Jordan in registers for sets of up to 16,
-        // the LDS Cholesky beyond (the force model's sets up to 32: register rows of 32 would go to scratch)
+        // nu = W_SS^-1 (b - z_0)_S, lane i holding row i: Gauss-Jordan in registers for sets of up to 16
+        // (one lane per row) and 32 (two lanes per row: register rows of 32 would go to scratch), the LDS
+        // Cholesky beyond
         bool pd = true;
         double y;
         if (WSM <= 16 || m <= 16) {
             y = solve_set_gj<T, (WSM < 16 ? WSM : 16)>(p, L, m, lane, lane < m ? L.se_t[lane] : 0.0, pd);
+        } else if (WSM >= 32 && m <= 32) {
+            y = solve_set_gj2<T>(p, L, m, lane, (lane & 31) < m ? L.se_t[lane & 31] : 0.0, pd);
         } else {
             pd = factor_set(p, L, m, lane);
             y = solve_upper(L, m, lane, solve_lower(L, m, lane, lane < m ? L.se_t[lane] : 0.0));
@@ -796,7 +850,15 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<
         }
         if (NX % 2) s0 = fma(tr[NX - 1], (T)L.xs[NX - 1], s0);
         T z = s0 + s1;
-        for (int i = 0; i < m; i++) z = fma(p.W[(size_t)L.se_e[i] * ne + e], (T)L.se_nu[i], z);
+        // W[S, e] nu in batches of 4 (the loads of a batch issued together)
+        for (int i0 = 0; i0 < m; i0 += 4) {
+            T wv[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) wv[q] = i0 + q < m ? p.W[(size_t)L.se_e[i0 + q] * ne + e] : T(0);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (i0 + q < m) z = fma(wv[q], (T)L.se_nu[i0 + q], z);
+        }
         put(e, z);
     }
 }
@@ -840,9 +902,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         sse[s] = v ? p.s_e[s] : -1;
         ssrc[s] = v ? p.s_src[s] : -1;
     }
+    __shared__ int wg_next;   // the workgroup's next instance (offset into its range)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
     if (lane < 32) L.xs[lane] = 0.0;
+    if (threadIdx.x == 0) wg_next = 0;
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
 
@@ -854,30 +918,41 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 
     // persistent wavefronts: each takes the next instance from the launch's work counter until none is
     // left (every wavefront reaches the exit; an instance's cost varies 10x with its active sets)
+    // persistent wavefronts: the workgroup owns a contiguous range of instances, its wavefronts take the
+    // next one from a counter in LDS until none is left (an instance's cost varies 10x with its active
+    // sets; a device-wide counter costs a far-memory atomic round trip of several microseconds per
+    // instance when thousands of wavefronts claim at once)
+    const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int wg_lo = (int)blockIdx.x * per_wg, wg_hi = min(p.B, wg_lo + per_wg);
     for (;;) {
-        int inst = 0;
-        if (lane == 0) inst = atomicAdd(p.work, 1);
-        inst = __builtin_amdgcn_readfirstlane(inst);
-        if (inst >= p.B) break;
+        int next = 0;
+        if (lane == 0) next = atomicAdd(&wg_next, 1);
+        const int inst = wg_lo + __builtin_amdgcn_readfirstlane(next);
+        if (inst >= wg_hi) break;
         const long long inst_t0 = p.iter_log ? wall_clock64() : 0;
+        // the instance's record, issued together: step, state (lane i < NX holds x_i), active flags of the
+        // last solution by slot (bit 2j lower, 2j+1 upper; meaningful after step 0), offset, status
         int step = p.istep[inst];
-        if (step >= p.target) continue;
-        // lane-distributed state: lane i < NX holds x_i
         double xl = lane < NX ? (double)p.state[(size_t)inst * NX + lane] : 0.0;
-        // active flags of the last solution by slot: bit 2j lower, 2j+1 upper
+        signed char fb[EPL];
+#pragma unroll
+        for (int j = 0; j < EPL; j++) {
+            const int s = j * 64 + lane;
+            fb[j] = s < p.nslot ? p.flags[(size_t)inst * p.nslot + s] : 0;
+        }
+        const unsigned off = (unsigned)p.offset[inst];
+        const int st_prev = p.status[inst];
+        if (step >= p.target) continue;
         unsigned fl = 0;
         if (step > 0) {
 #pragma unroll
-            for (int j = 0; j < EPL; j++) {
-                const int s = j * 64 + lane;
-                const signed char f = s < p.nslot ? p.flags[(size_t)inst * p.nslot + s] : 0;
-                fl |= (f < 0 ? 1u : (f > 0 ? 2u : 0u)) << (2 * j);
-            }
+            for (int j = 0; j < EPL; j++) fl |= (fb[j] < 0 ? 1u : (fb[j] > 0 ? 2u : 0u)) << (2 * j);
         }
-        int t = (int)(((unsigned)p.offset[inst] % (unsigned)p.period + (unsigned)step % (unsigned)p.period) % (unsigned)p.period);
+        int t = (int)((off % (unsigned)p.period + (unsigned)step % (unsigned)p.period) % (unsigned)p.period);
         double cost = 0.0, aed = 0.0;   // this lane's terms (component lane), summed over the wave at the end
         int nfail = 0, nst = 0;
-        int last_status = step > 0 ? p.status[inst] : 0, last_iters = 0;
+        int last_status = step > 0 ? st_prev : 0, last_iters = 0;
+        bool last_gi = false;   // the previous step of this launch ran the dual fallback
         bool parked = false;
         // v_t at the slots one step ahead (the step's first dependency); the reference component and the
         // noise draw are issued at the top of the step and consumed after the solve
@@ -932,6 +1007,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             for (int j = 0; j < EPL; j++) z[j] += z1[j];
             bool ok = false;
             int status = 0, iters = 1, m_acc = 0;
+            const bool gi_prev = last_gi;
+            last_gi = false;
             if (!__any(wf != 0)) {
                 bool bad = false;
 #pragma unroll
@@ -945,13 +1022,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 // and one more PDAS run solves and checks it; else the instance parks
                 // (an instance whose last solve failed tries the certificate first: infeasible QPs come in runs).
                 // The first PDAS run takes at most PDAS_ROUNDS rounds (its long runs are cycles, which the
-                // fallback resolves in a few steps), the run after the fallback polish_steps.
+                // fallback resolves in a few steps) — one round when the instance's previous step of this
+                // launch needed the fallback (saturation arcs: the shifted set is right or the fallback is
+                // needed again) — the run after the fallback polish_steps.
                 int r = 0, steps_ = 0;
                 unsigned wset = wf;
                 const bool cert_first = last_status == 4;
                 if (cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) status = 4;
                 for (int pass = 0; pass < 2 && status != 4; pass++) {
-                    r = wsteps_run<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, pass == 0 ? min(p.polish_steps, PDAS_ROUNDS) : p.polish_steps);
+                    const int rounds = pass == 1 ? p.polish_steps : (gi_prev ? 1 : min(p.polish_steps, PDAS_ROUNDS));
+                    r = wsteps_run<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, rounds);
                     steps_ += r >> 16;
                     if ((r & 1) || pass == 1) break;
                     if (!cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) {
@@ -959,6 +1039,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                         break;
                     }
                     int git = 0;
+                    last_gi = true;
                     const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git);
                     steps_ += git;
                     if (!found) break;
@@ -1094,7 +1175,8 @@ hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int
     } else if (nx == 6 && nu == 2) {
         launch_one<T, 6, 2, 5, 16, 8, 0, lpc::DenseStructure<6, 2>>(p, waves, s);
     } else if (nx == 4 && nu == 2) {
-        launch_one<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>(p, waves, s);
+        if (var == 1) launch_one<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>(p, waves, s);
+        else launch_one<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>(p, waves, s);
     } else {
         return hipErrorInvalidValue;
     }

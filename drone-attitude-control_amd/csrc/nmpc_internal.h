@@ -131,7 +131,6 @@ struct ClFastParams {
     T *xout, *uout;               // trajectories of the last solve (written at the last step)
     int *status, *iters;
     int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
-    int *work;                    // the next instance to take (persistent wavefronts; 0 at the launch)
     int *iter_log;                // optional [steps][B]: active-set steps (<= 255) | status << 8 | wall-clock ticks (<= 32767) << 16
 };
 // compiled fast kernels: EPL slots per lane (0 if none for this shape)

@@ -1544,6 +1544,8 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
         for (int b = 0; b < batch; b++) {
             double *st = state + (size_t)b * nx;
             signed char *ab = act ? act + (size_t)b * ne : NULL;
+            int gi_prev = 0;   /* the previous step of this call ran the dual fallback (a kernel launch's
+                                * register: one call here = one launch there) */
             for (int s = 0; s < steps; s++) {
                 const int step = step0 + s, t = (int)(((long long)offsets[b] + step) % c->period);
                 for (int k = 0; k < N; k++) memcpy(yref + (size_t)k * ny, c->table + (size_t)(t + k) * c->cols, sizeof(double) * ny);
@@ -1560,17 +1562,20 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                         for (int e = 0; e < ne; e++) nw += wf[e] != 0;
                         memcpy(w0, wf, (size_t)ne);   /* the warm set (the fallback's start) */
                         /* an instance whose last solve failed tries the certificate first (solve_one returns
-                         * status 4 for it); the first PDAS run takes at most PDAS_ROUNDS rounds */
+                         * status 4 for it); the first PDAS run takes at most PDAS_ROUNDS rounds, one after a
+                         * step that ran the fallback */
                         const int cert_first = failed && failed[b];
+                        const int r0 = gi_prev ? 1 : (d->polish_steps < PDAS_ROUNDS ? d->polish_steps : PDAS_ROUNDS);
+                        gi_prev = 0;
                         if (!(cert_first && infeasible_stage(d, st) > 0))
-                            ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax,
-                                             d->polish_steps < PDAS_ROUNDS ? d->polish_steps : PDAS_ROUNDS) > 0;
+                            ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, r0) > 0;
                         cnt[3] += wst;
                         /* not settled: unless the interval certificate proves the QP infeasible (solve_one
                          * returns that), the dual active-set fallback, its set then solved and checked by
                          * fast_finish */
                         if (!ok && infeasible_stage(d, st) == 0) {
                             int git = 0;
+                            gi_prev = 1;
                             if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
                                 ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
                                 cnt[3] += wst;

@@ -12,6 +12,11 @@ if [ "${VARIANTS:-0}" = "1" ]; then
   NMPC_CLF_VARIANT=1 run --model quad13 --batch 8192 --repeats 10 --oracle 0 || exit $?
   cp gpurun_out/${T}_quad13_8192.json gpurun_out/${T}_quad13_8192_v1.json
   run --model quad13 --batch 8192 --repeats 10 --oracle 0 || exit $?
+  for b in 1024 8192; do
+    cp gpurun_out/${T}_force_$b.json gpurun_out/${T}_force_${b}_v0.json
+    NMPC_CLF_DEBUG=1 NMPC_CLF_VARIANT=1 run --model force --batch $b --repeats 10 || exit $?
+    cp gpurun_out/${T}_force_$b.json gpurun_out/${T}_force_${b}_v1.json; cp gpurun_out/${T}_force_$b.err gpurun_out/${T}_force_${b}_v1.err
+  done
 fi
 if [ "${STEPS:-0}" = "1" ]; then
   for a in "force 1024" "quad13 8192" "jerk 4096"; do set -- $a
