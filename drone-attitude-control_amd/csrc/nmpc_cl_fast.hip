@@ -1093,12 +1093,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         cost = wave_sum(cost);
         aed = wave_sum(aed);
         if (lane < NX) p.state[(size_t)inst * NX + lane] = (T)xl;
+        if (lane < 4)   // lanes 0..3: [cost, AED numerator, failures, steps], added in the L2 (no return:
+                        // nothing waits for the old sums; each instance's sums have one writer)
+            unsafeAtomicAdd(p.acc + (size_t)inst * 4 + lane, lane == 0 ? cost : lane == 1 ? aed : lane == 2 ? (double)nfail : (double)nst);
         if (lane == 0) {
-            double *a = p.acc + (size_t)inst * 4;
-            a[0] += cost;
-            a[1] += aed;
-            a[2] += (double)nfail;
-            a[3] += (double)nst;
             p.istep[inst] = step;
             if (parked) {
                 const int pos = atomicAdd(p.park_count, 1);
