@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--mode", default="closed_loop", choices=["closed_loop", "solve"],
+                    help="closed_loop (default, the BASELINE metric): the batched closed loop; solve: the "
+                         "general batched nmpc_solve on per-instance yref windows (the reference's "
+                         "set(k,'yref') / solve() pattern, src/force_model/ocp.py:117-122, controller.py:32)")
     ap.add_argument("--repeats", type=int, default=10,
                     help="timed regions of --steps steps each; value = the median region (BASELINE.md: median of >= 10)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -126,9 +130,11 @@ def cpu_baseline(model, N, table, offsets, x_init, warmup, steps, seconds, preci
                             "sample": f"{n1} of those instances, the same steps, in {e1:.2f} s"}}, st["flops"] / solves
 
 
-def load_pmc(model, N, batch, precision, kernel):
-    """The committed rocprofv3 PMC summary entry (profiles/pmc_traffic.json) for this config and
-    solve kernel, if one matches: memory-side bytes per launch and MFMA instructions per launch."""
+def load_pmc(model, N, batch, precision, kernel, steps_per_launch, mode="closed_loop"):
+    """The committed rocprofv3 PMC summary entry (profiles/pmc_traffic.json) for this config, kernel
+    and launch length, if one matches: memory-side bytes per launch, executed FP64 flops and MFMA
+    instructions. An entry measured on launches of another length is refused (a launch's fixed costs —
+    the trajectory write-back, the per-instance record loads — are spread over its steps)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return {}
@@ -136,11 +142,20 @@ def load_pmc(model, N, batch, precision, kernel):
         d = json.load(open(path))
         for e in d.get("entries", []):
             if (e.get("model"), e.get("N"), e.get("batch"), e.get("precision")) == (model, N, batch, precision) \
-                    and e.get("kernel", kernel) == kernel:
+                    and e.get("kernel", kernel) == kernel and e.get("mode", "closed_loop") == mode \
+                    and e.get("steps_per_launch") == steps_per_launch:
                 return e
     except (ValueError, OSError):
         return {}
     return {}
+
+
+def min_bytes_per_instance_step(nx, nu, precision):
+    """Minimal algorithmic bytes of one closed-loop instance-step with the shared reference table:
+    x0 and the start offset (int32) in, u0 and x1 out ('with a shared reference table,
+    per-instance input drops to x0 + offset')."""
+    w = 8 if precision == "fp64" else 4
+    return (2 * nx + nu) * w + 4
 
 
 def python_loop_rate(N, steps):
@@ -159,8 +174,7 @@ def python_loop_rate(N, steps):
             "sample": f"{steps} steps of controllers.force_follow_trajectory (force, N={N}, B=1, fp64) in {el:.2f} s"}
 
 
-def main():
-    args = parse()
+def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -176,6 +190,35 @@ def main():
         else:
             device = local_rank % max(1, torch.cuda.device_count())
             dist.init_process_group("gloo")
+    return world, rank, dist, device
+
+
+def timing_block(regions, elapsed, note):
+    return {"regions": len(regions), "value_from": "median region",
+            "region_ms": [round(float(r) * 1e3, 4) for r in regions],
+            "spread": float((regions.max() - regions.min()) / elapsed),
+            "iqr_rel": float((np.percentile(regions, 75) - np.percentile(regions, 25)) / elapsed),
+            "note": note}
+
+
+def workload_label(model, tols, paths):
+    """config.workload: what the timed step runs, with the path mix of the CPU run of the same
+    algorithm over the same steps (None on multi-rank runs, which skip the CPU baseline)."""
+    mix = ("path mix not measured in this run (the CPU baseline, which counts it, runs at N=1 only)" if paths is None
+           else f"of the solves {paths['fast_unconstrained']:.2%} the explicit unconstrained solution, "
+                f"{paths['fast_set']:.2%} warm-started active-set steps on W (incl. the dual active-set fallback), "
+                f"{paths['full']:.3%} the full IPM + exact finish, {paths['failed']:.3%} certified infeasible "
+                f"(status 4) — counted by the CPU run of the same algorithm over the timed steps")
+    return (f"{model} closed-loop NMPC step on the lean loop (cl_fast_kernel): yref window from the shared "
+            f"reference table + x0 pin + the QP solved to its exact, KKT-checked solution ({mix}; "
+            f"full-solve options tol_comp {tols[0]:g}, tol_res {tols[1]:g}) + plant/noise advance + cost/AED")
+
+
+def main():
+    args = parse()
+    world, rank, dist, device = init_dist(args)
+    if args.mode == "solve":
+        return main_solve(args, world, rank, dist, device)
 
     from drone_attitude_control_amd.batched import DEFAULT_N, ClosedLoop
     from drone_attitude_control_amd.sharding import rank_workload, reduce_run
@@ -202,7 +245,7 @@ def main():
             dist.barrier()
 
     cl.run(args.warmup, sync=True)
-    regions, kernel_ms_r = [], []
+    regions, kernel_ms_r, parked = [], [], 0
     for _ in range(max(1, args.repeats)):
         barrier()
         t0 = time.perf_counter()
@@ -211,7 +254,8 @@ def main():
         barrier()
         regions.append(t1 - t0)
         st = cl.stats()
-        # solve-kernel time per closed-loop step (a fused launch carries all the region's steps)
+        parked += st["parked"]
+        # closed-loop kernel time per step (a launch carries up to 64 of the region's steps)
         kernel_ms_r.append(st["solve_kernel_ms"] / max(1, st["steps"]))
     regions = np.array(regions)
     st = cl.stats()
@@ -238,10 +282,13 @@ def main():
         peak = PEAK_TFLOPS[args.precision]
         info = cl.solver.launch_info()
         kernel = info["closed_loop_kernel"] if info["closed_loop_kernel"] != "fused" else info["kernel"]
-        pmc = load_pmc(model, N, B, args.precision, kernel)
+        spl = min(args.steps, 64)   # steps per launch of the timed regions (clf_run / fused chunks)
+        pmc = load_pmc(model, N, B, args.precision, kernel, spl)
         headline = model == "quad13" and N == 20
         metric = ("NMPC steps/sec (batched trajectories), N=20 nx=13 nu=4, 1/2/4/8 MI355X" if headline else
                   f"NMPC steps/sec (batched trajectories), N={N} nx={nx} nu={nu} ({model}), 1/2/4/8 MI355X")
+        min_b = min_bytes_per_instance_step(nx, nu, args.precision) * B
+        traffic = pmc.get("hbm_bytes_per_step")
         line = {
             "metric": metric,
             "value": value,
@@ -255,18 +302,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "fp64" else "f32",
             "data": "synthetic (seeded closed-loop Monte-Carlo instances on the reference circle)",
-            "config": {"workload": f"{model} closed-loop NMPC step: yref window + x0 pin + IPM solve "
-                                   f"(tol_comp {tols[0]:g}, tol_res {tols[1]:g}, exact finish from mu <= {tols[2]:g}, <= {tols[3]} active-set steps) + plant/noise advance",
+            "config": {"workload": workload_label(model, tols, cpu and cpu.get("paths_per_step")),
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"instance-sharded x{world}, "
                                                                     f"{'gloo' if args.dist_backend == 'gloo' else 'RCCL'} stats reduce",
-                       "instances_per_wave": info["instances_per_wave"]},
-            "timing": {"regions": len(regions), "steps_per_region": args.steps, "value_from": "median region",
-                       "region_ms": [round(float(r) * 1e3, 4) for r in regions],
-                       "spread": float((regions.max() - regions.min()) / elapsed),
-                       "iqr_rel": float((np.percentile(regions, 75) - np.percentile(regions, 25)) / elapsed),
-                       "note": "each region is one fused launch whose time is set by its slowest wavefront; "
-                               "region-to-region differences below the IQR are not resolved"},
+                       "instances_per_wave": info["instances_per_wave"], "steps_per_launch": spl},
+            "timing": dict(timing_block(regions, elapsed, "each region is one closed-loop launch of --steps steps whose "
+                                                          "time is set by its slowest wavefront; region-to-region "
+                                                          "differences below the IQR are not resolved"),
+                           steps_per_region=args.steps),
             "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32",
                          "pipe": ("FP64 FMA on the VALU" if args.precision == "fp64" else "FP32 FMA on the VALU")
                          + " (MI355X: FP64 matrix peak = FP64 vector peak; FP32 matrix peak = FP32 vector peak)",
@@ -281,23 +325,146 @@ def main():
                          "executed_frac": (pmc["fp64_flops_per_step"] / (kernel_ms * 1e-3) / 1e12 / peak
                                            if pmc.get("fp64_flops_per_step") else None),
                          "executed_note": "FP64 flops the kernel issues (64 x SQ_INSTS_VALU_FLOPS_FP64 per step, idle "
-                                          f"lanes included; {pmc.get('source', 'no PMC pass for this config')}) / this "
-                                          "run's kernel time / peak",
+                                          f"lanes included; {pmc.get('source', 'no PMC pass for this config and launch length')}) "
+                                          "/ this run's kernel time / peak",
                          "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
-                         "traffic": pmc.get("hbm_bytes_per_step", pmc.get("hbm_bytes_per_launch")),
-                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per closed-loop step (per launch / fused steps per "
-                                         "launch) from the committed rocprofv3 PMC pass "
-                                         f"({pmc.get('source', 'none for this config')}); no x2 FETCH_SIZE "
-                                         "correction: the kernel's loads are 4/8-B per lane, the guide's x2 is "
-                                         "calibrated for 16-B streams; includes Infinity-Cache hits",
+                         "traffic": traffic,
+                         "min_bytes_per_step": min_b,
+                         "traffic_vs_min_bytes": traffic / min_b if traffic else None,
+                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per closed-loop step (per launch / steps per launch) "
+                                         f"from the committed rocprofv3 PMC pass on launches of {spl} steps "
+                                         f"({pmc.get('source', 'none for this config and launch length')}); no x2 "
+                                         "FETCH_SIZE correction: the kernel's loads are 4/8-B per lane, the guide's x2 "
+                                         "is calibrated for 16-B streams; includes Infinity-Cache hits. min_bytes: x0 + "
+                                         "offset in, u0 + x1 out per instance (shared reference table)",
                          "gpu_mean_qp_iter": st["mean_qp_iter"]},
-            "solve_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "QP solves/s",
-                           "note": "solve kernel alone (median of the regions' mean launch durations, HIP events), "
-                                   "all ranks"},
+            "kernel_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "NMPC steps/s",
+                            "note": "closed-loop kernel time only (median of the regions' launch durations, HIP "
+                                    "events; plant, cost and instance bookkeeping included), all ranks. Not a "
+                                    "QP-solve rate: the general solve on per-instance windows is bench.py --mode solve"},
+            "parked_solves": int(parked),
             "cpu_baseline": cpu,
             "closed_loop": {"mean_cost_per_step": red[0] / max(1.0, red[3]),
                             "aed": red[1] / max(1.0, red[3]) / (2 if model != "quad13" else 3),
                             "failed_solves": int(red[2]), "instance_steps": int(red[3])},
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main_solve(args, world, rank, dist, device):
+    """--mode solve: the general batched solve (nmpc_solve_async on the handle's device buffers) of B
+    QPs per GPU with per-instance yref windows staged in HBM — what the reference's per-step pattern
+    (set(k, 'yref') for every stage, set(0, 'lbx'/'ubx'), solve(); src/force_model/ocp.py:117-122,
+    controller.py:29-32) hits, with no shared reference table and no warm start: every QP is solved
+    cold by the full IPM + exact finish (ipm_lpc_kernel / ipm_kernel). The QPs are the closed loop's
+    first-step QPs of the bench workload (batched.first_step_qps). A step = one batched solve."""
+    from drone_attitude_control_amd.acados import AcadosOcpSolver
+    from drone_attitude_control_amd.batched import DEFAULT_N, first_step_qps, flops_per_iter
+    from drone_attitude_control_amd.models import OCPS
+    from drone_attitude_control_amd.sharding import rank_workload, reduce_run
+
+    model = args.model
+    N = args.horizon or DEFAULT_N[model]
+    B = args.batch
+    table, offsets_r, x_r, _ = rank_workload(model, N, B, world, rank, args.seed)
+    x0, Y = first_step_qps(model, N, table, offsets_r, x_r)
+    ocp = OCPS[model](N)
+    s = AcadosOcpSolver(ocp, batch=B, device=device if world > 1 else 0, precision=args.precision)
+    s.set_batch("x0", x0)
+    s.set_batch("yref", Y)
+    s.solve()                                   # uploads the windows once; they stay resident in HBM
+    nx, nu = s.nx, s.nu
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cref, models
+        ref = cref.RiccatiIpmRef.for_options(models.MODELS[model](N), ocp.solver_options, args.precision)
+        n0 = min(B, 256)
+        t0 = time.perf_counter()
+        ref.solve(x0[:n0], Y[:n0])
+        el0 = time.perf_counter() - t0
+        n = int(min(B, max(n0, n0 / max(el0, 1e-6) * args.cpu_seconds)))
+        t0 = time.perf_counter()
+        _, _, st_c, it_c = ref.solve(x0[:n], Y[:n])
+        el = time.perf_counter() - t0
+        n1 = min(n, 128)
+        t1 = time.perf_counter()
+        ref.solve(x0[:n1], Y[:n1], nthreads=1)
+        e1 = time.perf_counter() - t1
+        cpu = {"value": n / el, "unit": "QP solves/s", "cores": ref.max_threads(), "kind": "port",
+               "sample": f"{n} of the {B} QPs in {el:.2f} s: oracle/c/riccati_ipm.c riccati_ipm_solve_batch (the same "
+                         f"cold IPM + exact finish, fp64), OpenMP over instances",
+               "mean_newton_systems": float(np.mean(it_c)), "failed": int((st_c != 0).sum()),
+               "single_core": {"value": n1 / e1, "cores": 1, "sample": f"{n1} QPs in {e1:.2f} s"}}
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(max(1, args.warmup)):
+        s.solve_async()
+    s.synchronize()
+    regions, kms = [], []
+    for _ in range(max(1, args.repeats)):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            s.solve_async()
+        s.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        regions.append(t1 - t0)
+        kms.append(s.get_stats("time_tot") * 1e3)   # the region's last launch (HIP events)
+    status = s.get_batch_int("status")
+    iters = s.get_batch_int("qp_iter")
+    red, regions, kms = reduce_run(dist, np.array([float((status != 0).sum()), float(iters.sum()), float(B)]),
+                                   np.array(regions), np.array(kms),
+                                   device="cuda" if dist is not None and args.dist_backend == "nccl" else None)
+    regions, kms = np.atleast_1d(regions), np.atleast_1d(kms)
+    med = int(np.argsort(regions)[len(regions) // 2])
+    elapsed = float(regions[med])
+    kernel_ms = float(np.median(kms))
+    if rank == 0:
+        info = s.launch_info()
+        n_newton = cpu["mean_newton_systems"] if cpu else float(red[1] / max(1.0, red[2]))
+        fl_solve = flops_per_iter(nx, nu, N) * n_newton
+        achieved = fl_solve * B / (kernel_ms * 1e-3) / 1e12
+        peak = PEAK_TFLOPS[args.precision]
+        pmc = load_pmc(model, N, B, args.precision, info["kernel"], 1, mode="solve")
+        line = {
+            "metric": f"QP solves/sec (batched nmpc_solve, per-instance yref windows), N={N} nx={nx} nu={nu} ({model})",
+            "value": world * B * args.steps / elapsed,
+            "unit": "QP solves/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64" if args.precision == "fp64" else "f32",
+            "data": "synthetic (the bench workload's first-step QPs, per-instance yref windows)",
+            "config": {"workload": f"{model} batched cold QP solve: {B} independent QPs per GPU, each with its own "
+                                   f"stage-stacked yref window and x0 resident in HBM; full Mehrotra IPM + exact "
+                                   f"active-set finish, no shared table, no warm start ({info['kernel']})",
+                       "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"instance-sharded x{world}", "instances_per_wave": info["instances_per_wave"]},
+            "timing": dict(timing_block(regions, elapsed, "each region enqueues --steps batched solves back to back"),
+                           steps_per_region=args.steps),
+            "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32", "kernel": info["kernel"],
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                         "credit": "SURVEY 8d F_iter (one Riccati factorisation + predictor/corrector sweeps + box "
+                                   "elementwise per Newton system) x the CPU baseline's mean Newton systems per QP on "
+                                   "the same QPs x B / kernel time",
+                         "flops_per_solve": fl_solve, "kernel_ms": kernel_ms,
+                         "executed_fp64_flops_per_step": pmc.get("fp64_flops_per_step"),
+                         "traffic": pmc.get("hbm_bytes_per_step"),
+                         "min_bytes_per_step": float(B * (nx + N * (nx + nu) + nx + N * nu + (N + 1) * nx)
+                                                     * (8 if args.precision == "fp64" else 4)),
+                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per batched solve from the committed PMC pass "
+                                         f"({pmc.get('source', 'none for this config')}); min bytes = x0 + yref window "
+                                         "in, full x/u trajectories out (SURVEY 8d)",
+                         "gpu_mean_qp_iter": float(red[1] / max(1.0, red[2]))},
+            "failed_solves": int(red[0]),
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     if dist is not None:

@@ -136,13 +136,13 @@ class ClosedLoop:
             raise NmpcError(f"nmpc_closed_loop_run: {self.lib.nmpc_last_error(self.solver._h).decode()}")
 
     def stats(self):
-        out = np.zeros(8)
-        rc = self.lib.nmpc_closed_loop_stats(self.solver._h, _lib.dptr(out), 8)
+        out = np.zeros(10)
+        rc = self.lib.nmpc_closed_loop_stats(self.solver._h, _lib.dptr(out), 10)
         if rc != 0:
             raise NmpcError(f"nmpc_closed_loop_stats: {self.lib.nmpc_last_error(self.solver._h).decode()}")
         return {"cost_sum": out[0], "aed_sum": out[1], "failed": out[2], "instance_steps": out[3],
                 "solve_kernel_ms": out[4], "solve_launches": int(out[5]), "mean_qp_iter": out[6],
-                "steps": int(out[7])}
+                "steps": int(out[7]), "parked": int(out[8]), "fast_launches": int(out[9])}
 
     def instance_stats(self):
         """Per-instance [cost sum, AED numerator, failed solves, steps] (batch x 4)."""

@@ -228,6 +228,8 @@ struct nmpc_solver {
     int clf_nfree = 0;
     int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
+    int clf_resident = 0;                  // workgroups of cl_fast_kernel the handle's device holds at once
+    int clf_parked = 0, clf_rounds = 0;    // the last run: parked solves (list-mode full solves), fast launches
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
@@ -596,16 +598,23 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     if (cl_steps > 0) {
         p.cl = cl_params<T>(h);
         p.cl_noise = h->d_fnoise;
+        // env NMPC_ITER_LOG: the fused launch's step record. The list mode (the lean loop's fallback)
+        // neither writes nor resizes it: the lean loop's own log (clf_run) stays as that run left it
         static const bool iter_log = std::getenv("NMPC_ITER_LOG") != nullptr;
-        if (iter_log && !h->d_iter_log &&
-            hipMalloc((void **)&h->d_iter_log, (size_t)h->batch * CL_FUSED_CHUNK * sizeof(int)) != hipSuccess)
-            h->d_iter_log = nullptr;
-        if (h->d_iter_log && h->iter_log_cap < (size_t)h->batch * CL_FUSED_CHUNK) h->iter_log_cap = (size_t)h->batch * CL_FUSED_CHUNK;
-        p.iter_log = iter_log && !la ? h->d_iter_log : nullptr;
+        if (iter_log && !la) {
+            const size_t need = (size_t)h->batch * CL_FUSED_CHUNK;
+            if (h->iter_log_cap < need) {   // the capacity is set only where the allocation happens
+                if (h->d_iter_log) hipFree(h->d_iter_log);
+                h->d_iter_log = nullptr;
+                h->iter_log_cap = 0;
+                if (hipMalloc((void **)&h->d_iter_log, need * sizeof(int)) == hipSuccess) h->iter_log_cap = need;
+            }
+            p.iter_log = h->d_iter_log;
+            h->iter_log_steps = p.iter_log ? cl_steps : 0;
+        }
         const bool no_expl = std::getenv("NMPC_EXPLICIT") && std::getenv("NMPC_EXPLICIT")[0] == '0';
         p.cl_tx = no_expl ? nullptr : (const T *)h->d_cltx;
         p.cl_v = no_expl ? nullptr : (const T *)h->d_clv;
-        h->iter_log_steps = p.iter_log ? cl_steps : 0;
     }
     p.B = h->batch;
     p.N = h->N;
@@ -1608,6 +1617,9 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     if (e == hipSuccess) e = hipMemset(h->d_istep, 0, (size_t)h->batch * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * nslot);
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init lean tables");
+    // resident workgroups on this handle's device (nmpc_closed_loop_init runs on it: hipSetDevice above)
+    h->clf_resident = nmpc::cl_fast_resident(nx, nu, nmpc::ipm_structure<double>(fk), h->device);
+    if (h->clf_resident <= 0) return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_init: lean closed-loop occupancy query");
     h->clf = true;
     h->clf_nslot = nslot;
     h->clf_nfree = (int)fr.size();
@@ -1678,6 +1690,10 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     p.iters = h->d_iters;
     p.park_count = h->d_park;
     p.park_list = h->d_park + 2;
+    // env NMPC_CLF_NO_GI=1 (test knob): no dual active-set fallback, so every step whose PDAS run does
+    // not settle parks and takes the list-mode full solve (tests/test_gpu_bench_parity.py forces parks)
+    const char *nogi = std::getenv("NMPC_CLF_NO_GI");
+    p.gi = (nogi && nogi[0] == '1') ? 0 : 1;
     return p;
 }
 
@@ -1691,27 +1707,29 @@ hipEvent_t cl_event(nmpc_solver *h, size_t i)
     return h->cl_events[i];
 }
 
-// `steps` closed-loop steps on the lean loop: noise draws of the run, then rounds of (fast kernel
-// over every instance up to the target step; the count of parked instances back to the host; one
-// full solve + plant step per parked instance, ipm_lpc_kernel in list mode) until none is parked.
-// Returns the number of kernel launches (each bracketed by an event pair), or < 0.
+constexpr int CLF_CHUNK = 64;   // closed-loop steps per lean-loop launch (bounded noise / log buffers)
+
+// `steps` closed-loop steps on the lean loop, in chunks of at most CLF_CHUNK steps: per chunk the noise
+// draws, then rounds of (fast kernel over every instance up to the chunk's target step; the count of
+// parked instances back to the host — the one host wait per round; one full solve + plant step per
+// parked instance, ipm_lpc_kernel in list mode) until none is parked. Returns the number of kernel
+// launches (each bracketed by an event pair), or < 0. h->clf_parked / clf_rounds: the run's parked
+// solves and fast launches.
 int clf_run(nmpc_solver *h, int steps)
 {
-    const int target = h->cl_step + steps;
-    const size_t need = (size_t)h->batch * steps;
+    const size_t need = (size_t)h->batch * std::min(steps, CLF_CHUNK);
     if (h->fnoise_cap < need) {
         if (h->d_fnoise) hipFree(h->d_fnoise);
         h->d_fnoise = nullptr;
+        h->fnoise_cap = 0;
         if (hipMalloc((void **)&h->d_fnoise, need * sizeof(double)) != hipSuccess)
             return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: noise buffer");
         h->fnoise_cap = need;
     }
-    nmpc::ClParams<double> cp = cl_params<double>(h);
-    hipError_t e = nmpc::cl_noise_launch<double>(cp, h->cl_step, steps, h->d_fnoise, h->stream);
-    if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
-    nmpc::ClFastParams<double> fp = clf_params(h, target, h->cl_step, steps);
-    // env NMPC_ITER_LOG: the per-step record of the run (tuning aid, nmpc_closed_loop_iter_log)
+    // env NMPC_ITER_LOG: the per-step record of the run's last chunk (tuning aid, nmpc_closed_loop_iter_log);
+    // filled with -1 first, so the rows of steps the list-mode fallback solved read as that marker
     static const bool iter_log = std::getenv("NMPC_ITER_LOG") != nullptr;
+    static const bool dbg = std::getenv("NMPC_CLF_DEBUG") != nullptr;
     if (iter_log) {
         const size_t cap = need + 2 * (size_t)h->batch;   // + two rows: each instance's start and end
         if (h->iter_log_cap < cap) {
@@ -1720,44 +1738,69 @@ int clf_run(nmpc_solver *h, int steps)
             h->iter_log_cap = 0;
             if (hipMalloc((void **)&h->d_iter_log, cap * sizeof(int)) == hipSuccess) h->iter_log_cap = cap;
         }
-        fp.iter_log = h->d_iter_log;
-        h->iter_log_steps = h->d_iter_log ? steps + 2 : 0;   // + the instance start / end rows
     }
     int launches = 0;
-    // one wavefront per instance at a time, as many as the device holds (persistent, cl_fast_launch)
-    const int waves = h->batch;
-    for (int round = 0; round <= steps; round++) {
-        if ((e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
-        hipEventRecord(cl_event(h, 2 * launches), h->stream);
-        e = nmpc::cl_fast_launch<double>(h->nx, h->nu, h->clf_sid, fp, waves, h->stream);
-        hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
-        launches++;
-        if (e != hipSuccess) return hip_fail(h, e, "lean closed-loop kernel launch");
-        int parked = 0;
-        e = hipMemcpyAsync(&parked, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-        if (e != hipSuccess) return hip_fail(h, e, "lean closed loop (fast kernel)");
-        static const bool dbg = std::getenv("NMPC_CLF_DEBUG") != nullptr;
-        if (dbg) std::fprintf(stderr, "[nmpc clf] steps %d..%d round %d: %d parked\n", h->cl_step, target, round, parked);
-        if (parked <= 0) break;
-        // the fallback: one full solve + plant step for every parked instance
-        const ListArgs la{parked, h->cl_step, steps};
-        const int r = launch<double>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
-        launches++;
-        if (r < 0) return r;
-        if (dbg && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "lean closed loop (list-mode fallback)");
+    h->clf_parked = h->clf_rounds = 0;
+    for (int done = 0; done < steps;) {
+        const int n = std::min(CLF_CHUNK, steps - done), target = h->cl_step + n;
+        nmpc::ClParams<double> cp = cl_params<double>(h);
+        hipError_t e = nmpc::cl_noise_launch<double>(cp, h->cl_step, n, h->d_fnoise, h->stream);
+        if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
+        nmpc::ClFastParams<double> fp = clf_params(h, target, h->cl_step, n);
+        if (iter_log && h->d_iter_log) {
+            const size_t rows = (size_t)(n + 2) * h->batch;
+            if ((e = hipMemsetAsync(h->d_iter_log, 0xff, rows * sizeof(int), h->stream)) != hipSuccess)
+                return hip_fail(h, e, "iter log reset");
+            fp.iter_log = h->d_iter_log;
+            h->iter_log_steps = n + 2;   // + the instance start / end rows
+        }
+        for (int round = 0; round <= n; round++) {
+            if ((e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
+            hipEventRecord(cl_event(h, 2 * launches), h->stream);
+            e = nmpc::cl_fast_launch<double>(h->nx, h->nu, h->clf_sid, fp, h->batch, h->clf_resident, h->stream);
+            hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
+            launches++;
+            h->clf_rounds++;
+            if (e != hipSuccess) return hip_fail(h, e, "lean closed-loop kernel launch");
+            int parked = 0;
+            e = hipMemcpyAsync(&parked, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+            if (e != hipSuccess) return hip_fail(h, e, "lean closed loop (fast kernel)");
+            if (dbg) std::fprintf(stderr, "[nmpc clf] steps %d..%d round %d: %d parked\n", h->cl_step, target, round, parked);
+            if (parked <= 0) break;
+            h->clf_parked += parked;
+            // the fallback: one full solve + plant step for every parked instance
+            const ListArgs la{parked, h->cl_step, n};
+            const int r = launch<double>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
+            launches++;
+            if (r < 0) return r;
+            if (dbg && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "lean closed loop (list-mode fallback)");
+        }
+        h->cl_step = target;
+        done += n;
     }
-    static const bool dbg = std::getenv("NMPC_CLF_DEBUG") != nullptr;
     if (dbg && hipStreamSynchronize(h->stream) == hipSuccess)
         for (int i = 0; i < launches; i++) {
             float ms = 0.f, gap = 0.f;
             hipEventElapsedTime(&ms, cl_event(h, 2 * i), cl_event(h, 2 * i + 1));
             if (i + 1 < launches) hipEventElapsedTime(&gap, cl_event(h, 2 * i + 1), cl_event(h, 2 * i + 2));
-            std::fprintf(stderr, "[nmpc clf] steps %d..%d launch %d (%s): %.4f ms, then %.4f ms to the next\n", h->cl_step,
-                         target, i, i % 2 ? "list-mode full solve" : "fast", ms, gap);
+            std::fprintf(stderr, "[nmpc clf] run of %d steps, launch %d: %.4f ms, then %.4f ms to the next\n", steps, i, ms, gap);
         }
-    h->cl_step = target;
     return launches;
+}
+
+// the lean loop keeps each instance's step and warm-start flags on the device (d_istep, d_flags); a run
+// on another path (NMPC_CL_FUSED=0 / per-step launches) advances every instance to h->cl_step without
+// them, so they are resynchronised after it: istep = cl_step for every instance, flags cleared (the
+// warm start only steers the active-set path, the certified solutions do not depend on it)
+int clf_resync(nmpc_solver *h)
+{
+    if (!h->clf) return 0;
+    std::vector<int> st((size_t)h->batch, h->cl_step);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipMemcpy(h->d_istep, st.data(), st.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * h->clf_nslot);
+    return e == hipSuccess ? 0 : hip_fail(h, e, "lean closed loop resync");
 }
 
 }  // namespace
@@ -1882,8 +1925,10 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
     h->iter_log_steps = 0;   // the log describes the last fused launch of this run only
     int launches = 0;
     const char *fused_env = std::getenv("NMPC_CL_FUSED");
-    if (h->clf && steps > 0 && !(fused_env && fused_env[0] == '0')) {
-        launches = clf_run(h, steps);
+    const bool lean = h->clf && !(fused_env && fused_env[0] == '0');
+    h->clf_parked = h->clf_rounds = 0;
+    if (lean) {
+        launches = steps > 0 ? clf_run(h, steps) : 0;
         if (launches < 0) return launches;
     } else if (cl_fused(h)) {
         if (h->fnoise_cap < (size_t)h->batch * CL_FUSED_CHUNK) {
@@ -1905,6 +1950,10 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
             if (r < 0) return r;
         }
     }
+    if (!lean && steps > 0) {
+        const int r = clf_resync(h);
+        if (r < 0) return r;
+    }
     h->cl_last_launches = launches;
     h->cl_last_steps = steps;
     // the loop rewrote the device x0 / yref: the next nmpc_solve re-uploads the host-staged inputs
@@ -1925,7 +1974,7 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_stats");
     std::vector<double> acc((size_t)h->batch * 4);
     hipMemcpy(acc.data(), h->d_acc, acc.size() * sizeof(double), hipMemcpyDeviceToHost);
-    double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = 0; b < h->batch; b++)
         for (int j = 0; j < 4; j++) v[j] += acc[(size_t)b * 4 + j];
     double ms = 0.0;
@@ -1941,7 +1990,9 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
     for (int b = 0; b < h->batch; b++) mean += it[b];
     v[6] = mean / h->batch;
     v[7] = h->cl_last_steps;
-    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
+    v[8] = h->clf_parked;
+    v[9] = h->clf_rounds;
+    for (int i = 0; i < n && i < 10; i++) out[i] = v[i];
     return 0;
 }
 

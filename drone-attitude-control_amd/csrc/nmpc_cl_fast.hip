@@ -1036,6 +1036,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                         status = 4;
                         break;
                     }
+                    if (!p.gi) break;   // test knob: no fallback, the step parks
                     int git = 0;
                     last_gi = true;
                     const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git);
@@ -1138,47 +1139,62 @@ int cl_fast_wsmax(int nx, int nu)
     return (nx == 4 && nu == 2) ? 32 : 16;
 }
 
-// grid: the workgroups the device holds at once (persistent wavefronts), at most one wavefront per instance
-template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
-static void launch_one(const ClFastParams<T> &p, int waves, hipStream_t s)
-{
-    static int resident = 0;
-    if (resident == 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, clf::cl_fast_kernel<T, NX, NU, EPL, WSM, WPB, MW, SP>,
-                                                         64 * WPB, 0) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            cus < 1)
-            cus = 256;
-        resident = per_cu * cus;
-    }
-    const int blocks = std::min((waves + WPB - 1) / WPB, resident);
-    hipLaunchKernelGGL((clf::cl_fast_kernel<T, NX, NU, EPL, WSM, WPB, MW, SP>), dim3(blocks), dim3(64 * WPB), 0, s, p);
-}
+// one compiled variant per shape, as a tag type
+template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, int MW_, class SP_>
+struct Variant {
+    static constexpr int WPB = WPB_;
+    static constexpr auto kernel() { return clf::cl_fast_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_>; }
+};
 
-// NMPC_CLF_VARIANT=1 (tuning): quad13 with an occupancy target of 4 waves per SIMD (spills; measured
-// 10 % slower than the default without a target)
-template <typename T>
-hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, hipStream_t s)
+// calls f(Variant<...>{}) for the shape's compiled variant; false: none. NMPC_CLF_VARIANT=1 (tuning):
+// an occupancy target (quad13 4 waves per SIMD: spills, measured 10 % slower than the default)
+template <typename T, class F>
+static bool clf_dispatch(int nx, int nu, int sid, F &&f)
 {
     static const int var = std::getenv("NMPC_CLF_VARIANT") ? std::atoi(std::getenv("NMPC_CLF_VARIANT")) : 0;
     if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) {
-        if (var == 1) launch_one<T, 13, 4, 4, 16, 8, 4, lpc::Quad13Structure>(p, waves, s);
-        else launch_one<T, 13, 4, 4, 16, 8, 0, lpc::Quad13Structure>(p, waves, s);
+        if (var == 1) f(Variant<T, 13, 4, 4, 16, 8, 4, lpc::Quad13Structure>{});
+        else f(Variant<T, 13, 4, 4, 16, 8, 0, lpc::Quad13Structure>{});
     } else if (nx == 13 && nu == 4) {
-        launch_one<T, 13, 4, 4, 16, 8, 0, lpc::DenseStructure<13, 4>>(p, waves, s);
+        f(Variant<T, 13, 4, 4, 16, 8, 0, lpc::DenseStructure<13, 4>>{});
     } else if (nx == 6 && nu == 2) {
-        launch_one<T, 6, 2, 5, 16, 8, 0, lpc::DenseStructure<6, 2>>(p, waves, s);
+        f(Variant<T, 6, 2, 5, 16, 8, 0, lpc::DenseStructure<6, 2>>{});
     } else if (nx == 4 && nu == 2) {
-        if (var == 1) launch_one<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>(p, waves, s);
-        else launch_one<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>(p, waves, s);
+        if (var == 1) f(Variant<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>{});
+        else f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>{});
     } else {
-        return hipErrorInvalidValue;
+        return false;
     }
-    return hipGetLastError();
+    return true;
 }
 
-template hipError_t cl_fast_launch<double>(int, int, int, const ClFastParams<double> &, int, hipStream_t);
+// the workgroups of the shape's kernel that `device` holds at once (the persistent grid), queried for
+// the given device at nmpc_closed_loop_init and kept on the handle (no process-wide cache)
+int cl_fast_resident(int nx, int nu, int sid, int device)
+{
+    int res = 0;
+    clf_dispatch<double>(nx, nu, sid, [&](auto v) {
+        using V = decltype(v);
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, V::kernel(), 64 * V::WPB, 0) != hipSuccess || per_cu < 1) return;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) return;
+        res = per_cu * cus;
+    });
+    return res;
+}
+
+// grid: min(workgroups for one wavefront per instance, the resident workgroups)
+template <typename T>
+hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, int resident, hipStream_t s)
+{
+    const bool ok = clf_dispatch<T>(nx, nu, sid, [&](auto v) {
+        using V = decltype(v);
+        const int blocks = std::max(1, std::min((waves + V::WPB - 1) / V::WPB, resident));
+        hipLaunchKernelGGL(V::kernel(), dim3(blocks), dim3(64 * V::WPB), 0, s, p);
+    });
+    return ok ? hipGetLastError() : hipErrorInvalidValue;
+}
+
+template hipError_t cl_fast_launch<double>(int, int, int, const ClFastParams<double> &, int, int, hipStream_t);
 
 }  // namespace nmpc

@@ -107,6 +107,7 @@ struct ClFastParams {
     int target;                   // run every instance up to this closed-loop step
     int step0, noise_ld;          // noise[b][step - step0], row length noise_ld
     int polish_steps;             // active-set rounds of the fast path
+    int gi;                       // 1: the dual active-set fallback runs; 0 (test knob): such steps park
     int x1_slot;                  // slot (lane, j = 0) of x_1[0] (cost of the jerk loop: cost_stage 1)
     const T *table;               // reference table [rows][table_cols]
     const int *offset;            // [B]
@@ -137,8 +138,11 @@ struct ClFastParams {
 int cl_fast_epl(int nx, int nu);
 // largest active set of the fast path for the shape (oracle/cref.py WSMAX)
 int cl_fast_wsmax(int nx, int nu);
+// workgroups of the shape's cl_fast_kernel that `device` holds at once (the persistent grid), or 0
+int cl_fast_resident(int nx, int nu, int sid, int device);
+// grid = min(waves / wavefronts per workgroup, resident)
 template <typename T>
-hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, hipStream_t s);
+hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, int resident, hipStream_t s);
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);
 

@@ -224,24 +224,34 @@ typedef struct nmpc_closed_loop_desc {
 
 /* bind the closed loop to a solver handle (allocates the table/state/accumulators on the device) */
 int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d);
-/* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion. With the
- * lane-per-component and wavefront kernel families the steps run fused: each solve launch carries
- * up to 64 steps of every instance (prepare + solve + advance per instance, no step barrier
- * between instances; env NMPC_CL_FUSED=0 for one prepare / solve / advance launch per step) —
- * the same results either way */
+/* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion.
+ * Paths (the same results on every one; the choice may change from run to run on one handle):
+ *   - the lean loop (nmpc_cl_fast.hip; quad13 / jerk / force shapes, fp64, the default): launches of at
+ *     most 64 steps; after each launch the host reads the count of parked instances (a step the fast
+ *     path could not solve) and runs their full solve in list mode. That read waits for the launch, so
+ *     the lean loop returns only when its last launch is done, whatever `sync` says;
+ *   - fused (lane-per-component and wavefront kernel families, NMPC_CL_FAST=0): each solve launch
+ *     carries up to 64 steps of every instance (prepare + solve + advance per instance, no step barrier
+ *     between instances); asynchronous with sync = 0;
+ *   - per step (env NMPC_CL_FUSED=0): one prepare / solve / advance launch per step. */
 int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync);
 /* out[0] sum closed-loop cost, out[1] sum AED numerator, out[2] failed solves, out[3] instance-steps,
  * out[4] total device ms of the solve kernel launches of the last run (HIP events around each),
  * out[5] solve launches in the last run, out[6] mean qp_iter of the last step, out[7] closed-loop
- * steps of the last run */
+ * steps of the last run, out[8] solves of the last run that parked (lean loop: list-mode full solves),
+ * out[9] lean-loop fast-kernel launches of the last run; n <= 10 values are written */
 int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n);
 /* per-instance accumulators, batch*4: [cost sum, AED numerator, failed solves, steps] of each
  * instance (the Monte-Carlo distribution behind nmpc_closed_loop_stats' sums) */
 int nmpc_closed_loop_instance_stats(nmpc_solver *h, double *out, size_t count);
-/* tuning aid: with env NMPC_ITER_LOG set, the per-step solve record of the last fused launch of the
- * fused lane-per-component / wavefront kernels (not the lean loop: NMPC_CL_FAST=0), steps*batch values
- * [step][instance] = finish steps | IPM iterations << 8 | status << 16; returns the step count.
- * out = NULL: returns the step count only (0: no log) */
+/* tuning aid: with env NMPC_ITER_LOG set, the per-step solve record of the last run, rows*batch values
+ * [row][instance]; returns the row count (out = NULL: the row count only, 0: no log). Layouts:
+ *   - fused lane-per-component / wavefront kernels (NMPC_CL_FAST=0): the run's last launch, one row per
+ *     step = finish steps | IPM iterations << 8 | status << 16;
+ *   - the lean loop: the run's last launch (<= 64 steps) + 2 rows. Step rows = active-set steps (<= 255)
+ *     | status << 8 | wall-clock ticks of the step (100 MHz, <= 32767) << 16; a step the list-mode
+ *     fallback solved keeps the marker -1. The last two rows: each instance's start and end in that
+ *     launch (wall-clock ticks, low 31 bits). */
 int nmpc_closed_loop_iter_log(nmpc_solver *h, int32_t *out, size_t count);
 /* current closed-loop states, batch*nx */
 int nmpc_closed_loop_get_state(nmpc_solver *h, double *out, size_t count);

@@ -117,3 +117,76 @@ def test_force_fused_loop_families_agree():
     assert _rel(xl, ref.state).max() < 1e-6
     assert np.array_equal(sl[:, 2:], ref.acc[:, 2:])
     np.testing.assert_allclose(sl[:, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.timeout(300)
+def test_lean_loop_list_mode_fallback_with_forced_parks():
+    """The lean loop's list-mode fallback (nmpc_api.cpp clf_run -> ipm_lpc_kernel in list mode, the path
+    whose idle lanes once read an unset noise column, nmpc_ipm_lpc.hip list mode) forced by the test knob
+    NMPC_CLF_NO_GI=1: without the dual active-set fallback every force step whose PDAS run does not
+    settle parks and gets the full solve. Force (saturating inputs, src/force_model/ocp.py:64-68), a
+    ragged batch of 2049 over 40 steps in three runs (3 + 20 + 17, reference loop
+    src/force_model/controller.py:25-54): parks happen, and states / sums match the exact oracle loop
+    (mode 0) at 1e-6 with the failure counts exact."""
+    from drone_attitude_control_amd.batched import ClosedLoop, workload
+    from oracle import cref, models
+    os.environ["NMPC_CLF_NO_GI"] = "1"
+    try:
+        cl = ClosedLoop("force", 2049, N=20, seed=5)
+        assert cl.solver.launch_info()["closed_loop_kernel"] == "cl_fast_kernel"
+        parked = 0
+        for n in (3, 20, 17):
+            cl.run(n)
+            parked += cl.stats()["parked"]
+        x, acc = cl.state(), cl.instance_stats()
+    finally:
+        os.environ.pop("NMPC_CLF_NO_GI", None)
+    assert parked > 0
+    table, off, x0 = workload("force", 20, 2049, 5)
+    ref = cref.ClosedLoopRef(models.force_model(20), "force", table, off, x0, mode=0, seed=5)
+    ref.run(40)
+    assert _rel(x, ref.state).max() < 1e-6, _rel(x, ref.state).max()
+    assert np.array_equal(acc[:, 2:], ref.acc[:, 2:])
+    np.testing.assert_allclose(acc[:, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
+
+
+_ITER_LOG_RUN = r"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["ROOT"])
+from drone_attitude_control_amd.batched import ClosedLoop
+cl = ClosedLoop("force", 2049, N=20, seed=5)
+cl.run(3)
+cl.run(20)
+st = cl.stats()
+it, s, kc = cl.iter_log()
+raw = it.astype(np.int64) | (s.astype(np.int64) << 8) | (kc.astype(np.int64) << 16)
+print(json.dumps({"rows": int(it.shape[0]), "parked": st["parked"],
+                  "marked": int((raw[:-2] == -1).sum()), "state": cl.state().tolist()}))
+"""
+
+
+@pytest.mark.timeout(300)
+def test_lean_loop_iter_log_survives_list_mode():
+    """NMPC_ITER_LOG with parks (the list-mode launch once resized the lean loop's log
+    bookkeeping without reallocating it, so run(3) then run(20) wrote past the buffer): in a fresh
+    process (the env switch is read once), force B=2049 with NMPC_CLF_NO_GI=1, run(3) then run(20):
+    the log has 20 + 2 rows, the parked steps carry the -1 marker (one per parked solve), and the
+    states match the exact oracle loop (mode 0)."""
+    import json
+    import subprocess
+    import sys
+    from drone_attitude_control_amd.batched import workload
+    from oracle import cref, models
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NMPC_ITER_LOG="1", NMPC_CLF_NO_GI="1", ROOT=root)
+    out = subprocess.run([sys.executable, "-c", _ITER_LOG_RUN], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["rows"] == 22
+    assert r["parked"] > 0 and r["marked"] == r["parked"], (r["parked"], r["marked"])
+    table, off, x0 = workload("force", 20, 2049, 5)
+    ref = cref.ClosedLoopRef(models.force_model(20), "force", table, off, x0, mode=0, seed=5)
+    ref.run(23)
+    assert _rel(np.array(r["state"]), ref.state).max() < 1e-6

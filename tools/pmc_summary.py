@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--traffic", default=None, help="model,N,batch,precision")
     ap.add_argument("--steps-per-launch", type=int, default=1,
                     help="closed-loop steps per solve launch (fused closed loop: the bench's --steps)")
+    ap.add_argument("--mode", default="closed_loop", help="bench.py --mode of the profiled run")
     a = ap.parse_args()
     means, ndisp, meta = collect(a.tag, a.kernel)
     if not means:
@@ -74,9 +75,12 @@ def main():
                      "per step = per launch / fused closed-loop steps per launch; mfma_insts_per_launch = "
                      "SQ_INSTS_MFMA; fp64_flops_per_step = 64 x SQ_INSTS_VALU_FLOPS_FP64 per step (executed FP64 "
                      "flops as the hardware counts them, idle lanes included)")
-        key = (model, int(N), int(batch), prec)
-        d["entries"] = [e for e in d["entries"] if (e["model"], e["N"], e["batch"], e["precision"]) != key]
+        key = (model, int(N), int(batch), prec, a.kernel, a.steps_per_launch, a.mode)
+        d["entries"] = [e for e in d["entries"]
+                        if (e["model"], e["N"], e["batch"], e["precision"], e.get("kernel"), e.get("steps_per_launch"),
+                            e.get("mode", "closed_loop")) != key]
         d["entries"].append({"model": model, "N": int(N), "batch": int(batch), "precision": prec, "kernel": a.kernel,
+                             "mode": a.mode,
                              "hbm_bytes_per_launch": res["traffic_bytes_per_launch"],
                              "steps_per_launch": a.steps_per_launch,
                              "hbm_bytes_per_step": res["traffic_bytes_per_launch"] / a.steps_per_launch,
@@ -86,6 +90,10 @@ def main():
                              # (the idle lanes of a wavefront included)
                              "fp64_flops_per_step": (64.0 * means["SQ_INSTS_VALU_FLOPS_FP64"] / a.steps_per_launch
                                                      if "SQ_INSTS_VALU_FLOPS_FP64" in means else None),
+                             "fp32_flops_per_step": (64.0 * means["SQ_INSTS_VALU_FLOPS_FP32"] / a.steps_per_launch
+                                                     if "SQ_INSTS_VALU_FLOPS_FP32" in means else None),
+                             "wait_any_frac": (means["SQ_WAIT_ANY"] / means["SQ_WAVE_CYCLES"]
+                                               if means.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in means else None),
                              "source": os.path.relpath(out, ROOT)})
         with open(path, "w") as fh:
             json.dump(d, fh, indent=1)
