@@ -417,6 +417,7 @@ def main_solve(args, world, rank, dist, device):
         barrier()
         regions.append(t1 - t0)
         kms.append(s.get_stats("time_tot") * 1e3)   # the region's last launch (HIP events)
+    s.solve()                                   # one synchronous solve: outputs, status and qp_iter to the host
     status = s.get_batch_int("status")
     iters = s.get_batch_int("qp_iter")
     red, regions, kms = reduce_run(dist, np.array([float((status != 0).sum()), float(iters.sum()), float(B)]),

@@ -1741,12 +1741,19 @@ int clf_run(nmpc_solver *h, int steps)
     }
     int launches = 0;
     h->clf_parked = h->clf_rounds = 0;
+    // env NMPC_CLF_CYCLES=<file> with a timing build (-DNMPC_CLF_TIMING): per-instance phase cycles of the
+    // run, [B][20] uint64, appended to <file> (tools/clf_phases.py)
+    static const char *cyc_path = std::getenv("NMPC_CLF_CYCLES");
+    unsigned long long *d_cyc = nullptr;
+    if (cyc_path && hipMalloc((void **)&d_cyc, (size_t)h->batch * 20 * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemsetAsync(d_cyc, 0, (size_t)h->batch * 20 * sizeof(unsigned long long), h->stream);
     for (int done = 0; done < steps;) {
         const int n = std::min(CLF_CHUNK, steps - done), target = h->cl_step + n;
         nmpc::ClParams<double> cp = cl_params<double>(h);
         hipError_t e = nmpc::cl_noise_launch<double>(cp, h->cl_step, n, h->d_fnoise, h->stream);
         if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
         nmpc::ClFastParams<double> fp = clf_params(h, target, h->cl_step, n);
+        fp.cycles = d_cyc;
         if (iter_log && h->d_iter_log) {
             const size_t rows = (size_t)(n + 2) * h->batch;
             if ((e = hipMemsetAsync(h->d_iter_log, 0xff, rows * sizeof(int), h->stream)) != hipSuccess)
@@ -1778,6 +1785,17 @@ int clf_run(nmpc_solver *h, int steps)
         }
         h->cl_step = target;
         done += n;
+    }
+    if (d_cyc) {
+        std::vector<unsigned long long> cy((size_t)h->batch * 20);
+        if (hipStreamSynchronize(h->stream) == hipSuccess &&
+            hipMemcpy(cy.data(), d_cyc, cy.size() * sizeof(cy[0]), hipMemcpyDeviceToHost) == hipSuccess) {
+            if (FILE *f = std::fopen(cyc_path, "ab")) {
+                std::fwrite(cy.data(), sizeof(cy[0]), cy.size(), f);
+                std::fclose(f);
+            }
+        }
+        (void)hipFree(d_cyc);
     }
     if (dbg && hipStreamSynchronize(h->stream) == hipSuccess)
         for (int i = 0; i < launches; i++) {

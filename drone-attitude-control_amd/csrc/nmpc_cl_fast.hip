@@ -45,6 +45,37 @@ namespace clf {
 
 constexpr int PDAS_ROUNDS = 6;   // rounds of the first PDAS run before the fallback (oracle: fast_finish's cap)
 
+// diagnostic build (-DNMPC_CLF_TIMING, build.build_experiment; env NMPC_CLF_CYCLES): shader cycles per
+// phase, summed per instance in the wavefront's LDS record and added to p.cycles[inst][CLF_NT] at its
+// write-back. Phases: 0 step prologue (loads, warm-start shift), 1 explicit form + bound test, 2 PDAS
+// runs (wsteps_run), 3 of which the set solves, 4 of which the W[:, S] nu combinations, 5 the dual
+// fallback (gi_set), 6 certificate, 7 outputs, 8 plant + cost, 9 instance record load / write-back;
+// counts: 10 PDAS rounds, 11 GI iterations, 12 slow steps, 13 steps; GI parts: 14 entering-bound choice,
+// 15 a = W[S, p] loads + r = H a + theta + ratio test, 16 dz combination, 17 H update; PDAS parts: 18 set
+// load, 19 bound tests / additions after the combination
+constexpr int CLF_NT = 20;
+#ifdef NMPC_CLF_TIMING
+#define CLF_T(v) const long long v = clock64()
+#define CLF_TADD(L, i, v)                              \
+    do {                                               \
+        if (lane == 0) (L).tacc[i] += clock64() - (v); \
+    } while (0)
+#define CLF_TCNT(L, i, n)                 \
+    do {                                  \
+        if (lane == 0) (L).tacc[i] += (n); \
+    } while (0)
+#else
+#define CLF_T(v) \
+    do {         \
+    } while (0)
+#define CLF_TADD(L, i, v) \
+    do {                  \
+    } while (0)
+#define CLF_TCNT(L, i, n) \
+    do {                  \
+    } while (0)
+#endif
+
 template <typename T>
 __device__ __forceinline__ bool has_b(T b)
 {
@@ -57,6 +88,15 @@ __device__ __forceinline__ double bcast(double v, int l)
     const long long b = __builtin_bit_cast(long long, v);
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// 1 / d: v_rcp_f64 refined by two Newton steps (to the last bit or one off; a division is ~10 dependent
+// instructions on the sweep's critical path)
+__device__ __forceinline__ double rcp_nr(double d)
+{
+    double f = __builtin_amdgcn_rcp(d);
+    f = fma(fma(-d, f, 1.0), f, f);
+    return fma(fma(-d, f, 1.0), f, f);
 }
 
 // sum / max / min over the wavefront's lanes (butterfly)
@@ -80,17 +120,31 @@ __device__ __forceinline__ double wave_min(double v)
 }
 
 // per-wavefront LDS: active flags by slot (the warm-start shift), the set of an active-set step
-// (element, sign, target b - z_0, multiplier), W_SS and its Cholesky factor, the per-component argmax
-// of the violated states, the certificate's stage exchange and the state copy
+// (element, sign, target b - z_0, multiplier), the explicit inverse H = W_SS^-1 of the set's block of W
+// (hm, rows by set position; the dual fallback's incremental updates, the sweep of sets > 16), two
+// broadcast vectors, the per-component argmax of the violated states, the certificate's stage exchange
+// and the state copy
+template <int WSM>
+struct HGeom {
+    static constexpr int CPL = WSM * WSM / 64;   // H columns per lane: lane = row i + WSM * column group g
+    static constexpr int HP = WSM + 2;           // row pitch (even: 16-byte aligned column groups)
+};
 template <int NSLOT, int NZ, int WSM>
 struct Lds {
     alignas(16) double xs[32];   // x (lane i writes x_i; x_nx.. stay 0): explicit form, plant rows, rare paths
     signed char fl[NSLOT];       // the warm-start shift buffer
-    double se_t[WSM], se_nu[WSM], wdg[WSM], wss[WSM][WSM + 1];
-    int se_e[WSM], se_s[WSM], gi_slot[WSM];
+    alignas(16) double hm[WSM][HGeom<WSM>::HP];
+    alignas(16) double vb1[WSM], vb2[WSM];
+    double se_t[WSM], se_nu[WSM], wdg[WSM];
+    int se_e[WSM], se_s[WSM], gi_slot[WSM], se_ord[WSM];
+    int cl_e[WSM];               // compacted element list of the active positions (w_combo_slots)
+    double cl_c[WSM];            // ... and their coefficients
     unsigned long long vmax[NZ];
     int vslot[NZ];
     double cm[32], cr[32];       // certificate exchange
+#ifdef NMPC_CLF_TIMING
+    long long tacc[CLF_NT];
+#endif
 };
 
 // the workgroup's slot constants (LDS), seen from one lane: slot j of this lane is j * 64 + lane.
@@ -151,49 +205,11 @@ __device__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, 
     return v;
 }
 
-// Cholesky of W_SS for the m elements in L.se_e (W_SS gathered over 8 x 8 lane tiles into the lower
-// triangle of L.wss, its diagonal into L.wdg; right-looking: column c scaled by its lanes, then the
-// trailing update over lane tiles). A pivot below 1e-9 of its diagonal W_ii (a bound linearly dependent
-// on the ones before it) is regularised to 1e-6 W_ii: that bound is held by a penalty (oracle/c/
-// riccati_ipm.c fast_finish / gi_factor). false: a non-positive W_ii.
-template <typename T, class LdsT>
-__device__ bool factor_set(const ClFastParams<T> &p, LdsT &L, int m, int lane)
-{
-    const int ne = p.ne, ti_ = lane >> 3, tj_ = lane & 7;
-    for (int a = 0; a * 8 < m; a++)
-        for (int b = 0; b <= a; b++) {
-            const int i = a * 8 + ti_, j = b * 8 + tj_;
-            if (i < m && j <= i) {
-                const double wij = (double)p.W[(size_t)L.se_e[j] * ne + L.se_e[i]];
-                L.wss[i][j] = wij;
-                if (i == j) L.wdg[i] = wij;
-            }
-        }
-    CLF_SYNC();
-    bool pd = true;
-    for (int c = 0; c < m; c++) {
-        const double d = L.wss[c][c], wcc = L.wdg[c];
-        pd = pd && wcc > 0.0;
-        const double lcc = d > 1e-9 * wcc ? sqrt(d) : sqrt(fmax(d, 0.0) + 1e-6 * wcc);
-        const int i = c + lane;
-        if (i < m) L.wss[i][c] = i == c ? lcc : L.wss[i][c] / lcc;   // the diagonal read above precedes this write
-        CLF_SYNC();
-        const int r0 = c + 1;
-        for (int a = 0; r0 + a * 8 < m; a++)
-            for (int b = 0; b <= a; b++) {
-                const int ii = r0 + a * 8 + ti_, jj = r0 + b * 8 + tj_;
-                if (ii < m && jj <= ii) L.wss[ii][jj] = fma(-L.wss[ii][c], L.wss[jj][c], L.wss[ii][jj]);
-            }
-        CLF_SYNC();
-    }
-    return pd;
-}
-
 // W_SS nu = t for the m elements in L.se_e by Gauss-Jordan elimination in registers: lane i holds row i
 // of W_SS (gathered with all its loads in flight) and t_i; pivot c's row reaches the other lanes by
 // readlane, every other row eliminates column c, so at the end nu_i = t_i / (row i's pivot). Pivots get
-// factor_set's regularisation (below 1e-9 of W_ii: + 1e-6 W_ii), i.e. the same regularised system the
-// Cholesky path solves. The diagonal W_ii goes to L.wdg (the multiplier test). pd: every W_ii > 0.
+// fast_finish's regularisation (below 1e-9 of W_ii: + 1e-6 W_ii), i.e. the same regularised system the
+// oracle's Cholesky solves. The diagonal W_ii goes to L.wdg (the multiplier test). pd: every W_ii > 0.
 template <typename T, int WSM, class LdsT>
 __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, int m, int lane, double t, bool &pd)
 {
@@ -230,104 +246,142 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, int m, int lan
     return lane < m ? t / dd : 0.0;
 }
 
-// solve_set_gj for sets of 17..32: two lanes per row — lane r < 32 holds columns 0..15 of row r, lane
-// r + 32 columns 16..31, t_r on both. Each pivot row goes through LDS (L.wss[0], free outside the
-// Cholesky path): its two lanes store it, every lane reads its half back (broadcast reads); W'(r, c)
-// comes from the lane holding that column by shuffle. The same eliminations and regularisation as
-// solve_set_gj.
-template <typename T, class LdsT>
-__device__ double solve_set_gj2(const ClFastParams<T> &p, LdsT &L, int m, int lane, double t, bool &pd)
+// The symmetric sweep (in-place Gauss-Jordan inversion) of W_SS for the m set elements in L.se_e
+// (positions 0..m-1): lane = row i + WSM * column group g holds CPL entries of its row in registers; pivot
+// k's column reaches every lane through one LDS all-gather (each row's holder of column k writes it, every
+// lane reads its row's entry, the pivot and its column group's entries), then the rank-1 update
+// a_ij -= a_ik a_kj / d, row and column k scaled by 1 / d, a_kk = -1 / d. After m pivots a = -W_SS^-1.
+// The pivot d (the Schur complement of the leading block, i.e. the Cholesky pivot squared) gets
+// fast_finish's regularisation: below 1e-9 W_kk it becomes max(d, 0) + 1e-6 W_kk, so the result is the
+// inverse of the same regularised system the Cholesky / Gauss-Jordan paths solve. H = W_SS^-1 goes to
+// L.hm (zero outside the m x m block), W_ii to L.wdg. false: a non-positive W_ii.
+template <typename T, int WSM, class LdsT>
+__device__ bool sweep_inverse(const ClFastParams<T> &p, LdsT &L, int m, int lane)
 {
-    const int ne = p.ne, r = lane & 31, h = lane >> 5;
-    double row[16];
-    const int er = r < m ? L.se_e[r] : 0;
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int i = lane % WSM, g = lane / WSM, ne = p.ne;
+    double a[CPL];
+    const int ei = i < m ? L.se_e[i] : 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int col = 16 * h + k;
-        row[k] = (col < m && r < m) ? (double)p.W[(size_t)L.se_e[col] * ne + er] : 0.0;
+    for (int q = 0; q < CPL; q++) {
+        const int j = g * CPL + q;
+        a[q] = (i < m && j < m) ? (double)p.W[(size_t)L.se_e[j] * ne + ei] : 0.0;
     }
-    double wv = 1.0;
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-        if (16 * h + k == r) wv = row[k];
-    const double wii = __shfl(wv, r + 32 * (r >> 4));   // W_rr, from the half holding column r
-    if (lane < m) L.wdg[lane] = wii;
-    pd = true;
-    double piv = 1.0;
-    double *prow = &L.wss[0][0];
+    for (int q = 0; q < CPL; q++)
+        if (g * CPL + q == i && i < m) L.wdg[i] = a[q];
+    CLF_SYNC();
+    bool pd = true;
 #pragma unroll
-    for (int c = 0; c < 32; c++) {
-        if (c >= m) break;
-        const int pk = c & 15;
-        if (r == c) {
+    for (int k = 0; k < WSM; k++) {
+        if (k >= m) break;
+        if (g == k / CPL) L.vb1[i] = a[k % CPL];
+        CLF_SYNC();
+        const double ci = L.vb1[i], d0 = L.vb1[k], wkk = L.wdg[k];
+        pd = pd && wkk > 0.0;
+        const double d = d0 > 1e-9 * wkk ? d0 : fmax(d0, 0.0) + 1e-6 * wkk;
+        const double f = rcp_nr(d);
+        // rows i != k: a_ij - c_i f c_j; row k (a_kj = c_j by symmetry): a_kj - (1 - f) c_j = c_j f
+        const double cif = i == k ? 1.0 - f : ci * f;
 #pragma unroll
-            for (int k = 0; k < 16; k++) prow[16 * h + k] = row[k];
-        }
-        __builtin_amdgcn_wave_barrier();
-        const double wrc = __shfl(row[pk], r + 32 * (c >> 4));
-        const double d0 = prow[c], wcc = bcast(wii, c), tc = bcast(t, c);
-        pd = pd && wcc > 0.0;
-        const double d = d0 > 1e-9 * wcc ? d0 : fmax(d0, 0.0) + 1e-6 * wcc;
-        const double f = (r != c && r < m) ? wrc / d : 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int col = 16 * h + k;
-            if (col > c && col < m) row[k] = fma(-f, prow[col], row[k]);
-        }
-        t = fma(-f, tc, t);
-        if (r == c) piv = d;
-        __builtin_amdgcn_wave_barrier();
+        for (int q = 0; q < CPL; q++) a[q] = fma(-cif, L.vb1[g * CPL + q], a[q]);
+        if (g == k / CPL) a[k % CPL] = i == k ? -f : ci * f;
     }
-    return (h == 0 && r < m) ? t / piv : 0.0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) L.hm[i][g * CPL + q] = -a[q];
+    CLF_SYNC();
+    return pd;
 }
 
-// y = L^-1 y (forward) or L^-T y (backward) for the factor in L.wss, the vector lane-distributed (lane
-// i holds y_i, i < m; the pivot of each column broadcast by readlane)
-template <class LdsT>
-__device__ double solve_lower(LdsT &L, int m, int lane, double y)
+// y_i = sum_j H_ij x_j with x all-gathered in LDS (x_j = 0 outside the set): the row's CPL-column
+// partial sums, reduced over the row's lanes; y_i on every lane of row i
+template <int WSM, class LdsT>
+__device__ double h_matvec(const LdsT &L, const double *x, int lane)
 {
-    const double dg = lane < m ? L.wss[lane][lane] : 1.0;
-    for (int c = 0; c < m; c++) {
-        const double yc = bcast(y, c) / bcast(dg, c);
-        if (lane == c) y = yc;
-        else if (lane > c && lane < m) y = fma(-L.wss[lane][c], yc, y);
-    }
-    return y;
-}
-template <class LdsT>
-__device__ double solve_upper(LdsT &L, int m, int lane, double y)
-{
-    const double dg = lane < m ? L.wss[lane][lane] : 1.0;
-    for (int c = m - 1; c >= 0; c--) {
-        const double xc = bcast(y, c) / bcast(dg, c);
-        if (lane == c) y = xc;
-        else if (lane < c) y = fma(-L.wss[c][lane], xc, y);
-    }
-    return y;
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int i = lane % WSM, g = lane / WSM;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) s = fma(L.hm[i][g * CPL + q], x[g * CPL + q], s);
+    if (WSM == 16) s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    return s;
 }
 
-// sum_i W[e_i][e] c_i over the m elements in L.se_e with coefficients in cf (LDS), loads 8 at a time
-template <typename T, class LdsT>
-__device__ T w_combo(const ClFastParams<T> &p, LdsT &L, const double *cf, int m, int e, T acc)
+// x . y over the set positions for two all-gathered vectors (every lane gets the sum)
+template <int WSM>
+__device__ double h_dot(const double *x, const double *y, int lane)
 {
-    const int ne = p.ne;
-    for (int i0 = 0; i0 < m; i0 += 8) {
-        T w[8];
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int g = lane / WSM;
+    double s = 0.0;
 #pragma unroll
-        for (int q = 0; q < 8; q++) w[q] = i0 + q < m ? p.W[(size_t)L.se_e[i0 + q] * ne + e] : T(0);
+    for (int q = 0; q < CPL; q++) s = fma(x[g * CPL + q], y[g * CPL + q], s);
+    if (WSM == 16) s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    return s;
+}
+
+// bordering: position q (free: row and column q of H zero) joins with r = H W[S, p] all-gathered in
+// L.vb2 (r_q = 0) and Schur complement theta = W_pp - W[S, p] . r > 0: H += r r^T / theta,
+// H_iq = H_qi = -r_i / theta, H_qq = 1 / theta
+template <int WSM, class LdsT>
+__device__ void h_add(LdsT &L, int q, double theta, int lane)
+{
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int i = lane % WSM, g = lane / WSM;
+    const double it = rcp_nr(theta), rit = L.vb2[i] * it;
 #pragma unroll
-        for (int q = 0; q < 8; q++)
-            if (i0 + q < m) acc = fma(w[q], (T)cf[i0 + q], acc);
+    for (int c = 0; c < CPL; c++) {
+        const int j = g * CPL + c;
+        const double rj = L.vb2[j];
+        double v = fma(rit, rj, L.hm[i][j]);
+        if (j == q) v = i == q ? it : -rit;
+        if (i == q) v = j == q ? it : -rj * it;
+        L.hm[i][j] = v;
     }
-    return acc;
+    CLF_SYNC();
+}
+
+// position k leaves: H_ij -= H_ik H_kj / H_kk (the inverse of the set without k), row and column k zeroed.
+// One wavefront: every lane's reads of a column group precede the writes to it (LDS program order)
+template <int WSM, class LdsT>
+__device__ void h_drop(LdsT &L, int k, int lane)
+{
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int i = lane % WSM, g = lane / WSM;
+    const double f = L.hm[i][k] * rcp_nr(L.hm[k][k]);
+#pragma unroll
+    for (int c = 0; c < CPL; c++) {
+        const int j = g * CPL + c;
+        const double v = fma(-f, L.hm[k][j], L.hm[i][j]);
+        L.hm[i][j] = (i == k || j == k) ? 0.0 : v;
+    }
+    CLF_SYNC();
+}
+
+// the active positions (bitmask am) as a compacted list for w_combo_slots: elements to L.cl_e, the
+// coefficients (lane i < WSM holds position i's) to L.cl_c; returns the count
+template <int WSM, class LdsT>
+__device__ int compact_set(LdsT &L, unsigned am, int lane, double coef)
+{
+    const bool act = lane < WSM && ((am >> lane) & 1u);
+    const unsigned long long b = __ballot(act);
+    if (act) {
+        const int to = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+        L.cl_e[to] = L.se_e[lane];
+        L.cl_c[to] = coef;
+    }
+    CLF_SYNC();
+    return __popcll(b);
 }
 
 // acc[j] += sum_i W[e_i][e_j] c_i at every slot j of the lane (padding slots untouched) for the m
-// elements in L.se_e with coefficients cf (LDS): the set in batches of QB, each batch's loads for all the
+// elements el (LDS) with coefficients cf (LDS): the set in batches of QB, each batch's loads for all the
 // lane's slots in flight together (one memory latency per batch, not one per slot and batch); per slot
-// the sum runs in set order, as w_combo's
-template <typename T, int EPL, class LdsT>
-__device__ void w_combo_slots(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, const double *cf, int m,
+// the sum runs in list order
+template <typename T, int EPL>
+__device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const SlotView<EPL> sv, const double *cf, int m,
                               T (&acc)[EPL])
 {
     constexpr int QB = EPL <= 2 ? 8 : (EPL <= 4 ? 4 : 2);
@@ -339,7 +393,7 @@ __device__ void w_combo_slots(const ClFastParams<T> &p, LdsT &L, const SlotView<
         T w[QB][EPL];
 #pragma unroll
         for (int q = 0; q < QB; q++) {
-            const int row = i0 + q < m ? L.se_e[i0 + q] : 0;
+            const int row = i0 + q < m ? el[i0 + q] : 0;
 #pragma unroll
             for (int j = 0; j < EPL; j++) w[q][j] = (i0 + q < m && e[j] >= 0) ? p.W[(size_t)row * ne + e[j]] : T(0);
         }
@@ -470,20 +524,27 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         }
         if (m > WSM) break;
         int pos[EPL];
+        CLF_T(tl_set);
         load_set<T, EPL, WSM>(L, sv, lane, wf, z0, pos);
+        CLF_TADD(L, 18, tl_set);
         // nu = W_SS^-1 (b - z_0)_S, lane i holding row i: Gauss-Jordan in registers for sets of up to 16
         // (one lane per row) and 32 (two lanes per row: register rows of 32 would go to scratch), the LDS
         // Cholesky beyond
         bool pd = true;
         double y;
+        CLF_T(ts0);
         if (WSM <= 16 || m <= 16) {
             y = solve_set_gj<T, (WSM < 16 ? WSM : 16)>(p, L, m, lane, lane < m ? L.se_t[lane] : 0.0, pd);
-        } else if (WSM >= 32 && m <= 32) {
-            y = solve_set_gj2<T>(p, L, m, lane, (lane & 31) < m ? L.se_t[lane & 31] : 0.0, pd);
         } else {
-            pd = factor_set(p, L, m, lane);
-            y = solve_upper(L, m, lane, solve_lower(L, m, lane, lane < m ? L.se_t[lane] : 0.0));
+            // sets of 17..WSM: the sweep's explicit inverse, nu = H (b - z_0)_S
+            pd = sweep_inverse<T, WSM>(p, L, m, lane);
+            if (lane < WSM) L.vb2[lane] = lane < m ? L.se_t[lane] : 0.0;
+            CLF_SYNC();
+            y = h_matvec<WSM>(L, L.vb2, lane);
+            y = lane < m ? y : 0.0;
         }
+        CLF_TADD(L, 3, ts0);
+        CLF_TCNT(L, 10, 1);
         if (!pd) break;
         // multiplier signs as displacements nu_i W_ii (lower: >= 0, upper: <= 0) to 1e-10 (1 + |b - z_0|)
         bool rmv = false;
@@ -504,7 +565,10 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         unsigned sgn = 0, nwf = wf;
 #pragma unroll
         for (int j = 0; j < EPL; j++) z[j] = z0[j];
-        w_combo_slots<T, EPL>(p, L, sv, L.se_nu, m, z);
+        CLF_T(tc0);
+        w_combo_slots<T, EPL>(p, L.se_e, sv, L.se_nu, m, z);
+        CLF_TADD(L, 4, tc0);
+        CLF_T(tk0);
 #pragma unroll
         for (int j = 0; j < EPL; j++) {
             v[j] = 0.0;
@@ -526,10 +590,14 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
             }
             z[j] = zz;
         }
-        if (!__any(bad)) return done(m);
+        if (!__any(bad)) {
+            CLF_TADD(L, 19, tk0);
+            return done(m);
+        }
         if (addok) add_states(v, sgn, nwf);
         wf = nwf;
         CLF_SYNC();
+        CLF_TADD(L, 19, tk0);
     }
 #pragma unroll
     for (int j = 0; j < EPL; j++) z[j] = z0[j];   // not accepted: z_0 back to the caller
@@ -540,75 +608,71 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
 // (oracle/c/riccati_ipm.c gi_set): the Goldfarb-Idnani dual active-set method on W, which converges for
 // any strictly convex QP. Bounds are constraints n_i^T z >= b_i, n_i = +e (lower) / -e (upper), sign
 // sg_i. From z = z_0 and an empty set the most violated inactive bound p enters (ties: the first slot):
-// l' = L^-1 W[S][p] (the unsigned factor of W_SS in L.wss), theta = W_pp - |l'|^2, the multipliers'
-// rate r_i = sg_p sg_i (L^-T l')_i, dz = sg_p (W[:, p] - W[:, S] L^-T l'); the full step
-// t2 = -sg_p (z_p - b_p) / theta makes p active (the factor grows by the row l', sqrt(theta)), the
-// partial step t1 = min u_i / r_i (r_i > 0) drops the bound whose multiplier reaches zero first
-// (refactored); z += t dz, u -= t r, u_p += t. theta ~ 0 (p dependent on the set) only drops; no
-// blocking bound then: infeasible. The set lives in L.se_e / L.se_s (+ slot), the multipliers on lanes
-// i < m. true: no inactive bound violated beyond 1e-13, the set in wf (per-lane flag bits), for
-// wsteps_run to solve exactly and check. z_0 is not modified.
+// with a = W[S, p] and H = W_SS^-1 (L.hm, kept up to date by bordering / downdating instead of being
+// refactored), r = H a, theta = W_pp - a . r (the curvature along p), the multipliers' rate
+// r_i' = sg_p sg_i r_i, dz = sg_p (W[:, p] - W[:, S] r); the full step t2 = -sg_p (z_p - b_p) / theta
+// makes p active (h_add), the partial step t1 = min u_i / r_i' (r_i' > 0; ties: the earliest entry) drops
+// the bound whose multiplier reaches zero first (h_drop); z += t dz, u -= t r', u_p += t. theta ~ 0 (p
+// dependent on the set) only drops; no blocking bound then: infeasible. Set positions stay fixed (am:
+// the occupied ones, se_ord: entry order); multipliers on lanes i < WSM. true: no inactive bound violated
+// beyond 1e-13, the set in wf (per-lane flag bits), for wsteps_run to solve exactly and check. z_0 is not
+// modified.
 template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
 __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, const T (&z0)[EPL],
                        unsigned w0, unsigned &wf, int &iters)
 {
-    const int ne = p.ne;
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int ne = p.ne, hi_ = lane % WSM, hg = lane / WSM;
     T z[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; j++) z[j] = z0[j];
-    int m = 0, ps = -1, sp = 0, ep = 0;   // the entering bound: slot, sign (+1 lower, -1 upper), element
-    double u = 0.0, up = 0.0;             // lane i < m: the multiplier u_i; up: the entering bound's
+    unsigned am = 0;                      // occupied set positions (wave-uniform)
+    int ps = -1, sp = 0, ep = 0, ord = 0; // the entering bound: slot, sign (+1 lower, -1 upper), element
+    double u = 0.0, up = 0.0;             // lane i < WSM: the multiplier u_i of position i; up: the entering bound's
+    const bool pl = lane < WSM;
     // warm start: the set the PDAS rounds started from (w0), made dual feasible — its equality-constrained
-    // solution nu = W_SS^-1 (b - z_0)_S, u_i = sg_i nu_i; the negative ones leave, re-solved until none
-    // is left — and z = z_0 + W[:, S] nu
+    // solution nu = W_SS^-1 (b - z_0)_S, u_i = sg_i nu_i; the negative ones leave (downdates), re-solved
+    // until none is left — and z = z_0 + W[:, S] nu
     {
         int pos[EPL];
-        m = load_set<T, EPL, WSM>(L, sv, lane, w0, z0, pos);
+        int m = load_set<T, EPL, WSM>(L, sv, lane, w0, z0, pos);
         wf = m <= WSM ? w0 : 0u;
         if (m > WSM) m = 0;
-        double nu = 0.0;
-        while (m > 0) {
-            factor_set(p, L, m, lane);
-            nu = solve_upper(L, m, lane, solve_lower(L, m, lane, lane < m ? L.se_t[lane] : 0.0));
-            u = lane < m ? (double)(-L.se_s[lane]) * nu : 0.0;
-            const bool keep = lane < m && !(u < 0.0);
-            const unsigned long long km = __ballot(keep);
-            if (__popcll(km) == m) break;
-            // compact: the kept entries to their new positions, the dropped slots' flags cleared
-            const int to = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
-            int e_ = 0, s_ = 0, sl_ = 0;
-            double t_ = 0.0;
-            if (lane < m) {
-                e_ = L.se_e[lane];
-                s_ = L.se_s[lane];
-                sl_ = L.gi_slot[lane];
-                t_ = L.se_t[lane];
-            }
-            CLF_SYNC();
-            if (keep) {
-                L.se_e[to] = e_;
-                L.se_s[to] = s_;
-                L.gi_slot[to] = sl_;
-                L.se_t[to] = t_;
-            }
-            const unsigned long long dm = __ballot(lane < m && !keep);
-            for (unsigned long long d_ = dm; d_; d_ &= d_ - 1) {
-                const int sk = __shfl(sl_, (int)__builtin_ctzll(d_));
-                if (lane == (sk & 63)) wf &= ~(3u << (2 * (sk >> 6)));
-            }
-            m = __popcll(km);
-            CLF_SYNC();
-        }
         if (m > 0) {
-            if (lane < m) L.se_nu[lane] = nu;
+            sweep_inverse<T, WSM>(p, L, m, lane);
+            am = m == 32 ? 0xffffffffu : ((1u << m) - 1u);
+        } else {
+#pragma unroll
+            for (int c = 0; c < CPL; c++) L.hm[hi_][hg * CPL + c] = 0.0;
+        }
+        if (pl) L.se_ord[lane] = lane;
+        ord = m;
+        double nu = 0.0;
+        while (am) {
+            if (pl) L.vb2[lane] = ((am >> lane) & 1u) ? L.se_t[lane] : 0.0;
             CLF_SYNC();
-            w_combo_slots<T, EPL>(p, L, sv, L.se_nu, m, z);
+            nu = h_matvec<WSM>(L, L.vb2, lane);
+            u = (pl && ((am >> lane) & 1u)) ? (double)(-L.se_s[lane]) * nu : 0.0;
+            const unsigned long long neg = __ballot(pl && ((am >> lane) & 1u) && u < 0.0);
+            if (!neg) break;
+            for (unsigned long long d_ = neg; d_; d_ &= d_ - 1) {
+                const int k = (int)__builtin_ctzll(d_);
+                const int sk = L.gi_slot[k];
+                if (lane == (sk & 63)) wf &= ~(3u << (2 * (sk >> 6)));
+                h_drop<WSM>(L, k, lane);
+                am &= ~(1u << k);
+            }
+        }
+        if (am) {
+            const int mc = compact_set<WSM>(L, am, lane, nu);
+            w_combo_slots<T, EPL>(p, L.cl_e, sv, L.cl_c, mc, z);
             CLF_SYNC();
         }
     }
     const int cap = 3 * WSM + 16;
     int it = 0;
     for (; it < cap; it++) {
+        CLF_T(tg_sel);
         if (ps < 0) {
             double v[EPL], vm = 0.0;
 #pragma unroll
@@ -628,6 +692,12 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
             ep = sv.e_[ps];
             up = 0.0;
         }
+        CLF_TADD(L, 14, tg_sel);
+        CLF_T(tg_sol);
+        // a = W[S, p] (occupied positions) and W_pp, loads issued together
+        const bool occ = pl && ((am >> lane) & 1u);
+        const double ai = occ ? (double)p.W[(size_t)L.se_e[lane] * ne + ep] : 0.0;
+        const double wpp = (double)p.W[(size_t)ep * ne + ep];
         double zc = 0.0;
 #pragma unroll
         for (int j = 0; j < EPL; j++)
@@ -635,24 +705,27 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         const double zp = bcast(zc, ps & 63);
         if (up == 0.0) sp = zp < sv.lo_[ps] ? 1 : -1;   // entering: the violated side
         const double bp = sp > 0 ? sv.lb_[ps] : sv.ub_[ps];
-        const double wpp = (double)p.W[(size_t)ep * ne + ep];
-        const double l_ = solve_lower(L, m, lane, lane < m ? (double)p.W[(size_t)L.se_e[lane] * ne + ep] : 0.0);
-        const double theta = wpp - wave_sum(lane < m ? l_ * l_ : 0.0);
-        const double r_ = solve_upper(L, m, lane, l_);
-        const double ri = lane < m ? (double)sp * (double)(-L.se_s[lane]) * r_ : 0.0;
-        const double q = (lane < m && ri > 0.0) ? u / ri : INFINITY;
+        if (pl) L.vb1[lane] = ai;
+        CLF_SYNC();
+        const double r_ = h_matvec<WSM>(L, L.vb1, lane);   // r = H a
+        if (pl) L.vb2[lane] = r_;
+        CLF_SYNC();
+        const double theta = wpp - h_dot<WSM>(L.vb1, L.vb2, lane);
+        const double ri = occ ? (double)sp * (double)(-L.se_s[lane]) * r_ : 0.0;
+        const double q = (occ && ri > 0.0) ? u / ri : INFINITY;
         const double t1 = wave_min(q);
         const double t2 = theta > 1e-12 * wpp ? -(double)sp * (zp - bp) / theta : INFINITY;
         if (t1 == INFINITY && t2 == INFINITY) break;   // infeasible
         const bool full = t2 <= t1;
         const double t = full ? t2 : t1;
+        CLF_TADD(L, 15, tg_sol);
+        CLF_T(tg_cmb);
         if (t2 < INFINITY) {
-            if (lane < m) L.se_nu[lane] = r_;
-            CLF_SYNC();
+            const int mc = compact_set<WSM>(L, am, lane, r_);
             T comb[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) comb[j] = T(0);
-            w_combo_slots<T, EPL>(p, L, sv, L.se_nu, m, comb);
+            w_combo_slots<T, EPL>(p, L.cl_e, sv, L.cl_c, mc, comb);
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 const int e = sv.e(j);
@@ -660,45 +733,44 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
             }
             CLF_SYNC();
         }
-        if (lane < m) u = fma(-t, ri, u);
+        CLF_TADD(L, 16, tg_cmb);
+        CLF_T(tg_upd);
+        if (occ) u = fma(-t, ri, u);
         up += t;
         if (full) {
-            if (m >= WSM) break;
-            if (lane < m) L.wss[m][lane] = l_;
-            if (lane == m) {
-                L.wss[m][m] = sqrt(theta);
-                L.se_e[m] = ep;
-                L.se_s[m] = sp > 0 ? -1 : 1;
-                L.gi_slot[m] = ps;
+            if (__popc(am) >= WSM) break;
+            const int qn = (int)__builtin_ctz(~am);   // the lowest free position
+            h_add<WSM>(L, qn, theta, lane);
+            if (lane == qn) {
+                L.se_e[qn] = ep;
+                L.se_s[qn] = sp > 0 ? -1 : 1;
+                L.gi_slot[qn] = ps;
+                L.se_ord[qn] = ord;
                 u = up;
             }
+            ord++;
+            am |= 1u << qn;
             if (lane == (ps & 63)) wf |= (sp > 0 ? 1u : 2u) << (2 * (ps >> 6));
-            m++;
             ps = -1;
             CLF_SYNC();
         } else {
-            const unsigned long long kb = __ballot(lane < m && ri > 0.0 && q == t1);
-            const int kk = (int)__builtin_ctzll(kb);
+            // the blocking bound (ties: the earliest entry, as the oracle's list order)
+            const bool tie = occ && ri > 0.0 && q == t1;
+            const unsigned long long kb = __ballot(tie);
+            int kk = (int)__builtin_ctzll(kb);
+            if (__popcll(kb) > 1) {
+                const int o = tie ? L.se_ord[lane] : 0x7fffffff;
+                int om = o;
+#pragma unroll
+                for (int s_ = 32; s_ > 0; s_ >>= 1) om = min(om, __shfl_xor(om, s_));
+                kk = (int)__builtin_ctzll(__ballot(tie && o == om));
+            }
             const int sk = L.gi_slot[kk];
             if (lane == (sk & 63)) wf &= ~(3u << (2 * (sk >> 6)));
-            const int src = lane >= kk ? lane + 1 : lane;
-            int e_ = 0, s_ = 0, sl_ = 0;
-            if (lane + 1 < m) {
-                e_ = L.se_e[src];
-                s_ = L.se_s[src];
-                sl_ = L.gi_slot[src];
-            }
-            u = __shfl(u, src & 63);
-            CLF_SYNC();
-            if (lane + 1 < m) {
-                L.se_e[lane] = e_;
-                L.se_s[lane] = s_;
-                L.gi_slot[lane] = sl_;
-            }
-            m--;
-            CLF_SYNC();
-            factor_set(p, L, m, lane);
+            h_drop<WSM>(L, kk, lane);
+            am &= ~(1u << kk);
         }
+        CLF_TADD(L, 17, tg_upd);
     }
     iters = it;
     return ps < 0 && it < cap;
@@ -863,6 +935,55 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<
     }
 }
 
+// The rare path of one step (the instance's wavefront): PDAS rounds from the warm set wf; if they do not
+// settle, the interval certificate (oracle/c/riccati_ipm.c infeasible_stage: status 4), else the dual
+// active-set fallback finds the set and one more PDAS run solves and checks it; else the step parks. An
+// instance whose last solve failed (cert_first) tries the certificate first: infeasible QPs come in runs.
+// The first PDAS run takes at most PDAS_ROUNDS rounds (its long runs are cycles, which the fallback
+// resolves in a few steps) — one round when the instance's previous step of this launch needed the
+// fallback (gi_prev: saturation arcs, where the shifted set is right or the fallback is needed again) —
+// the run after the fallback polish_steps. z: z_0 in, the solution out when accepted. Returns status |
+// accepted << 8 | ran the fallback << 9 | set size << 10 | (status 4 ? 0 : 1 + active-set steps) << 18.
+template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
+__device__ int slow_step(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, const double *abl,
+                         const double *cl, T (&z)[EPL], unsigned wf, bool cert_first, bool gi_prev)
+{
+    int r = 0, steps_ = 0, status = 0;
+    bool ran_gi = false;
+    unsigned wset = wf;
+    CLF_T(tcf);
+    if (cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) status = 4;
+    CLF_TADD(L, 6, tcf);
+    for (int pass = 0; pass < 2 && status != 4; pass++) {
+        const int rounds = pass == 1 ? p.polish_steps : (gi_prev ? 1 : min(p.polish_steps, PDAS_ROUNDS));
+        CLF_T(tw0);
+        r = wsteps_run<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, rounds);
+        CLF_TADD(L, 2, tw0);
+        steps_ += r >> 16;
+        if ((r & 1) || pass == 1) break;
+        CLF_T(tc1);
+        const bool infeas = !cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane);
+        CLF_TADD(L, 6, tc1);
+        if (infeas) {
+            status = 4;
+            break;
+        }
+        if (!p.gi) break;   // test knob: no fallback, the step parks
+        int git = 0;
+        ran_gi = true;
+        CLF_T(tg0);
+        const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git);
+        CLF_TADD(L, 5, tg0);
+        CLF_TCNT(L, 11, git);
+        steps_ += git;
+        if (!found) break;
+    }
+    const bool ok = (r & 1) != 0;
+    const int m_acc = ok ? (r >> 8) & 0xff : 0;
+    const int iters = status == 4 ? 0 : 1 + steps_;
+    return status | (ok ? 1 << 8 : 0) | (ran_gi ? 1 << 9 : 0) | (m_acc << 10) | (min(iters, 0x3fff) << 18);
+}
+
 // WPB wavefronts per workgroup (the slot tables in LDS are shared by them), MW the occupancy target
 // (waves per SIMD; 0: none)
 template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
@@ -906,6 +1027,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
     if (lane < 32) L.xs[lane] = 0.0;
+#ifdef NMPC_CLF_TIMING
+    if (lane < CLF_NT) L.tacc[lane] = 0;
+#endif
     if (threadIdx.x == 0) wg_next = 0;
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
@@ -927,6 +1051,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         if (lane == 0) next = atomicAdd(&wg_next, 1);
         const int inst = wg_lo + __builtin_amdgcn_readfirstlane(next);
         if (inst >= wg_hi) break;
+        CLF_T(tr0);
         const long long inst_t0 = p.iter_log ? wall_clock64() : 0;
         // the instance's record, issued together: step, state (lane i < NX holds x_i), active flags of the
         // last solution by slot (bit 2j lower, 2j+1 upper; meaningful after step 0), offset, status
@@ -961,8 +1086,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             for (int j = 0; j < EPL; j++) vtn[j] = vp[j * 64 + lane];
         };
         fetch_v(t);
+        CLF_TADD(L, 9, tr0);
         for (; step < p.target; step++) {
             const long long clk0 = p.iter_log ? wall_clock64() : 0;
+            CLF_T(tp0);
             T vt[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) vt[j] = vtn[j];
@@ -984,6 +1111,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 }
             }
             CLF_SYNC();
+            CLF_TADD(L, 0, tp0);
+            CLF_T(te0);
             // ---- explicit unconstrained solution at the lane's slots (x pairs broadcast from LDS)
             T z[EPL], z1[EPL];
 #pragma unroll
@@ -1013,39 +1142,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 for (int j = 0; j < EPL; j++) bad |= !(z[j] >= (T)sv.lo(j) && z[j] <= (T)sv.hi(j));   // NaN: bad
                 ok = !__any(bad);
             }
+            CLF_TADD(L, 1, te0);
+            CLF_TCNT(L, 13, 1);
             if (!ok) {
-                // ---- active-set steps on W (rare)
-                // PDAS rounds from the warm set; if they do not settle: the interval certificate (oracle/c/
-                // riccati_ipm.c infeasible_stage: status 4), else the dual active-set fallback finds the set
-                // and one more PDAS run solves and checks it; else the instance parks
-                // (an instance whose last solve failed tries the certificate first: infeasible QPs come in runs).
-                // The first PDAS run takes at most PDAS_ROUNDS rounds (its long runs are cycles, which the
-                // fallback resolves in a few steps) — one round when the instance's previous step of this
-                // launch needed the fallback (saturation arcs: the shifted set is right or the fallback is
-                // needed again) — the run after the fallback polish_steps.
-                int r = 0, steps_ = 0;
-                unsigned wset = wf;
-                const bool cert_first = last_status == 4;
-                if (cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) status = 4;
-                for (int pass = 0; pass < 2 && status != 4; pass++) {
-                    const int rounds = pass == 1 ? p.polish_steps : (gi_prev ? 1 : min(p.polish_steps, PDAS_ROUNDS));
-                    r = wsteps_run<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, rounds);
-                    steps_ += r >> 16;
-                    if ((r & 1) || pass == 1) break;
-                    if (!cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) {
-                        status = 4;
-                        break;
-                    }
-                    if (!p.gi) break;   // test knob: no fallback, the step parks
-                    int git = 0;
-                    last_gi = true;
-                    const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git);
-                    steps_ += git;
-                    if (!found) break;
-                }
-                ok = (r & 1) != 0;
-                m_acc = ok ? (r >> 8) & 0xff : 0;
-                iters = status == 4 ? 0 : 1 + steps_;
+                CLF_TCNT(L, 12, 1);
+                const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, wf, last_status == 4, gi_prev);
+                status = sr & 0xff;
+                last_gi = (sr >> 9) & 1;
+                ok = (sr >> 8) & 1;
+                m_acc = (sr >> 10) & 0xff;
+                iters = sr >> 18;
                 if (!ok && status != 4) {
                     parked = true;
                     break;
@@ -1080,9 +1186,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             last_status = status;
             last_iters = iters;
             // ---- the trajectory outputs of the instance's last step of the run
+            CLF_T(to0);
             if (step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, t, status, m_acc, z);
+            CLF_TADD(L, 7, to0);
+            CLF_T(tl0);
             // ---- plant step + noise
             xl = plant_step<T, NX, NU, SP>(p, abl, cl, L.xs, xl, u0, w, lane);
+            CLF_TADD(L, 8, tl0);
             t = tn;
             if (p.iter_log && lane == 0) {
                 const long long kc = wall_clock64() - clk0;   // constant-rate ticks (hipDeviceAttributeWallClockRate)
@@ -1091,6 +1201,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             }
         }
         // ---- write back: state, sums, step, flags, status
+        CLF_T(tb0);
         cost = wave_sum(cost);
         aed = wave_sum(aed);
         if (lane < NX) p.state[(size_t)inst * NX + lane] = (T)xl;
@@ -1117,6 +1228,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(inst_t0 & 0x7fffffff);
             p.iter_log[(size_t)(p.target - p.step0 + 1) * p.B + inst] = (int)(wall_clock64() & 0x7fffffff);
         }
+#ifdef NMPC_CLF_TIMING
+        CLF_TADD(L, 9, tb0);
+        CLF_SYNC();
+        if (p.cycles && lane < CLF_NT) p.cycles[(size_t)inst * CLF_NT + lane] += (unsigned long long)L.tacc[lane];
+        CLF_SYNC();
+        if (lane < CLF_NT) L.tacc[lane] = 0;
+#endif
         CLF_SYNC();   // L.xs / L.fl of this instance are read before the next one overwrites them
     }
 }

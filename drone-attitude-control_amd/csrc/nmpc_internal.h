@@ -133,6 +133,7 @@ struct ClFastParams {
     int *status, *iters;
     int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
     int *iter_log;                // optional [steps][B]: active-set steps (<= 255) | status << 8 | wall-clock ticks (<= 32767) << 16
+    unsigned long long *cycles;   // diagnostic builds (NMPC_CLF_TIMING): [B][14] phase cycles / counts per instance
 };
 // compiled fast kernels: EPL slots per lane (0 if none for this shape)
 int cl_fast_epl(int nx, int nu);

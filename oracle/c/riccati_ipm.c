@@ -19,6 +19,7 @@
  *   s.t. x_{k+1} = A x_k + B u_k + c,   lb_k <= z_k <= ub_k  (|bound| >= 1e20: absent)
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -993,6 +994,9 @@ static void fast_free(fast_tables *f)
 /* element (k, i) is a decision variable of the QP (x_0 pinned; stage N has no inputs) */
 static int valid_el(int nx, int N, int k, int i) { return !(k == 0 && i < nx) && (k < N || i < nx); }
 
+/* tuning aid: env RIC_DEBUG_INST=<instance> prints the PDAS rounds of that instance (run with 1 thread) */
+static int ric_dbg = 0;
+
 /* The fast finish of one step (mode 1). wf: the warm set (shifted flags, in), the set reached
  * (out). Returns 1 and the solution in z (clamped onto the bounds) when accepted, else why not:
  * -2 a set larger than WSMAX, -3 a non-positive diagonal of W (never for a decision variable), -4
@@ -1099,6 +1103,11 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
         }
         const int addok = round == 0 || nrem == 0;
         int wbad = nrem;
+        if (ric_dbg) {
+            fprintf(stderr, "  round %d m=%d set:", round, m);
+            for (int i = 0; i < m; i++) fprintf(stderr, " %d.%d%c%s", S[i] / nz, S[i] % nz, wf[S[i]] < 0 ? 'l' : 'u', rem[i] ? "(rm)" : "");
+            fprintf(stderr, "\n");
+        }
         double cv[NZMAX];
         int ck[NZMAX];
         for (int i = 0; i < nz; i++) { cv[i] = 0.0; ck[i] = -1; }
@@ -1113,6 +1122,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
                 const double lb = LBk(d, k, c), ub = UBk(d, k, c);
                 if (wf[e]) {
                     const double bb = wf[e] < 0 ? lb : ub;
+                    if (ric_dbg && !(fabs(zz - bb) <= 1e-9 * (1.0 + fabs(bb)))) fprintf(stderr, "    held-miss %d.%d %.3g\n", k, c, zz - bb);
                     wbad += !(fabs(zz - bb) <= 1e-9 * (1.0 + fabs(bb)));
                     zz = bb;
                     for (int i = 0; i < m; i++)
@@ -1121,6 +1131,7 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
                     const int lo = has(lb) && zz < lb - 1e-13 * (1.0 + fabs(lb)), hi = has(ub) && zz > ub + 1e-13 * (1.0 + fabs(ub));
                     wbad += lo || hi || !isfinite(zz);
                     const double v = lo ? lb - zz : (hi ? zz - ub : 0.0);
+                    if (ric_dbg && (lo || hi)) fprintf(stderr, "    viol %d.%d %s %.3g\n", k, c, lo ? "lo" : "hi", v);
                     if (c >= nx && (lo || hi)) nf_[e] = lo ? -1 : 1;   /* inputs join at once */
                     if (c < nx && v > cv[c]) { cv[c] = v; ck[c] = k; }
                 }
@@ -1540,9 +1551,12 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
         double *xo = (double *)malloc(sizeof(double) * (N + 1) * nx), *uo = (double *)malloc(sizeof(double) * N * nu);
         double *z0 = (double *)malloc(sizeof(double) * ne), *zf = (double *)malloc(sizeof(double) * ne);
         signed char *wf = (signed char *)malloc(ne), *w0 = (signed char *)malloc(ne);
+        const char *dbg_env = getenv("RIC_DEBUG_INST");
+        const int dbg_inst = dbg_env ? atoi(dbg_env) : -1;
 #pragma omp for schedule(dynamic, 4)
         for (int b = 0; b < batch; b++) {
             double *st = state + (size_t)b * nx;
+            ric_dbg = b == dbg_inst;
             signed char *ab = act ? act + (size_t)b * ne : NULL;
             int gi_prev = 0;   /* the previous step of this call ran the dual fallback (a kernel launch's
                                 * register: one call here = one launch there) */
@@ -1551,6 +1565,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                 for (int k = 0; k < N; k++) memcpy(yref + (size_t)k * ny, c->table + (size_t)(t + k) * c->cols, sizeof(double) * ny);
                 memcpy(yref + (size_t)N * ny, c->table + (size_t)(t + N) * c->cols, sizeof(double) * nye);
                 int status = 0, path = 2, iters = 0, ok = 0;
+                if (ric_dbg) fprintf(stderr, "step %d t=%d\n", step, t);
                 /* mode 1 tries the fast path from the first step on (an empty warm set at step 0) */
                 const int warm = mode == 1 && ab != NULL;
                 if (warm) {   /* the previous solution's flags shifted by one stage */

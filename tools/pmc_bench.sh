@@ -24,6 +24,6 @@ for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
   timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d $PWD/$OUT/pmc_${TAG}_$i -o run -- python3 bench.py $ARGS > $OUT/pmc_${TAG}_$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $OUT/pmc_${TAG}_$i.log; exit 1; }
 done
 SPL=$STEPS; [ "$MODE" = "solve" ] && SPL=1
-python tools/pmc_summary.py $TAG --kernel ${KERNEL:-cl_fast_kernel} --out profiles/${TAG}_pmc.json \
+python tools/pmc_summary.py $TAG --kernel ${KERNEL:-cl_fast_kernel} --out gpurun_out/${TAG}_pmc.json \
     ${TRAFFIC:+--traffic $TRAFFIC} --steps-per-launch $SPL --mode $MODE > /dev/null || { echo "pmc summary failed"; exit 1; }
 echo "pmc $TAG done"
