@@ -421,7 +421,7 @@ class AcadosOcpSolver:
         return {"instances_per_wave": out[0], "workgroups": out[1], "threads": out[2], "lds_bytes": out[3],
                 "kernel": {0: "ipm_kernel", 1: "ipm_lpc_kernel", 2: "cond_ipm_kernel", 3: "ipm_lpi_kernel"}.get(out[4], str(out[4])),
                 "structure": {0: "dense", 1: "force", 2: "jerk", 3: "quad13"}.get(out[5], str(out[5])),
-                "closed_loop_kernel": "cl_fast_kernel" if out[6] else "fused",
+                "closed_loop_kernel": {0: "fused", 1: "cl_fast_kernel", 2: "cl_lock_kernel"}.get(out[6], str(out[6])),
                 "active_set_max": out[7]}
 
     def discrete_model(self):

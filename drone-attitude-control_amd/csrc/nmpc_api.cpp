@@ -229,6 +229,7 @@ struct nmpc_solver {
     int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
     int clf_resident = 0;                  // workgroups of cl_fast_kernel the handle's device holds at once
+    bool clf_lock = false;                 // the lockstep kernel (cl_lock_kernel) runs the lean loop
     int clf_parked = 0, clf_rounds = 0;    // the last run: parked solves (list-mode full solves), fast launches
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
     std::vector<float> tmp_x0f, tmp_yf;
@@ -1381,7 +1382,7 @@ int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
     const bool f64 = h->precision == NMPC_FP64;
     const int kind = h->cond ? 2 : f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
     const int sid = h->cond ? 0 : f64 ? nmpc::ipm_structure<double>(h->kidx) : nmpc::ipm_structure<float>(h->kidx);
-    const int v[8] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid, h->clf ? 1 : 0,
+    const int v[8] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid, h->clf ? (h->clf_lock ? 2 : 1) : 0,
                       h->clf ? nmpc::cl_fast_wsmax(h->nx, h->nu) : 0};
     for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
     return 0;
@@ -1617,8 +1618,17 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     if (e == hipSuccess) e = hipMemset(h->d_istep, 0, (size_t)h->batch * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * nslot);
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init lean tables");
+    // the lockstep kernel for the shapes that have one, with the controller-model plant and the cost on x_0
+    // (env NMPC_CLF_LOCK=0: the one-instance-per-wavefront kernel)
+    const char *lenv = std::getenv("NMPC_CLF_LOCK");
+    h->clf_lock = nmpc::cl_lock_shape(nx, nu) && d.plant == NMPC_PLANT_MODEL && d.cost_stage == 0 && !(lenv && lenv[0] == '0');
     // resident workgroups on this handle's device (nmpc_closed_loop_init runs on it: hipSetDevice above)
-    h->clf_resident = nmpc::cl_fast_resident(nx, nu, nmpc::ipm_structure<double>(fk), h->device);
+    h->clf_resident = nmpc::cl_fast_resident(nx, nu, nmpc::ipm_structure<double>(fk), h->clf_lock, h->device);
+    // the lockstep kernel's per-workgroup queue holds at most 512 demoted instances
+    if (h->clf_lock && h->clf_resident > 0 && (h->batch + h->clf_resident - 1) / h->clf_resident > 512) {
+        h->clf_lock = false;
+        h->clf_resident = nmpc::cl_fast_resident(nx, nu, nmpc::ipm_structure<double>(fk), false, h->device);
+    }
     if (h->clf_resident <= 0) return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_init: lean closed-loop occupancy query");
     h->clf = true;
     h->clf_nslot = nslot;
@@ -1694,6 +1704,8 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     // not settle parks and takes the list-mode full solve (tests/test_gpu_bench_parity.py forces parks)
     const char *nogi = std::getenv("NMPC_CLF_NO_GI");
     p.gi = (nogi && nogi[0] == '1') ? 0 : 1;
+    const char *lw = std::getenv("NMPC_LOCK_WORKERS");
+    p.lock_workers = lw ? std::max(0, std::min(4, std::atoi(lw))) : 0;
     return p;
 }
 
@@ -1764,7 +1776,7 @@ int clf_run(nmpc_solver *h, int steps)
         for (int round = 0; round <= n; round++) {
             if ((e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
             hipEventRecord(cl_event(h, 2 * launches), h->stream);
-            e = nmpc::cl_fast_launch<double>(h->nx, h->nu, h->clf_sid, fp, h->batch, h->clf_resident, h->stream);
+            e = nmpc::cl_fast_launch<double>(h->nx, h->nu, h->clf_sid, h->clf_lock, fp, h->batch, h->clf_resident, h->stream);
             hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
             launches++;
             h->clf_rounds++;

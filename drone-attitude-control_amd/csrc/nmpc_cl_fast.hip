@@ -984,6 +984,191 @@ __device__ int slow_step(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> 
     return status | (ok ? 1 << 8 : 0) | (ran_gi ? 1 << 9 : 0) | (m_acc << 10) | (min(iters, 0x3fff) << 18);
 }
 
+// One instance's closed-loop steps up to p.target on the whole wavefront (cl_fast_kernel's instance loop,
+// and the lockstep kernel's rare path): record load, per step the warm-start shift, the explicit form
+// (explicit_form(z, vt): z = v_t + T_x x at the lane's slots, x in L.xs), the bound test, slow_step when
+// needed, flags, u0, cost / AED, the outputs at the last step, the plant; write-back (or park).
+template <typename T, int NX, int NU, int EPL, int WSM, class SP, class LdsT, class ExplicitF>
+__device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane,
+                                             const double *abl, const double *cl, int inst, ExplicitF &&explicit_form)
+{
+    constexpr int NZ = NX + NU, NSLOT = EPL * 64;
+    const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
+    const double wl = lane < p.ncl ? (double)p.wcl[lane] : 0.0;   // this lane's cost weight
+    double uin[NU];                                                // inputs of a failed step (mid-box)
+#pragma unroll
+    for (int i = 0; i < NU; i++) uin[i] = (double)p.uinit[i];
+    CLF_T(tr0);
+    const long long inst_t0 = p.iter_log ? wall_clock64() : 0;
+    // the instance's record, issued together: step, state (lane i < NX holds x_i), active flags of the
+    // last solution by slot (bit 2j lower, 2j+1 upper; meaningful after step 0), offset, status
+    int step = p.istep[inst];
+    double xl = lane < NX ? (double)p.state[(size_t)inst * NX + lane] : 0.0;
+    signed char fb[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; j++) {
+        const int s = j * 64 + lane;
+        fb[j] = s < p.nslot ? p.flags[(size_t)inst * p.nslot + s] : 0;
+    }
+    const unsigned off = (unsigned)p.offset[inst];
+    const int st_prev = p.status[inst];
+    if (step >= p.target) return;
+    unsigned fl = 0;
+    if (step > 0) {
+#pragma unroll
+        for (int j = 0; j < EPL; j++) fl |= (fb[j] < 0 ? 1u : (fb[j] > 0 ? 2u : 0u)) << (2 * j);
+    }
+    int t = (int)((off % (unsigned)p.period + (unsigned)step % (unsigned)p.period) % (unsigned)p.period);
+    double cost = 0.0, aed = 0.0;   // this lane's terms (component lane), summed over the wave at the end
+    int nfail = 0, nst = 0;
+    int last_status = step > 0 ? st_prev : 0, last_iters = 0;
+    bool last_gi = false;   // the previous step of this launch ran the dual fallback
+    bool parked = false;
+    // v_t at the slots one step ahead (the step's first dependency); the reference component and the
+    // noise draw are issued at the top of the step and consumed after the solve
+    T vtn[EPL];
+    auto fetch_v = [&](int tt) {
+        const T *vp = p.vb + (size_t)tt * NSLOT;
+#pragma unroll
+        for (int j = 0; j < EPL; j++) vtn[j] = vp[j * 64 + lane];
+    };
+    fetch_v(t);
+    CLF_TADD(L, 9, tr0);
+    for (; step < p.target; step++) {
+        const long long clk0 = p.iter_log ? wall_clock64() : 0;
+        CLF_T(tp0);
+        T vt[EPL];
+#pragma unroll
+        for (int j = 0; j < EPL; j++) vt[j] = vtn[j];
+        const int tn = t + 1 == p.period ? 0 : t + 1;
+        if (step + 1 < p.target) fetch_v(tn);
+        const double xr = lane < nref ? (double)p.table[(size_t)t * p.table_cols + lane] : 0.0;
+        const double w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
+        if (lane < NX) L.xs[lane] = xl;
+        // ---- warm start: the last solution's flags shifted by one stage (slot source)
+        unsigned wf = 0;
+        if (__any(fl != 0)) {
+#pragma unroll
+            for (int j = 0; j < EPL; j++) L.fl[j * 64 + lane] = flag_of(fl, j);
+            CLF_SYNC();
+#pragma unroll
+            for (int j = 0; j < EPL; j++) {
+                const int sr_ = sv.src(j);
+                wf |= bits_of(sr_ >= 0 ? L.fl[sr_] : (signed char)0) << (2 * j);
+            }
+        }
+        CLF_SYNC();
+        CLF_TADD(L, 0, tp0);
+        CLF_T(te0);
+        // ---- explicit unconstrained solution at the lane's slots (the kernel's functor; x in L.xs)
+        T z[EPL];
+        explicit_form(z, vt);
+        bool ok = false;
+        int status = 0, iters = 1, m_acc = 0;
+        const bool gi_prev = last_gi;
+        last_gi = false;
+        if (!__any(wf != 0)) {
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < EPL; j++) bad |= !(z[j] >= (T)sv.lo(j) && z[j] <= (T)sv.hi(j));   // NaN: bad
+            ok = !__any(bad);
+        }
+        CLF_TADD(L, 1, te0);
+        CLF_TCNT(L, 13, 1);
+        if (!ok) {
+            CLF_TCNT(L, 12, 1);
+            const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, wf, last_status == 4, gi_prev);
+            status = sr & 0xff;
+            last_gi = (sr >> 9) & 1;
+            ok = (sr >> 8) & 1;
+            m_acc = (sr >> 10) & 0xff;
+            iters = sr >> 18;
+            if (!ok && status != 4) {
+                parked = true;
+                break;
+            }
+        }
+        // ---- the solution's active flags (z on a bound to 1e-7): the next step's warm start
+        fl = 0;
+        if (status == 0) {
+#pragma unroll
+            for (int j = 0; j < EPL; j++)
+                fl |= (z[j] <= (T)sv.onl(j) ? 1u : (z[j] >= (T)sv.onu(j) ? 2u : 0u)) << (2 * j);
+        }
+        // ---- u0 (slots 0..nu-1: lanes 0..nu-1 of j = 0), clamped onto its bound
+        const T z0c = fmin(fmax(z[0], (T)sv.lb(0)), (T)sv.ub(0));
+        double u0[NU];
+#pragma unroll
+        for (int i = 0; i < NU; i++) u0[i] = status == 0 ? bcast((double)z0c, i) : uin[i];
+        // ---- cost (controller.py:40-41) at x_0 = the state, or x_1 (jerk loop), and the AED numerator:
+        // lane i adds component i
+        {
+            double xo = xl;
+            if (p.cost_stage != 0) {
+                const double x1 = __shfl((double)z0c, p.x1_slot + lane);
+                xo = status == 0 ? x1 : (lane < NX ? (double)init_point(p, NX, NZ, 1, lane, t, T(0)) : 0.0);
+            }
+            const double e = xo - xr;
+            if (lane < p.ncl) cost = fma(wl * e, e, cost);
+            if (lane < p.aed_dims) aed += fabs(xr - xl);
+        }
+        nfail += status != 0;
+        nst++;
+        last_status = status;
+        last_iters = iters;
+        // ---- the trajectory outputs of the instance's last step of the run
+        CLF_T(to0);
+        if (step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, t, status, m_acc, z);
+        CLF_TADD(L, 7, to0);
+        CLF_T(tl0);
+        // ---- plant step + noise
+        xl = plant_step<T, NX, NU, SP>(p, abl, cl, L.xs, xl, u0, w, lane);
+        CLF_TADD(L, 8, tl0);
+        t = tn;
+        if (p.iter_log && lane == 0) {
+            const long long kc = wall_clock64() - clk0;   // constant-rate ticks (hipDeviceAttributeWallClockRate)
+            p.iter_log[(size_t)(step - p.step0) * p.B + inst] =
+                (iters < 255 ? iters : 255) | (status << 8) | ((int)(kc < 32767 ? kc : 32767) << 16);
+        }
+    }
+    // ---- write back: state, sums, step, flags, status
+    CLF_T(tb0);
+    cost = wave_sum(cost);
+    aed = wave_sum(aed);
+    if (lane < NX) p.state[(size_t)inst * NX + lane] = (T)xl;
+    if (lane < 4)   // lanes 0..3: [cost, AED numerator, failures, steps], added in the L2 (no return:
+                    // nothing waits for the old sums; each instance's sums have one writer)
+        unsafeAtomicAdd(p.acc + (size_t)inst * 4 + lane, lane == 0 ? cost : lane == 1 ? aed : lane == 2 ? (double)nfail : (double)nst);
+    if (lane == 0) {
+        p.istep[inst] = step;
+        if (parked) {
+            const int pos = atomicAdd(p.park_count, 1);
+            p.park_list[pos] = inst;
+        } else {
+            p.status[inst] = last_status;
+            p.iters[inst] = last_iters;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < EPL; j++) {
+        const int s = j * 64 + lane;
+        if (s < p.nslot) p.flags[(size_t)inst * p.nslot + s] = flag_of(fl, j);
+    }
+    if (p.iter_log && lane == 0) {   // the instance's start and end in this launch (rows target - step0 + 0 / 1,
+        // wall-clock ticks, low 31 bits)
+        p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(inst_t0 & 0x7fffffff);
+        p.iter_log[(size_t)(p.target - p.step0 + 1) * p.B + inst] = (int)(wall_clock64() & 0x7fffffff);
+    }
+#ifdef NMPC_CLF_TIMING
+    CLF_TADD(L, 9, tb0);
+    CLF_SYNC();
+    if (p.cycles && lane < CLF_NT) p.cycles[(size_t)inst * CLF_NT + lane] += (unsigned long long)L.tacc[lane];
+    CLF_SYNC();
+    if (lane < CLF_NT) L.tacc[lane] = 0;
+#endif
+    CLF_SYNC();   // L.xs / L.fl of this instance are read before the next one overwrites them
+}
+
 // WPB wavefronts per workgroup (the slot tables in LDS are shared by them), MW the occupancy target
 // (waves per SIMD; 0: none)
 template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
@@ -1051,70 +1236,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         if (lane == 0) next = atomicAdd(&wg_next, 1);
         const int inst = wg_lo + __builtin_amdgcn_readfirstlane(next);
         if (inst >= wg_hi) break;
-        CLF_T(tr0);
-        const long long inst_t0 = p.iter_log ? wall_clock64() : 0;
-        // the instance's record, issued together: step, state (lane i < NX holds x_i), active flags of the
-        // last solution by slot (bit 2j lower, 2j+1 upper; meaningful after step 0), offset, status
-        int step = p.istep[inst];
-        double xl = lane < NX ? (double)p.state[(size_t)inst * NX + lane] : 0.0;
-        signed char fb[EPL];
-#pragma unroll
-        for (int j = 0; j < EPL; j++) {
-            const int s = j * 64 + lane;
-            fb[j] = s < p.nslot ? p.flags[(size_t)inst * p.nslot + s] : 0;
-        }
-        const unsigned off = (unsigned)p.offset[inst];
-        const int st_prev = p.status[inst];
-        if (step >= p.target) continue;
-        unsigned fl = 0;
-        if (step > 0) {
-#pragma unroll
-            for (int j = 0; j < EPL; j++) fl |= (fb[j] < 0 ? 1u : (fb[j] > 0 ? 2u : 0u)) << (2 * j);
-        }
-        int t = (int)((off % (unsigned)p.period + (unsigned)step % (unsigned)p.period) % (unsigned)p.period);
-        double cost = 0.0, aed = 0.0;   // this lane's terms (component lane), summed over the wave at the end
-        int nfail = 0, nst = 0;
-        int last_status = step > 0 ? st_prev : 0, last_iters = 0;
-        bool last_gi = false;   // the previous step of this launch ran the dual fallback
-        bool parked = false;
-        // v_t at the slots one step ahead (the step's first dependency); the reference component and the
-        // noise draw are issued at the top of the step and consumed after the solve
-        T vtn[EPL];
-        auto fetch_v = [&](int tt) {
-            const T *vp = p.vb + (size_t)tt * NSLOT;
-#pragma unroll
-            for (int j = 0; j < EPL; j++) vtn[j] = vp[j * 64 + lane];
-        };
-        fetch_v(t);
-        CLF_TADD(L, 9, tr0);
-        for (; step < p.target; step++) {
-            const long long clk0 = p.iter_log ? wall_clock64() : 0;
-            CLF_T(tp0);
-            T vt[EPL];
-#pragma unroll
-            for (int j = 0; j < EPL; j++) vt[j] = vtn[j];
-            const int tn = t + 1 == p.period ? 0 : t + 1;
-            if (step + 1 < p.target) fetch_v(tn);
-            const double xr = lane < nref ? (double)p.table[(size_t)t * p.table_cols + lane] : 0.0;
-            const double w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
-            if (lane < NX) L.xs[lane] = xl;
-            // ---- warm start: the last solution's flags shifted by one stage (slot source)
-            unsigned wf = 0;
-            if (__any(fl != 0)) {
-#pragma unroll
-                for (int j = 0; j < EPL; j++) L.fl[j * 64 + lane] = flag_of(fl, j);
-                CLF_SYNC();
-#pragma unroll
-                for (int j = 0; j < EPL; j++) {
-                    const int sr_ = sv.src(j);
-                    wf |= bits_of(sr_ >= 0 ? L.fl[sr_] : (signed char)0) << (2 * j);
-                }
-            }
-            CLF_SYNC();
-            CLF_TADD(L, 0, tp0);
-            CLF_T(te0);
-            // ---- explicit unconstrained solution at the lane's slots (x pairs broadcast from LDS)
-            T z[EPL], z1[EPL];
+        // explicit unconstrained solution at the lane's slots: T_x pairs from LDS against x pairs broadcast
+        run_instance<T, NX, NU, EPL, WSM, SP>(p, L, sv, lane, abl, cl, inst, [&](T(&z)[EPL], const T(&vt)[EPL]) {
+            T z1[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 z[j] = vt[j];
@@ -1132,110 +1256,413 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             }
 #pragma unroll
             for (int j = 0; j < EPL; j++) z[j] += z1[j];
-            bool ok = false;
-            int status = 0, iters = 1, m_acc = 0;
-            const bool gi_prev = last_gi;
-            last_gi = false;
-            if (!__any(wf != 0)) {
-                bool bad = false;
+        });
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// The lockstep closed loop (quad13-class shapes: controller-model plant, cost on x_0): four instances per
+// wavefront advance together and the step's dense products run on the matrix cores. Two phases per
+// workgroup, so the lockstep registers and the single-instance rare path never coexist:
+//
+// Phase 1, lockstep (the common path):
+//   * explicit form Z = V + T_x X for four instances at once on v_mfma_f64_4x4x4_4b_f64: M = slots in tiles
+//     of 16 (4 blocks of 4 rows), K = state components in chunks of 4, N = the 4 instances
+//     (A[b][i][k] = lane 16k + 4b + i, B[b][k][n] = lane 16k + 4b + n, D[b][i][n] = lane 16i + 4b + n,
+//     pinned by tools/ubench/mfma_f64_layout.hip). T_x sits in LDS in A-operand order (one conflict-free
+//     8-byte read per lane per MFMA), the states X are the B operand straight from registers (lane
+//     16k + 4b + n holds component 4 kc + k of instance n, all four blocks), V (the window's v_t at the
+//     lane's slots, loaded one step ahead) the accumulators' initial value. Lane l owns instance n = l & 3
+//     and the slots 16 t + 4 ((l >> 2) & 3) + (l >> 4), t < NT;
+//   * the bound test and the warm-start flags per lane, one ballot per wave: an instance whose z_0 meets
+//     every bound (1e-13) and whose last solution touched none is solved (cl_fast_kernel's fast path);
+//   * the plant X' = [A B] [X; U] + c as five more MFMAs (K = 16 states + 4 inputs), the result moved back
+//     into the B-operand layout by four lane permutes; cost / AED on the lanes of block 0;
+//   * an instance that needs the rare path (a violated bound, or a nonempty warm set) is demoted: its
+//     record goes back to memory (state, step, flags, sums so far) and into the workgroup's LDS queue, and
+//     the slot takes the next instance. Its last step's trajectory outputs are written from the lockstep
+//     layout.
+// Phase 2: each wavefront whose slots ran dry takes demoted instances from the queue and runs them to the
+// target with the single-instance code (run_instance: slow_step's PDAS on W, certificate, dual fallback,
+// parks; the explicit form on the same MFMA tiles), until every wavefront of the workgroup has left phase 1
+// and the queue is empty (all of a workgroup's wavefronts are co-resident: the wait always ends).
+// Same decisions, thresholds and outputs as cl_fast_kernel (oracle/c/riccati_ipm.c mode 1); only the
+// summation order of the explicit form and the plant differs (rounding).
+constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host checks B / grid <= LOCK_QCAP)
+
+template <typename T, int NX, int NU, int EPL, int WSM, int WPB, class SP>
+__global__ __launch_bounds__(64 * WPB) void cl_lock_kernel(ClFastParams<T> p)
+{
+    constexpr int NZ = NX + NU, NSLOT = EPL * 64, NT = NSLOT / 16, KC = (NX + 3) / 4, KU = (NU + 3) / 4;
+    static_assert(NX <= 16 && NU <= 4 && NZ <= 64 && NT <= 32, "lockstep layout: states in 4 chunks, inputs in one");
+    __shared__ Lds<NSLOT, NZ, WSM> lds_all[WPB];
+    __shared__ double zb_all[WPB][NSLOT];               // z staging in slot order (phase 2's explicit form)
+    __shared__ signed char flb_all[WPB][4][NSLOT];      // each slot's last solution flags, slot order
+    __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT], slo[NSLOT], shi[NSLOT], sol[NSLOT], sou[NSLOT];
+    __shared__ int sse[NSLOT], ssrc[NSLOT];
+    __shared__ double txA[NT][KC][64];                  // T_x in A-operand order
+    __shared__ double2 lohi[NSLOT], onb[NSLOT];         // (lo, hi) violation / (onl, onu) on-bound thresholds
+    __shared__ int dq[LOCK_QCAP];                       // demoted instances (-1: slot not yet written)
+    __shared__ int wg_next, dq_tail, dq_head, ph1_done;
+    for (int e = threadIdx.x; e < NT * KC * 64; e += 64 * WPB) {
+        const int t = e / (KC * 64), kc = (e / 64) % KC, l = e % 64;
+        const int s_ = 16 * t + 4 * ((l >> 2) & 3) + (l & 3), c = 4 * kc + (l >> 4);
+        txA[t][kc][l] = (s_ < p.nslot && c < NX) ? (double)p.s_tx[(size_t)s_ * NX + c] : 0.0;
+    }
+    for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) {
+        const int i = e / NZ, j = e % NZ;
+        abl[e] = SP::ab(i, j) ? (double)p.AB[e] : 0.0;
+    }
+    for (int e = threadIdx.x; e < NX; e += 64 * WPB) cl[e] = (double)p.c[e];
+    for (int s = threadIdx.x; s < NSLOT; s += 64 * WPB) {
+        const bool v = s < p.nslot;
+        const double l = v ? (double)p.s_lb[s] : -1e30, u = v ? (double)p.s_ub[s] : 1e30;
+        const bool hl = has_b(l), hu = has_b(u);
+        slb[s] = l;
+        sub[s] = u;
+        slo[s] = hl ? l - 1e-13 * (1.0 + fabs(l)) : -DBL_MAX;
+        shi[s] = hu ? u + 1e-13 * (1.0 + fabs(u)) : DBL_MAX;
+        sol[s] = hl ? l + 1e-7 * (1.0 + fabs(l)) : -DBL_MAX;
+        sou[s] = hu ? u - 1e-7 * (1.0 + fabs(u)) : DBL_MAX;
+        lohi[s] = make_double2(slo[s], shi[s]);
+        onb[s] = make_double2(sol[s], sou[s]);
+        sse[s] = v ? p.s_e[s] : -1;
+        ssrc[s] = v ? p.s_src[s] : -1;
+    }
+    for (int e = threadIdx.x; e < LOCK_QCAP; e += 64 * WPB) dq[e] = -1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
+    double *zb = zb_all[wave];
+    signed char(*flb)[NSLOT] = flb_all[wave];
+    if (lane < 32) L.xs[lane] = 0.0;
+#ifdef NMPC_CLF_TIMING
+    if (lane < CLF_NT) L.tacc[lane] = 0;
+#endif
+    if (threadIdx.x == 0) wg_next = dq_tail = dq_head = ph1_done = 0;
+    __syncthreads();
+    const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
+    const int n = lane & 3, ti = lane >> 4, tb = (lane >> 2) & 3;   // instance slot; D-layout slot offset
+    const int prow = lane & 15, drow = 4 * tb + ti;                 // plant A-operand row; D row
+    auto slot_of = [&](int q) { return 16 * q + 4 * tb + ti; };
+
+    // the workgroup's contiguous instance range (persistent grid)
+    const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int wg_lo = (int)blockIdx.x * per_wg, wg_hi = min(p.B, wg_lo + per_wg);
+
+    // ================= phase 1: lockstep (the workgroup's last wavefront starts as a phase-2 worker when
+    // NMPC_LOCK_WORKERS_FIRST (p.lock_workers) is set: the queued chains start at once)
+    if (wave < WPB - p.lock_workers) {
+        // per-instance state, replicated on the 16 lanes of its slot
+        int inst = -1, step = 0, t = 0, last_status = 0, nfail = 0, nst = 0;
+        bool flany = false;
+        double cost = 0.0, aed = 0.0;
+        long long inst_t0 = 0;
+        double xr[KC];
+        T vt[NT];
 #pragma unroll
-                for (int j = 0; j < EPL; j++) bad |= !(z[j] >= (T)sv.lo(j) && z[j] <= (T)sv.hi(j));   // NaN: bad
-                ok = !__any(bad);
+        for (int kc = 0; kc < KC; kc++) xr[kc] = 0.0;
+#pragma unroll
+        for (int q = 0; q < NT; q++) vt[q] = T(0);
+        auto fetch_v = [&](int tt) {
+            const T *vp = p.vb + (size_t)tt * NSLOT;
+#pragma unroll
+            for (int q = 0; q < NT; q++) vt[q] = vp[slot_of(q)];
+        };
+        // a new instance for every slot that wants one (lane q < 4 claims for slot q) and its record:
+        // step, state (B-operand layout), flags (slot order, LDS), offset, status; v of its first step
+        auto claim = [&](bool want) {
+            int nx_ = 0;
+            if (lane < 4 && want) nx_ = atomicAdd(&wg_next, 1);
+            nx_ = __shfl(nx_, n);
+            if (!want) return;
+            const int ni = wg_lo + nx_;
+            inst = ni < wg_hi ? ni : -1;
+            flany = false;
+            cost = aed = 0.0;
+            nfail = nst = 0;
+            if (inst < 0) return;
+            inst_t0 = p.iter_log ? wall_clock64() : 0;
+            step = p.istep[inst];
+            const unsigned off = (unsigned)p.offset[inst];
+            last_status = step > 0 ? p.status[inst] : 0;
+            t = (int)((off % (unsigned)p.period + (unsigned)step % (unsigned)p.period) % (unsigned)p.period);
+#pragma unroll
+            for (int kc = 0; kc < KC; kc++) {
+                const int c = 4 * kc + ti;
+                xr[kc] = c < NX ? (double)p.state[(size_t)inst * NX + c] : 0.0;
             }
-            CLF_TADD(L, 1, te0);
-            CLF_TCNT(L, 13, 1);
-            if (!ok) {
-                CLF_TCNT(L, 12, 1);
-                const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, wf, last_status == 4, gi_prev);
-                status = sr & 0xff;
-                last_gi = (sr >> 9) & 1;
-                ok = (sr >> 8) & 1;
-                m_acc = (sr >> 10) & 0xff;
-                iters = sr >> 18;
-                if (!ok && status != 4) {
-                    parked = true;
-                    break;
+            bool any = false;
+            for (int s = 4 * tb + ti; s < NSLOT; s += 16) {   // the slot's 16 lanes cover its flags
+                const signed char f = (s < p.nslot && step > 0) ? p.flags[(size_t)inst * p.nslot + s] : (signed char)0;
+                flb[n][s] = f;
+                any |= f != 0;
+            }
+            flany = (__ballot(any) & (0x1111111111111111ull << n)) != 0;
+            if (step < p.target) fetch_v(t);
+        };
+        // the instance's record back to memory (its slot's lanes): state, the sums so far (no-return f64
+        // atomics), step, status, flags; demote: into the workgroup queue for phase 2 (the record stores
+        // complete and are released at workgroup scope before the queue entry appears)
+        auto write_back = [&](bool demote) {
+            const long long t1 = p.iter_log ? wall_clock64() : 0;
+            double c_ = cost, a_ = aed;
+#pragma unroll
+            for (int o = 4; o < 64; o <<= 1) {
+                c_ += __shfl_xor(c_, o);
+                a_ += __shfl_xor(a_, o);
+            }
+            if (tb == 0) {
+#pragma unroll
+                for (int kc = 0; kc < KC; kc++) {
+                    const int c = 4 * kc + ti;
+                    if (c < NX) p.state[(size_t)inst * NX + c] = (T)xr[kc];
                 }
             }
-            // ---- the solution's active flags (z on a bound to 1e-7): the next step's warm start
-            fl = 0;
-            if (status == 0) {
-#pragma unroll
-                for (int j = 0; j < EPL; j++)
-                    fl |= (z[j] <= (T)sv.onl(j) ? 1u : (z[j] >= (T)sv.onu(j) ? 2u : 0u)) << (2 * j);
-            }
-            // ---- u0 (slots 0..nu-1: lanes 0..nu-1 of j = 0), clamped onto its bound
-            const T z0c = fmin(fmax(z[0], (T)sv.lb(0)), (T)sv.ub(0));
-            double u0[NU];
-#pragma unroll
-            for (int i = 0; i < NU; i++) u0[i] = status == 0 ? bcast((double)z0c, i) : uin[i];
-            // ---- cost (controller.py:40-41) at x_0 = the state, or x_1 (jerk loop), and the AED numerator:
-            // lane i adds component i
-            {
-                double xo = xl;
-                if (p.cost_stage != 0) {
-                    const double x1 = __shfl((double)z0c, p.x1_slot + lane);
-                    xo = status == 0 ? x1 : (lane < NX ? (double)init_point(p, NX, NZ, 1, lane, t, T(0)) : 0.0);
+            for (int s = 4 * tb + ti; s < p.nslot; s += 16) p.flags[(size_t)inst * p.nslot + s] = flany ? flb[n][s] : (signed char)0;
+            if (lane == n) {
+                if (nst > 0 || c_ != 0.0 || a_ != 0.0) {
+                    unsafeAtomicAdd(p.acc + (size_t)inst * 4 + 0, c_);
+                    unsafeAtomicAdd(p.acc + (size_t)inst * 4 + 1, a_);
+                    unsafeAtomicAdd(p.acc + (size_t)inst * 4 + 2, (double)nfail);
+                    unsafeAtomicAdd(p.acc + (size_t)inst * 4 + 3, (double)nst);
                 }
-                const double e = xo - xr;
-                if (lane < p.ncl) cost = fma(wl * e, e, cost);
-                if (lane < p.aed_dims) aed += fabs(xr - xl);
-            }
-            nfail += status != 0;
-            nst++;
-            last_status = status;
-            last_iters = iters;
-            // ---- the trajectory outputs of the instance's last step of the run
-            CLF_T(to0);
-            if (step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, t, status, m_acc, z);
-            CLF_TADD(L, 7, to0);
-            CLF_T(tl0);
-            // ---- plant step + noise
-            xl = plant_step<T, NX, NU, SP>(p, abl, cl, L.xs, xl, u0, w, lane);
-            CLF_TADD(L, 8, tl0);
-            t = tn;
-            if (p.iter_log && lane == 0) {
-                const long long kc = wall_clock64() - clk0;   // constant-rate ticks (hipDeviceAttributeWallClockRate)
-                p.iter_log[(size_t)(step - p.step0) * p.B + inst] =
-                    (iters < 255 ? iters : 255) | (status << 8) | ((int)(kc < 32767 ? kc : 32767) << 16);
-            }
-        }
-        // ---- write back: state, sums, step, flags, status
-        CLF_T(tb0);
-        cost = wave_sum(cost);
-        aed = wave_sum(aed);
-        if (lane < NX) p.state[(size_t)inst * NX + lane] = (T)xl;
-        if (lane < 4)   // lanes 0..3: [cost, AED numerator, failures, steps], added in the L2 (no return:
-                        // nothing waits for the old sums; each instance's sums have one writer)
-            unsafeAtomicAdd(p.acc + (size_t)inst * 4 + lane, lane == 0 ? cost : lane == 1 ? aed : lane == 2 ? (double)nfail : (double)nst);
-        if (lane == 0) {
-            p.istep[inst] = step;
-            if (parked) {
-                const int pos = atomicAdd(p.park_count, 1);
-                p.park_list[pos] = inst;
-            } else {
+                p.istep[inst] = step;
                 p.status[inst] = last_status;
-                p.iters[inst] = last_iters;
+                if (!demote) p.iters[inst] = 1;
+                if (p.iter_log && !demote) {
+                    p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(inst_t0 & 0x7fffffff);
+                    p.iter_log[(size_t)(p.target - p.step0 + 1) * p.B + inst] = (int)(t1 & 0x7fffffff);
+                }
             }
-        }
+            if (demote) {
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == n) {
+                    const int pos = atomicAdd(&dq_tail, 1);
+                    __hip_atomic_store(&dq[pos], inst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        };
+        claim(true);
+        for (;;) {
+            CLF_T(tk_idle);
+            // slots whose instance is already at the target move on
+            for (int guard = 0; guard < per_wg + 4; guard++) {
+                const bool idle = inst >= 0 && step >= p.target;
+                if (!__any(idle)) break;
+                if (idle && nst > 0) write_back(false);   // finished here (nothing to write for one claimed at the target)
+                claim(idle);
+            }
+            CLF_TADD(L, 0, tk_idle);
+            if (!__any(inst >= 0)) break;
+            const bool act = inst >= 0;
+            const long long clk0 = p.iter_log ? wall_clock64() : 0;
+            CLF_T(tk_mf);
+            // ---- explicit unconstrained solutions of the four instances: Z = V + T_x X on the matrix cores
+            T z[NT];
 #pragma unroll
-        for (int j = 0; j < EPL; j++) {
-            const int s = j * 64 + lane;
-            if (s < p.nslot) p.flags[(size_t)inst * p.nslot + s] = flag_of(fl, j);
-        }
-        if (p.iter_log && lane == 0) {   // the instance's start and end in this launch (rows target - step0 + 0 / 1,
-            // wall-clock ticks, low 31 bits)
-            p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(inst_t0 & 0x7fffffff);
-            p.iter_log[(size_t)(p.target - p.step0 + 1) * p.B + inst] = (int)(wall_clock64() & 0x7fffffff);
+            for (int q = 0; q < NT; q++) z[q] = vt[q];
+#pragma unroll
+            for (int kc = 0; kc < KC; kc++) {
+                __builtin_amdgcn_sched_barrier(0);   // one K-chunk's A operands in flight at a time
+#pragma unroll
+                for (int q = 0; q < NT; q++) z[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(txA[q][kc][lane], xr[kc], z[q], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            CLF_TADD(L, 1, tk_mf);
+            CLF_T(tk_bt);
+            const int tn = t + 1 == p.period ? 0 : t + 1;
+            // ---- bound test and flags (lanes of instance n)
+            bool bad = false;
+            unsigned long long flm = 0;   // 2 bits per tile
+#pragma unroll
+            for (int q = 0; q < NT; q++) {
+                const double2 lh = lohi[slot_of(q)], ob = onb[slot_of(q)];
+                const double zz = (double)z[q];
+                bad |= !(zz >= lh.x && zz <= lh.y);   // NaN: bad
+                flm |= (unsigned long long)(zz <= ob.x ? 1u : (zz >= ob.y ? 2u : 0u)) << (2 * q);
+            }
+            const unsigned long long mslot = 0x1111111111111111ull << n;
+            const bool slow = act && ((__ballot(bad) & mslot) != 0 || flany);
+            const bool fany = (__ballot(flm != 0) & mslot) != 0;
+            const bool adv = act && !slow;
+            // the demoted: record back, into the queue; their slots refill below
+            if (slow) write_back(true);
+            // fast instances: flags (slot order, only when some bound is touched), u0 (slots 0..nu-1: tile 0,
+            // block 0, lanes 16 i + n) clamped
+            if (adv && fany) {
+#pragma unroll
+                for (int q = 0; q < NT; q++) flb[n][slot_of(q)] = flag_of((unsigned)(flm >> (q >= 16 ? 32 : 0)), q & 15);
+            }
+            if (adv) flany = fany;
+            double u0v = 0.0;
+            if (tb == 0 && ti < NU) u0v = fmin(fmax((double)z[0], slb[ti]), sub[ti]);
+            CLF_TADD(L, 19, tk_bt);
+            CLF_T(tk_out);
+            // the trajectory outputs of a fast instance's last step (write_outputs' success branch with an
+            // empty set): x_0 the state, the bounded elements z clamped, the unbounded ones from the full tables
+            if (__any(adv && step + 1 == p.target)) {
+                double xa[NX];   // the instance's whole state on each of its lanes
+#pragma unroll
+                for (int c = 0; c < NX; c++) xa[c] = __shfl(xr[c / 4], 16 * (c % 4) + n);
+                if (adv && step + 1 == p.target) {
+                    if (tb == 0) {
+#pragma unroll
+                        for (int kc = 0; kc < KC; kc++)
+                            if (4 * kc + ti < NX) p.xout[(size_t)inst * (p.N + 1) * NX + 4 * kc + ti] = (T)xr[kc];
+                    }
+#pragma unroll
+                    for (int q = 0; q < NT; q++) {
+                        const int s_ = slot_of(q), e = sse[s_];
+                        if (e < 0) continue;
+                        const T zc = fmin(fmax(z[q], (T)slb[s_]), (T)sub[s_]);
+                        const int k = e / NZ, r = e % NZ;
+                        if (r < NX) p.xout[((size_t)inst * (p.N + 1) + k) * NX + r] = zc;
+                        else p.uout[((size_t)inst * p.N + k) * NU + (r - NX)] = zc;
+                    }
+                    for (int qf = 4 * tb + ti; qf < p.nfree; qf += 16) {
+                        const int e = p.s_free[qf];
+                        const T *tr = p.txfull + (size_t)e * NX;
+                        T zz = p.vfull[(size_t)t * p.ne + e];
+#pragma unroll
+                        for (int c = 0; c < NX; c++) zz = fma(tr[c], (T)xa[c], zz);
+                        const int k = e / NZ, r = e % NZ;
+                        if (r < NX) p.xout[((size_t)inst * (p.N + 1) + k) * NX + r] = zz;
+                        else p.uout[((size_t)inst * p.N + k) * NU + (r - NX)] = zz;
+                    }
+                }
+            }
+            CLF_TADD(L, 7, tk_out);
+            CLF_T(tk_ld);
+            // ---- the next step's v (one step ahead), this step's reference row and noise draw
+            double w = 0.0;
+            if (adv) w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
+            double xrf[KC];
+#pragma unroll
+            for (int kc = 0; kc < KC; kc++) {
+                const int c = 4 * kc + ti;
+                xrf[kc] = (adv && tb == 0 && c < NX && (c < p.ncl || c < p.aed_dims)) ? (double)p.table[(size_t)t * p.table_cols + c] : 0.0;
+            }
+            if (adv && step + 1 < p.target) fetch_v(tn);
+            CLF_TADD(L, 18, tk_ld);
+            CLF_T(tk_pl);
+            // ---- cost (controller.py:40-41) at x_0 and the AED numerator: lanes 16 k + n (block 0)
+            if (adv && tb == 0) {
+#pragma unroll
+                for (int kc = 0; kc < KC; kc++) {
+                    const int c = 4 * kc + ti;
+                    if (c < NX) {
+                        const double e = xr[kc] - xrf[kc];
+                        if (c < p.ncl) cost = fma((double)p.wcl[c] * e, e, cost);
+                        if (c < p.aed_dims) aed += fabs(xrf[kc] - xr[kc]);
+                    }
+                }
+            }
+            // ---- plant X' = [A B] [X; U] + c + noise on the matrix cores: A operand [A B] (row prow, columns
+            // 4 kc + (lane >> 4); the inputs' chunk last) from the workgroup's copy, C = c + noise
+            {
+                double d = (drow < NX ? cl[drow] : 0.0) + ((drow < p.noise_dims && drow < NX) ? w : 0.0);
+#pragma unroll
+                for (int kc = 0; kc < KC; kc++) {
+                    const int c = 4 * kc + (lane >> 4);
+                    const double a = (prow < NX && c < NX) ? abl[prow * NZ + c] : 0.0;
+                    d = __builtin_amdgcn_mfma_f64_4x4x4f64(a, xr[kc], d, 0, 0, 0);
+                }
+                const double ub = __shfl(u0v, lane & 0x33);   // U[k][n] from lane 16 k + n
+#pragma unroll
+                for (int ku = 0; ku < KU; ku++) {
+                    const int c = 4 * ku + (lane >> 4);
+                    const double a = (prow < NX && c < NU) ? abl[prow * NZ + NX + c] : 0.0;
+                    d = __builtin_amdgcn_mfma_f64_4x4x4f64(a, ub, d, 0, 0, 0);
+                }
+                double xn[KC];
+#pragma unroll
+                for (int kc = 0; kc < KC; kc++) xn[kc] = __shfl(d, (lane & 0x33) | (kc << 2));
+                if (adv) {
+#pragma unroll
+                    for (int kc = 0; kc < KC; kc++) xr[kc] = xn[kc];
+                }
+            }
+            CLF_TADD(L, 8, tk_pl);
+            CLF_T(tk_bk);
+            // ---- step bookkeeping
+            if (adv) {
+                nst++;
+                last_status = 0;
+                if (p.iter_log && lane == n) {
+                    const long long kc_ = wall_clock64() - clk0;
+                    p.iter_log[(size_t)(step - p.step0) * p.B + inst] = 1 | ((int)(kc_ < 32767 ? kc_ : 32767) << 16);
+                }
+                step++;
+                t = tn;
+            }
+            CLF_SYNC();
+            claim(slow);   // the demoted instances' slots refill
+            CLF_TADD(L, 9, tk_bk);
+            CLF_TCNT(L, 13, 4);
         }
 #ifdef NMPC_CLF_TIMING
-        CLF_TADD(L, 9, tb0);
+        // phase 1's wave totals into the row of the workgroup's instance wg_lo + wave (tools/clf_phases.py sums)
         CLF_SYNC();
-        if (p.cycles && lane < CLF_NT) p.cycles[(size_t)inst * CLF_NT + lane] += (unsigned long long)L.tacc[lane];
+        if (p.cycles && lane < CLF_NT && wg_lo + wave < wg_hi) p.cycles[(size_t)(wg_lo + wave) * CLF_NT + lane] += (unsigned long long)L.tacc[lane];
         CLF_SYNC();
         if (lane < CLF_NT) L.tacc[lane] = 0;
 #endif
-        CLF_SYNC();   // L.xs / L.fl of this instance are read before the next one overwrites them
+    }
+    if (lane == 0) atomicAdd(&ph1_done, 1);
+
+    // ================= phase 2: the demoted instances, one at a time on the whole wavefront
+    for (;;) {
+        int got = -1, fin = 0;
+        if (lane == 0) {
+            for (;;) {
+                const int h = __hip_atomic_load(&dq_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int tl = __hip_atomic_load(&dq_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (h < tl) {
+                    if (atomicCAS(&dq_head, h, h + 1) == h) {
+                        int v;
+                        while ((v = __hip_atomic_load(&dq[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0)
+                            __builtin_amdgcn_s_sleep(1);
+                        got = v;
+                        break;
+                    }
+                    continue;
+                }
+                if (__hip_atomic_load(&ph1_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == WPB &&
+                    __hip_atomic_load(&dq_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == h) {
+                    fin = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        fin = __builtin_amdgcn_readfirstlane(fin);
+        if (fin) break;
+        const int inst = __builtin_amdgcn_readfirstlane(got);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // explicit form of one instance on the same MFMA tiles: all four B columns the instance's x (L.xs),
+        // the n = 0 lanes' results staged to slot order
+        run_instance<T, NX, NU, EPL, WSM, SP>(p, L, sv, lane, abl, cl, inst, [&](T(&z)[EPL], const T(&vt)[EPL]) {
+            T zq[NT];
+#pragma unroll
+            for (int q = 0; q < NT; q++) zq[q] = T(0);
+#pragma unroll
+            for (int kc = 0; kc < KC; kc++) {
+                __builtin_amdgcn_sched_barrier(0);
+                const double xk = L.xs[4 * kc + (lane >> 4)];
+#pragma unroll
+                for (int q = 0; q < NT; q++) zq[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(txA[q][kc][lane], xk, zq[q], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (n == 0) {
+#pragma unroll
+                for (int q = 0; q < NT; q++) zb[slot_of(q)] = (double)zq[q];
+            }
+            CLF_SYNC();
+#pragma unroll
+            for (int j = 0; j < EPL; j++) z[j] = vt[j] + (T)zb[j * 64 + lane];
+            CLF_SYNC();
+        });
     }
 }
 
@@ -1263,13 +1690,28 @@ struct Variant {
     static constexpr int WPB = WPB_;
     static constexpr auto kernel() { return clf::cl_fast_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_>; }
 };
+// the lockstep kernel (four instances per wavefront, MFMA explicit form and plant)
+template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, class SP_>
+struct LockVariant {
+    static constexpr int WPB = WPB_;
+    static constexpr auto kernel() { return clf::cl_lock_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, SP_>; }
+};
+
+// whether the shape has a lockstep kernel (controller-model plant, cost on x_0: checked by the host)
+bool cl_lock_shape(int nx, int nu) { return nx == 13 && nu == 4; }
 
 // calls f(Variant<...>{}) for the shape's compiled variant; false: none. NMPC_CLF_VARIANT=1 (tuning):
 // an occupancy target (quad13 4 waves per SIMD: spills, measured 10 % slower than the default)
 template <typename T, class F>
-static bool clf_dispatch(int nx, int nu, int sid, F &&f)
+static bool clf_dispatch(int nx, int nu, int sid, bool lock, F &&f)
 {
     static const int var = std::getenv("NMPC_CLF_VARIANT") ? std::atoi(std::getenv("NMPC_CLF_VARIANT")) : 0;
+    if (lock) {
+        if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::Quad13Structure>{});
+        else if (nx == 13 && nu == 4) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::DenseStructure<13, 4>>{});
+        else return false;
+        return true;
+    }
     if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) {
         if (var == 1) f(Variant<T, 13, 4, 4, 16, 8, 4, lpc::Quad13Structure>{});
         else f(Variant<T, 13, 4, 4, 16, 8, 0, lpc::Quad13Structure>{});
@@ -1288,10 +1730,10 @@ static bool clf_dispatch(int nx, int nu, int sid, F &&f)
 
 // the workgroups of the shape's kernel that `device` holds at once (the persistent grid), queried for
 // the given device at nmpc_closed_loop_init and kept on the handle (no process-wide cache)
-int cl_fast_resident(int nx, int nu, int sid, int device)
+int cl_fast_resident(int nx, int nu, int sid, bool lock, int device)
 {
     int res = 0;
-    clf_dispatch<double>(nx, nu, sid, [&](auto v) {
+    clf_dispatch<double>(nx, nu, sid, lock, [&](auto v) {
         using V = decltype(v);
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, V::kernel(), 64 * V::WPB, 0) != hipSuccess || per_cu < 1) return;
@@ -1303,16 +1745,19 @@ int cl_fast_resident(int nx, int nu, int sid, int device)
 
 // grid: min(workgroups for one wavefront per instance, the resident workgroups)
 template <typename T>
-hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, int resident, hipStream_t s)
+hipError_t cl_fast_launch(int nx, int nu, int sid, bool lock, const ClFastParams<T> &p, int waves, int resident,
+                          hipStream_t s)
 {
-    const bool ok = clf_dispatch<T>(nx, nu, sid, [&](auto v) {
+    const bool ok = clf_dispatch<T>(nx, nu, sid, lock, [&](auto v) {
         using V = decltype(v);
-        const int blocks = std::max(1, std::min((waves + V::WPB - 1) / V::WPB, resident));
+        // the lockstep kernel: four instances per wavefront
+        const int wv = lock ? (waves + 3) / 4 : waves;
+        const int blocks = std::max(1, std::min((wv + V::WPB - 1) / V::WPB, resident));
         hipLaunchKernelGGL(V::kernel(), dim3(blocks), dim3(64 * V::WPB), 0, s, p);
     });
     return ok ? hipGetLastError() : hipErrorInvalidValue;
 }
 
-template hipError_t cl_fast_launch<double>(int, int, int, const ClFastParams<double> &, int, int, hipStream_t);
+template hipError_t cl_fast_launch<double>(int, int, int, bool, const ClFastParams<double> &, int, int, hipStream_t);
 
 }  // namespace nmpc

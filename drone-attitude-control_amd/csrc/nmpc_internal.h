@@ -108,6 +108,7 @@ struct ClFastParams {
     int step0, noise_ld;          // noise[b][step - step0], row length noise_ld
     int polish_steps;             // active-set rounds of the fast path
     int gi;                       // 1: the dual active-set fallback runs; 0 (test knob): such steps park
+    int lock_workers;             // lockstep kernel: wavefronts per workgroup that start in phase 2
     int x1_slot;                  // slot (lane, j = 0) of x_1[0] (cost of the jerk loop: cost_stage 1)
     const T *table;               // reference table [rows][table_cols]
     const int *offset;            // [B]
@@ -139,11 +140,16 @@ struct ClFastParams {
 int cl_fast_epl(int nx, int nu);
 // largest active set of the fast path for the shape (oracle/cref.py WSMAX)
 int cl_fast_wsmax(int nx, int nu);
-// workgroups of the shape's cl_fast_kernel that `device` holds at once (the persistent grid), or 0
-int cl_fast_resident(int nx, int nu, int sid, int device);
-// grid = min(waves / wavefronts per workgroup, resident)
+// whether the shape has the lockstep kernel cl_lock_kernel (four instances per wavefront, MFMA explicit form
+// and plant; the controller-model plant with the cost on x_0 only)
+bool cl_lock_shape(int nx, int nu);
+// workgroups of the shape's cl_fast_kernel (lock: cl_lock_kernel) that `device` holds at once (the
+// persistent grid), or 0
+int cl_fast_resident(int nx, int nu, int sid, bool lock, int device);
+// grid = min(waves / wavefronts per workgroup, resident); waves = instances (lock: instances / 4)
 template <typename T>
-hipError_t cl_fast_launch(int nx, int nu, int sid, const ClFastParams<T> &p, int waves, int resident, hipStream_t s);
+hipError_t cl_fast_launch(int nx, int nu, int sid, bool lock, const ClFastParams<T> &p, int waves, int resident,
+                          hipStream_t s);
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);
 

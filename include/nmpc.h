@@ -188,8 +188,9 @@ int nmpc_get_stats(nmpc_solver *h, double *stats, int n);
  * out[4] = kernel family (1: lane per component — the default, nx+nu lanes per instance;
  * 0: one wavefront per instance block, env NMPC_KERNEL=wave), out[5] = model structure the
  * kernel is specialised for (0: dense; 1 force, 2 jerk, 3 quad13; env NMPC_STRUCT=0 forces dense),
- * out[6] = the closed loop's kernel after nmpc_closed_loop_init (1: the lean loop, cl_fast_kernel;
- * 0: the fused / per-step launches of the family above), out[7] = the lean loop's largest active set */
+ * out[6] = the closed loop's kernel after nmpc_closed_loop_init (1: the lean loop, cl_fast_kernel; 2: the
+ * lean loop's lockstep kernel cl_lock_kernel, four instances per wavefront on MFMA; 0: the fused / per-step
+ * launches of the family above), out[7] = the lean loop's largest active set */
 int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n);
 
 /* ------------------------------------------------------------------ batched closed loop

@@ -51,7 +51,8 @@ def test_bench_closed_loop_matches_oracle(golden, model, N, B):
     loop = ClosedLoop(model, B, N=N, seed=42)             # bench.py's workload and defaults
     info = loop.solver.launch_info()
     assert info["kernel"] in ("ipm_lpc_kernel", "ipm_kernel")
-    assert info["closed_loop_kernel"] == "cl_fast_kernel"   # the lean loop bench.py times
+    # the lean loop bench.py times (quad13: its lockstep MFMA kernel)
+    assert info["closed_loop_kernel"] == ("cl_lock_kernel" if model == "quad13" else "cl_fast_kernel")
     states, sums = [], []
     for n in REGIONS:
         loop.run(n)
