@@ -230,12 +230,16 @@ def main():
     cl = ClosedLoop(model, B, N=N, device=device if world > 1 else 0, precision=args.precision,
                     table=table, offsets=offsets_r, x_init=x_r, instance_base=base, seed=args.seed)
     nx, nu = cl.solver.nx, cl.solver.nu
+    info = cl.solver.launch_info()
+    # the lean loop runs the exact fast path in both precisions (fp32: fp32 tables and explicit form, fp64
+    # set solves and acceptance), so its CPU counterpart is the fp64 oracle loop with the exact finish
+    lean = info["closed_loop_kernel"] != "fused"
 
     # CPU baseline and the B=1 Python drop-in loop first (rank 0, single-GPU runs only)
     cpu, flops_cpu, pyloop = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, flops_cpu = cpu_baseline(model, N, table, offsets_r, x_r, args.warmup, args.repeats * args.steps,
-                                      args.cpu_seconds, args.precision, args.seed)
+                                      args.cpu_seconds, "fp64" if lean else args.precision, args.seed)
         if args.python_loop_steps > 0:
             pyloop = python_loop_rate(20, args.python_loop_steps)
             cpu["python_loop"] = pyloop
@@ -280,7 +284,6 @@ def main():
         fl_launch = fl_step * B
         achieved = fl_launch / (kernel_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.precision]
-        info = cl.solver.launch_info()
         kernel = info["closed_loop_kernel"] if info["closed_loop_kernel"] != "fused" else info["kernel"]
         spl = min(args.steps, 64)   # steps per launch of the timed regions (clf_run / fused chunks)
         pmc = load_pmc(model, N, B, args.precision, kernel, spl)
@@ -301,6 +304,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "fp64" else "f32",
+            "dtype_note": None if args.precision == "fp64" or not lean else
+            "fp32 handle on the lean loop: fp32 storage (tables, W, state, trajectories), explicit form and fast-path "
+            "bound tests in fp32; active-set solves, W[:, S] nu combinations and KKT acceptance in fp64",
             "data": "synthetic (seeded closed-loop Monte-Carlo instances on the reference circle)",
             "config": {"workload": workload_label(model, tols, cpu and cpu.get("paths_per_step")),
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,

@@ -222,6 +222,7 @@ struct nmpc_solver {
     int clf_kidx = -1;                     // list-mode fallback kernel (lane per component)
     void *d_clf_scratch = nullptr;         // its scratch when the handle's own family is another
     void *d_fsT = nullptr;                 // typed: s_lb, s_ub, s_tx, vb, uinit
+    double *d_clw = nullptr;               // fp32 handles: the lean loop's W in fp64 (fp64 handles: the model's)
     size_t fso[5] = {0, 0, 0, 0, 0};
     int *d_fsI = nullptr;                  // s_e, s_src, eslot
     size_t fsi[4] = {0, 0, 0, 0};
@@ -497,7 +498,7 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
                     (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
-                    (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch})
+                    (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -613,7 +614,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
             p.iter_log = h->d_iter_log;
             h->iter_log_steps = p.iter_log ? cl_steps : 0;
         }
-        const bool no_expl = std::getenv("NMPC_EXPLICIT") && std::getenv("NMPC_EXPLICIT")[0] == '0';
+        const bool no_expl = (std::getenv("NMPC_EXPLICIT") && std::getenv("NMPC_EXPLICIT")[0] == '0') ||
+                             h->precision != NMPC_FP64;   // the fused loop's fast finish: fp64 handles
         p.cl_tx = no_expl ? nullptr : (const T *)h->d_cltx;
         p.cl_v = no_expl ? nullptr : (const T *)h->d_clv;
     }
@@ -650,7 +652,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     // tuning / test switches, read per launch: NMPC_LQR=0 drops the shared factorisation (every finish
     // step factors), NMPC_FAST=0 / 2 the fast finish (2: not at a launch's first step),
     // NMPC_WARM_SHIFT=0 the warm-start shift
-    const bool no_lqr = (std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0') || h->lqr_host.empty();
+    const bool no_lqr = (std::getenv("NMPC_LQR") && std::getenv("NMPC_LQR")[0] == '0') || h->lqr_host.empty() ||
+                        h->precision != NMPC_FP64;   // fp32 handles: no exact finish, the tables are the lean loop's
     p.lqr = no_lqr ? nullptr : (const T *)(m + h->off_lqr);
     p.lqrf = no_lqr ? nullptr : (const T *)(m + h->off_lqrf);
     const bool no_w = std::getenv("NMPC_WSET") && std::getenv("NMPC_WSET")[0] == '0';
@@ -994,9 +997,10 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_Ge = carve((size_t)nx * std::max(ny_e, 1));
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
-    // the unconstrained factorisation's tables (lqr_table, lqr_wmat) serve only the exact finish's
-    // shortcuts of the stage-wise kernels: fp64 handles with the finish on (polish_mu > 0)
-    const bool lqr_on = !h->cond && f64 && h->polish_mu > 0;
+    // the unconstrained factorisation's tables (lqr_table, lqr_wmat) serve the exact finish's shortcuts of
+    // the stage-wise kernels (fp64 handles with the finish on: polish_mu > 0) and the lean closed loop
+    // (W and the explicit solution's tables, both precisions; fp32 handles' solves never read them)
+    const bool lqr_on = !h->cond && (!f64 || h->polish_mu > 0);
     h->off_lqr = carve(lqr_on ? (size_t)N * nz * lqr_words(nx, nu) : 0);
     h->off_lqrf = carve(lqr_on ? (size_t)N * nz * lqrf_words(nx, nu) : 0);
     h->off_lqrw = carve(lqr_on ? (size_t)(N + 1) * nz * (N + 1) * nz : 0);
@@ -1510,8 +1514,9 @@ hipError_t put_typed(void *dst, const double *src, size_t n, bool f64)
     return hipMemcpy(dst, t.data(), n * sizeof(float), hipMemcpyHostToDevice);
 }
 
-// The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, a compiled slot
-// layout for (nx, nu) (quad13, jerk, force: on by default; NMPC_CL_FAST=0 off). Its fallback is the
+// The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, or fp32 (the tables
+// and the explicit form in fp32, the set solves and the acceptance in fp64), a compiled slot layout for
+// (nx, nu) (quad13, jerk, force: on by default; NMPC_CL_FAST=0 off). Its fallback is the
 // lane-per-component kernel's list mode: a handle of the wavefront family (small models at small
 // batches) gets that family's kernel and scratch as well.
 // Slots: the bounded elements of z in stage-major order (stage 0's inputs first), their bounds,
@@ -1523,19 +1528,25 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     const char *env = std::getenv("NMPC_CL_FAST");
     const bool want = !env || env[0] != '0';
     const int epl = nmpc::cl_fast_epl(nx, nu);
-    if (!want || h->precision != NMPC_FP64 || !(h->polish_mu > 0) || !h->g_diag || h->cond || epl <= 0)
+    const bool f64 = h->precision == NMPC_FP64;
+    const std::string fenv = std::getenv("NMPC_CL_FAST32") ? std::getenv("NMPC_CL_FAST32") : "1";
+    if (!want || (f64 && !(h->polish_mu > 0)) || (!f64 && fenv == "0") || !h->g_diag || h->cond || epl <= 0)
         return 0;
     int fk = h->kidx;
-    if (nmpc::ipm_kind<double>(h->kidx) != 1) {
-        fk = nmpc::ipm_find_family<double>(nx, nu, 1);
+    const int kind = f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
+    if (kind != 1) {
+        fk = f64 ? nmpc::ipm_find_family<double>(nx, nu, 1) : nmpc::ipm_find_family<float>(nx, nu, 1);
         if (fk < 0) return 0;
         std::vector<double> ABh((size_t)nx * nz);
         for (int r = 0; r < nx; r++) {
             for (int q = 0; q < nx; q++) ABh[r * nz + q] = h->A[r * nx + q];
             for (int q = 0; q < nu; q++) ABh[r * nz + nx + q] = h->B[r * nu + q];
         }
-        fk = nmpc::ipm_refine<double>(fk, ABh.data(), h->H.data(), h->He.data());
+        fk = f64 ? nmpc::ipm_refine<double>(fk, ABh.data(), h->H.data(), h->He.data())
+                 : nmpc::ipm_refine<float>(fk, ABh.data(), h->H.data(), h->He.data());
     }
+    const int fsid = f64 ? nmpc::ipm_structure<double>(fk) : nmpc::ipm_structure<float>(fk);
+    const size_t es = h->esz();
     std::vector<int> el, fr;
     std::vector<double> lb, ub;
     for (int k = 0; k <= N; k++)
@@ -1596,22 +1607,30 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         itot += (ip[i]->size() + 63) & ~(size_t)63;
     }
     for (void **q : {&h->d_fsT, (void **)&h->d_fsI, (void **)&h->d_istep, (void **)&h->d_park, (void **)&h->d_flags,
-                     &h->d_clf_scratch})
+                     &h->d_clf_scratch, (void **)&h->d_clw})
         if (*q) {
             hipFree(*q);
             *q = nullptr;
         }
-    bool ok = hipMalloc(&h->d_fsT, tot * sizeof(double)) == hipSuccess &&
+    bool ok = hipMalloc(&h->d_fsT, tot * es) == hipSuccess &&
               hipMalloc((void **)&h->d_fsI, itot * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_istep, (size_t)h->batch * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_park, (size_t)(h->batch + 2) * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_flags, (size_t)h->batch * nslot) == hipSuccess;
     if (ok && fk != h->kidx)
-        ok = hipMalloc(&h->d_clf_scratch, nmpc::ipm_scratch_elems<double>(fk, h->batch, N) * sizeof(double)) == hipSuccess;
+        ok = hipMalloc(&h->d_clf_scratch, (f64 ? nmpc::ipm_scratch_elems<double>(fk, h->batch, N)
+                                                : nmpc::ipm_scratch_elems<float>(fk, h->batch, N)) * es) == hipSuccess;
+    // fp32 handles: W in fp64 (the set solves' multipliers amplify W's rounding by cond(W_SS), ~4e4 for force)
+    std::vector<double> wm;
+    if (ok && !f64) {
+        lqr_wmat(nx, nu, N, h->A, h->B, h->lqr_host, wm);
+        ok = hipMalloc((void **)&h->d_clw, wm.size() * sizeof(double)) == hipSuccess;
+    }
     if (!ok) return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: lean closed-loop tables");
     hipError_t e = hipSuccess;
+    if (!wm.empty()) e = hipMemcpy(h->d_clw, wm.data(), wm.size() * sizeof(double), hipMemcpyHostToDevice);
     for (int i = 0; i < 5 && e == hipSuccess; i++)
-        e = hipMemcpy((double *)h->d_fsT + h->fso[i], parts[i]->data(), parts[i]->size() * sizeof(double), hipMemcpyHostToDevice);
+        e = put_typed((char *)h->d_fsT + h->fso[i] * es, parts[i]->data(), parts[i]->size(), f64);
     for (int i = 0; i < 4 && e == hipSuccess; i++)
         if (!ip[i]->empty())
             e = hipMemcpy(h->d_fsI + h->fsi[i], ip[i]->data(), ip[i]->size() * sizeof(int), hipMemcpyHostToDevice);
@@ -1621,13 +1640,14 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     // the lockstep kernel for the shapes that have one, with the controller-model plant and the cost on x_0
     // (env NMPC_CLF_LOCK=0: the one-instance-per-wavefront kernel)
     const char *lenv = std::getenv("NMPC_CLF_LOCK");
-    h->clf_lock = nmpc::cl_lock_shape(nx, nu) && d.plant == NMPC_PLANT_MODEL && d.cost_stage == 0 && !(lenv && lenv[0] == '0');
+    h->clf_lock = f64 && nmpc::cl_lock_shape(nx, nu) && d.plant == NMPC_PLANT_MODEL && d.cost_stage == 0 &&
+                  !(lenv && lenv[0] == '0');
     // resident workgroups on this handle's device (nmpc_closed_loop_init runs on it: hipSetDevice above)
-    h->clf_resident = nmpc::cl_fast_resident(nx, nu, nmpc::ipm_structure<double>(fk), h->clf_lock, h->device);
+    h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, h->clf_lock, f64, h->device);
     // the lockstep kernel's per-workgroup queue holds at most 512 demoted instances
     if (h->clf_lock && h->clf_resident > 0 && (h->batch + h->clf_resident - 1) / h->clf_resident > 512) {
         h->clf_lock = false;
-        h->clf_resident = nmpc::cl_fast_resident(nx, nu, nmpc::ipm_structure<double>(fk), false, h->device);
+        h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, false, f64, h->device);
     }
     if (h->clf_resident <= 0) return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_init: lean closed-loop occupancy query");
     h->clf = true;
@@ -1635,14 +1655,15 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     h->clf_nfree = (int)fr.size();
     h->clf_epl = epl;
     h->clf_x1slot = x1slot;
-    h->clf_sid = nmpc::ipm_structure<double>(fk);
+    h->clf_sid = fsid;
     h->clf_kidx = fk;
     return 0;
 }
 
-nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int noise_ld)
+template <typename T>
+nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int noise_ld)
 {
-    nmpc::ClFastParams<double> p{};
+    nmpc::ClFastParams<T> p{};
     const nmpc_closed_loop_desc &d = h->cl;
     const int nx = h->nx, nu = h->nu, nz = nx + nu;
     p.B = h->batch;
@@ -1668,14 +1689,14 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     p.noise_ld = noise_ld;
     p.polish_steps = h->polish_steps;
     p.x1_slot = h->clf_x1slot;
-    p.table = (const double *)h->d_table;
+    p.table = (const T *)h->d_table;
     p.offset = h->d_offsets;
-    p.state = (double *)h->d_state;
+    p.state = (T *)h->d_state;
     p.acc = h->d_acc;
     p.istep = h->d_istep;
     p.flags = h->d_flags;
     p.noise = h->d_fnoise;
-    const double *fT = (const double *)h->d_fsT;
+    const T *fT = (const T *)h->d_fsT;
     p.s_lb = fT + h->fso[0];
     p.s_ub = fT + h->fso[1];
     p.s_tx = fT + h->fso[2];
@@ -1685,17 +1706,17 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     p.s_src = h->d_fsI + h->fsi[1];
     p.s_free = h->d_fsI + h->fsi[3];
     p.nfree = h->clf_nfree;
-    p.vfull = (const double *)h->d_clv;
-    p.txfull = (const double *)h->d_cltx;
+    p.vfull = (const T *)h->d_clv;
+    p.txfull = (const T *)h->d_cltx;
     const char *m = (const char *)h->d_model;
-    p.W = (const double *)(m + h->off_lqrw);
-    p.lbnd = (const double *)(m + h->off_lb);
-    p.ubnd = (const double *)(m + h->off_ub);
-    p.AB = (const double *)(m + h->off_AB);
-    p.c = (const double *)(m + h->off_c);
-    p.wcl = (const double *)h->d_wcl;
-    p.xout = (double *)h->d_x;
-    p.uout = (double *)h->d_u;
+    p.W = h->d_clw ? h->d_clw : (const double *)(m + h->off_lqrw);
+    p.lbnd = (const T *)(m + h->off_lb);
+    p.ubnd = (const T *)(m + h->off_ub);
+    p.AB = (const T *)(m + h->off_AB);
+    p.c = (const T *)(m + h->off_c);
+    p.wcl = (const T *)h->d_wcl;
+    p.xout = (T *)h->d_x;
+    p.uout = (T *)h->d_u;
     p.status = h->d_status;
     p.iters = h->d_iters;
     p.park_count = h->d_park;
@@ -1705,7 +1726,9 @@ nmpc::ClFastParams<double> clf_params(nmpc_solver *h, int target, int step0, int
     const char *nogi = std::getenv("NMPC_CLF_NO_GI");
     p.gi = (nogi && nogi[0] == '1') ? 0 : 1;
     const char *lw = std::getenv("NMPC_LOCK_WORKERS");
-    p.lock_workers = lw ? std::max(0, std::min(4, std::atoi(lw))) : 0;
+    // one wavefront per workgroup starts in phase 2 (drains demoted instances while the others still run
+    // lockstep): quad13 B = 8192 415M (0) -> 458-463M (1), 452-457M (2), 405-412M (3) steps/s (tools/lock_ab.sh, ab1/ab2)
+    p.lock_workers = lw ? std::max(0, std::min(4, std::atoi(lw))) : 1;
     return p;
 }
 
@@ -1727,6 +1750,7 @@ constexpr int CLF_CHUNK = 64;   // closed-loop steps per lean-loop launch (bound
 // parked instance, ipm_lpc_kernel in list mode) until none is parked. Returns the number of kernel
 // launches (each bracketed by an event pair), or < 0. h->clf_parked / clf_rounds: the run's parked
 // solves and fast launches.
+template <typename T>
 int clf_run(nmpc_solver *h, int steps)
 {
     const size_t need = (size_t)h->batch * std::min(steps, CLF_CHUNK);
@@ -1761,10 +1785,10 @@ int clf_run(nmpc_solver *h, int steps)
         (void)hipMemsetAsync(d_cyc, 0, (size_t)h->batch * 20 * sizeof(unsigned long long), h->stream);
     for (int done = 0; done < steps;) {
         const int n = std::min(CLF_CHUNK, steps - done), target = h->cl_step + n;
-        nmpc::ClParams<double> cp = cl_params<double>(h);
-        hipError_t e = nmpc::cl_noise_launch<double>(cp, h->cl_step, n, h->d_fnoise, h->stream);
+        nmpc::ClParams<T> cp = cl_params<T>(h);
+        hipError_t e = nmpc::cl_noise_launch<T>(cp, h->cl_step, n, h->d_fnoise, h->stream);
         if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
-        nmpc::ClFastParams<double> fp = clf_params(h, target, h->cl_step, n);
+        nmpc::ClFastParams<T> fp = clf_params<T>(h, target, h->cl_step, n);
         fp.cycles = d_cyc;
         if (iter_log && h->d_iter_log) {
             const size_t rows = (size_t)(n + 2) * h->batch;
@@ -1776,7 +1800,7 @@ int clf_run(nmpc_solver *h, int steps)
         for (int round = 0; round <= n; round++) {
             if ((e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
             hipEventRecord(cl_event(h, 2 * launches), h->stream);
-            e = nmpc::cl_fast_launch<double>(h->nx, h->nu, h->clf_sid, h->clf_lock, fp, h->batch, h->clf_resident, h->stream);
+            e = nmpc::cl_fast_launch<T>(h->nx, h->nu, h->clf_sid, h->clf_lock, fp, h->batch, h->clf_resident, h->stream);
             hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
             launches++;
             h->clf_rounds++;
@@ -1790,7 +1814,7 @@ int clf_run(nmpc_solver *h, int steps)
             h->clf_parked += parked;
             // the fallback: one full solve + plant step for every parked instance
             const ListArgs la{parked, h->cl_step, n};
-            const int r = launch<double>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
+            const int r = launch<T>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
             launches++;
             if (r < 0) return r;
             if (dbg && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "lean closed loop (list-mode fallback)");
@@ -1958,7 +1982,7 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
     const bool lean = h->clf && !(fused_env && fused_env[0] == '0');
     h->clf_parked = h->clf_rounds = 0;
     if (lean) {
-        launches = steps > 0 ? clf_run(h, steps) : 0;
+        launches = steps <= 0 ? 0 : (h->precision == NMPC_FP64 ? clf_run<double>(h, steps) : clf_run<float>(h, steps));
         if (launches < 0) return launches;
     } else if (cl_fused(h)) {
         if (h->fnoise_cap < (size_t)h->batch * CL_FUSED_CHUNK) {

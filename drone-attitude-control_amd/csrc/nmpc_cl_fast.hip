@@ -34,6 +34,7 @@
 #include <cfloat>
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "nmpc_cl_device.h"
 #include "nmpc_internal.h"
@@ -75,6 +76,22 @@ constexpr int CLF_NT = 20;
     do {                  \
     } while (0)
 #endif
+
+// decision thresholds by storage precision, relative to 1 + |b|: viol — a bound counts as violated beyond
+// it (fast-path acceptance, PDAS additions, the dual fallback's entering bound); onb — the solution's
+// warm-start flags (z within it of a bound). fp32 handles hold z_0 = v_t + T_x x to a few fp32 ulps of the
+// terms' magnitude (|T_x x| ~ 1-10: ~1e-6 absolute), so their thresholds sit above that noise; the held-bound
+// check (1e-9) and the multiplier signs (1e-10) are taken on fp64 quantities in both precisions (W is
+// fp64 for both — an ill-conditioned set's multipliers would amplify its fp32 rounding by cond(W_SS) — the
+// W[:, S] nu combinations accumulate in fp64, the set solves run in fp64), DESIGN.md §6
+template <typename T>
+struct ClfTol {
+    static constexpr double viol = 1e-13, onb = 1e-7;
+};
+template <>
+struct ClfTol<float> {
+    static constexpr double viol = 2e-6, onb = 1e-5;
+};
 
 template <typename T>
 __device__ __forceinline__ bool has_b(T b)
@@ -379,10 +396,11 @@ __device__ int compact_set(LdsT &L, unsigned am, int lane, double coef)
 // acc[j] += sum_i W[e_i][e_j] c_i at every slot j of the lane (padding slots untouched) for the m
 // elements el (LDS) with coefficients cf (LDS): the set in batches of QB, each batch's loads for all the
 // lane's slots in flight together (one memory latency per batch, not one per slot and batch); per slot
-// the sum runs in list order
-template <typename T, int EPL>
+// the sum runs in list order, in the accumulator's precision A (fp64 for both storage precisions: the
+// terms of an ill-conditioned set cancel)
+template <typename T, int EPL, typename A>
 __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const SlotView<EPL> sv, const double *cf, int m,
-                              T (&acc)[EPL])
+                              A (&acc)[EPL])
 {
     constexpr int QB = EPL <= 2 ? 8 : (EPL <= 4 ? 4 : 2);
     const int ne = p.ne;
@@ -390,20 +408,20 @@ __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const Slo
 #pragma unroll
     for (int j = 0; j < EPL; j++) e[j] = sv.e(j);
     for (int i0 = 0; i0 < m; i0 += QB) {
-        T w[QB][EPL];
+        double w[QB][EPL];
 #pragma unroll
         for (int q = 0; q < QB; q++) {
             const int row = i0 + q < m ? el[i0 + q] : 0;
 #pragma unroll
-            for (int j = 0; j < EPL; j++) w[q][j] = (i0 + q < m && e[j] >= 0) ? p.W[(size_t)row * ne + e[j]] : T(0);
+            for (int j = 0; j < EPL; j++) w[q][j] = (i0 + q < m && e[j] >= 0) ? p.W[(size_t)row * ne + e[j]] : 0.0;
         }
 #pragma unroll
         for (int q = 0; q < QB; q++)
             if (i0 + q < m) {
-                const T c = (T)cf[i0 + q];
+                const A c = (A)cf[i0 + q];
 #pragma unroll
                 for (int j = 0; j < EPL; j++)
-                    if (e[j] >= 0) acc[j] = fma(w[q][j], c, acc[j]);
+                    if (e[j] >= 0) acc[j] = fma((A)w[q][j], c, acc[j]);
             }
     }
 }
@@ -430,7 +448,7 @@ __device__ int load_set(LdsT &L, const SlotView<EPL> sv, int lane, unsigned wf, 
             pos[j] = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal[j], 0u));
             L.se_e[pos[j]] = sv.e(j);
             L.se_s[pos[j]] = f == 1u ? -1 : 1;
-            L.se_t[pos[j]] = (double)((f == 1u ? (T)sv.lb(j) : (T)sv.ub(j)) - z0[j]);
+            L.se_t[pos[j]] = (f == 1u ? sv.lb(j) : sv.ub(j)) - (double)z0[j];   // fp64: b_S is met to 1e-9
             L.gi_slot[pos[j]] = j * 64 + lane;
         }
         base += __popcll(bal[j]);
@@ -508,9 +526,10 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
             unsigned sgn = 0;
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
-                const bool lo = z0[j] < (T)sv.lo(j), hi = z0[j] > (T)sv.hi(j);
-                bad |= lo || hi || !isfinite(z0[j]);
-                v[j] = lo ? (double)((T)sv.lb(j) - z0[j]) : (hi ? (double)(z0[j] - (T)sv.ub(j)) : 0.0);
+                const double zj = (double)z0[j];
+                const bool lo = zj < sv.lo(j), hi = zj > sv.hi(j);
+                bad |= lo || hi || !isfinite(zj);
+                v[j] = lo ? sv.lb(j) - zj : (hi ? zj - sv.ub(j) : 0.0);
                 sgn |= (lo ? 1u : (hi ? 2u : 0u)) << (2 * j);
                 if (comp(j) >= NX && (lo || hi)) wf |= (lo ? 1u : 2u) << (2 * j);   // inputs join at once
             }
@@ -563,32 +582,37 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         bool bad = nrem > 0;
         double v[EPL];
         unsigned sgn = 0, nwf = wf;
+        // z = z_0 + W[:, S] nu and its checks in fp64 (T = float: the stored z_0 and W widened)
+        double zd[EPL];
 #pragma unroll
-        for (int j = 0; j < EPL; j++) z[j] = z0[j];
+        for (int j = 0; j < EPL; j++) zd[j] = (double)z0[j];
         CLF_T(tc0);
-        w_combo_slots<T, EPL>(p, L.se_e, sv, L.se_nu, m, z);
+        w_combo_slots<T, EPL>(p, L.se_e, sv, L.se_nu, m, zd);
         CLF_TADD(L, 4, tc0);
         CLF_T(tk0);
 #pragma unroll
         for (int j = 0; j < EPL; j++) {
             v[j] = 0.0;
             const int e = sv.e(j);
-            if (e < 0) continue;
-            T zz = z[j];
+            if (e < 0) {
+                z[j] = z0[j];
+                continue;
+            }
+            double zz = zd[j];
             const unsigned f = (wf >> (2 * j)) & 3u;
             if (f) {
-                const T bb = f == 1u ? (T)sv.lb(j) : (T)sv.ub(j);
-                bad |= !(fabs(zz - bb) <= T(1e-9) * (T(1) + fabs(bb)));
+                const double bb = f == 1u ? sv.lb(j) : sv.ub(j);
+                bad |= !(fabs(zz - bb) <= 1e-9 * (1.0 + fabs(bb)));
                 zz = bb;
                 if ((remm >> pos[j]) & 1ull) nwf &= ~(3u << (2 * j));
             } else {
-                const bool lo = zz < (T)sv.lo(j), hi = zz > (T)sv.hi(j);
+                const bool lo = zz < sv.lo(j), hi = zz > sv.hi(j);
                 bad |= lo || hi || !isfinite(zz);
-                v[j] = lo ? (double)((T)sv.lb(j) - zz) : (hi ? (double)(zz - (T)sv.ub(j)) : 0.0);
+                v[j] = lo ? sv.lb(j) - zz : (hi ? zz - sv.ub(j) : 0.0);
                 sgn |= (lo ? 1u : (hi ? 2u : 0u)) << (2 * j);
                 if (e % NZ >= NX && (lo || hi)) nwf |= (lo ? 1u : 2u) << (2 * j);   // inputs join at once
             }
-            z[j] = zz;
+            z[j] = (T)zz;
         }
         if (!__any(bad)) {
             CLF_TADD(L, 19, tk0);
@@ -623,9 +647,9 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
 {
     constexpr int CPL = HGeom<WSM>::CPL;
     const int ne = p.ne, hi_ = lane % WSM, hg = lane / WSM;
-    T z[EPL];
+    double z[EPL];   // the iterate in fp64 for both storage precisions
 #pragma unroll
-    for (int j = 0; j < EPL; j++) z[j] = z0[j];
+    for (int j = 0; j < EPL; j++) z[j] = (double)z0[j];
     unsigned am = 0;                      // occupied set positions (wave-uniform)
     int ps = -1, sp = 0, ep = 0, ord = 0; // the entering bound: slot, sign (+1 lower, -1 upper), element
     double u = 0.0, up = 0.0;             // lane i < WSM: the multiplier u_i of position i; up: the entering bound's
@@ -678,8 +702,8 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 const bool held = ((wf >> (2 * j)) & 3u) != 0;
-                const bool lo = !held && z[j] < (T)sv.lo(j), hi = !held && z[j] > (T)sv.hi(j);
-                v[j] = lo ? (double)((T)sv.lb(j) - z[j]) : (hi ? (double)(z[j] - (T)sv.ub(j)) : 0.0);
+                const bool lo = !held && z[j] < sv.lo(j), hi = !held && z[j] > sv.hi(j);
+                v[j] = lo ? sv.lb(j) - z[j] : (hi ? z[j] - sv.ub(j) : 0.0);
                 vm = fmax(vm, v[j]);
             }
             vm = wave_max(vm);
@@ -701,7 +725,7 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         double zc = 0.0;
 #pragma unroll
         for (int j = 0; j < EPL; j++)
-            if (j == (ps >> 6)) zc = (double)z[j];
+            if (j == (ps >> 6)) zc = z[j];
         const double zp = bcast(zc, ps & 63);
         if (up == 0.0) sp = zp < sv.lo_[ps] ? 1 : -1;   // entering: the violated side
         const double bp = sp > 0 ? sv.lb_[ps] : sv.ub_[ps];
@@ -722,14 +746,14 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         CLF_T(tg_cmb);
         if (t2 < INFINITY) {
             const int mc = compact_set<WSM>(L, am, lane, r_);
-            T comb[EPL];
+            double comb[EPL];
 #pragma unroll
-            for (int j = 0; j < EPL; j++) comb[j] = T(0);
+            for (int j = 0; j < EPL; j++) comb[j] = 0.0;
             w_combo_slots<T, EPL>(p, L.cl_e, sv, L.cl_c, mc, comb);
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 const int e = sv.e(j);
-                if (e >= 0) z[j] = fma((T)t, (T)sp * (p.W[(size_t)ep * ne + e] - comb[j]), z[j]);
+                if (e >= 0) z[j] = fma(t, (double)sp * ((double)p.W[(size_t)ep * ne + e] - comb[j]), z[j]);
             }
             CLF_SYNC();
         }
@@ -914,24 +938,24 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<
     for (int q = lane; q < p.nfree; q += 64) {
         const int e = p.s_free[q];
         const T *tr = p.txfull + (size_t)e * NX;
-        T s0 = p.vfull[(size_t)t * ne + e], s1 = 0;
+        double s0 = (double)p.vfull[(size_t)t * ne + e], s1 = 0.0;   // fp64 sums (the set's terms cancel)
 #pragma unroll
         for (int c = 0; c + 1 < NX; c += 2) {
-            s0 = fma(tr[c], (T)L.xs[c], s0);
-            s1 = fma(tr[c + 1], (T)L.xs[c + 1], s1);
+            s0 = fma((double)tr[c], L.xs[c], s0);
+            s1 = fma((double)tr[c + 1], L.xs[c + 1], s1);
         }
-        if (NX % 2) s0 = fma(tr[NX - 1], (T)L.xs[NX - 1], s0);
-        T z = s0 + s1;
+        if (NX % 2) s0 = fma((double)tr[NX - 1], L.xs[NX - 1], s0);
+        double z = s0 + s1;
         // W[S, e] nu in batches of 4 (the loads of a batch issued together)
         for (int i0 = 0; i0 < m; i0 += 4) {
-            T wv[4];
+            double wv[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) wv[q] = i0 + q < m ? p.W[(size_t)L.se_e[i0 + q] * ne + e] : T(0);
+            for (int q = 0; q < 4; q++) wv[q] = i0 + q < m ? p.W[(size_t)L.se_e[i0 + q] * ne + e] : 0.0;
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (i0 + q < m) z = fma(wv[q], (T)L.se_nu[i0 + q], z);
+                if (i0 + q < m) z = fma(wv[q], L.se_nu[i0 + q], z);
         }
-        put(e, z);
+        put(e, (T)z);
     }
 }
 
@@ -1180,15 +1204,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // workgroup constants: [A B], c (plant), the slots' bounds, thresholds, elements and warm-start sources
     __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT], slo[NSLOT], shi[NSLOT], sol[NSLOT], sou[NSLOT];
     __shared__ int sse[NSLOT], ssrc[NSLOT];
-    // the slots' T_x rows, pairs of components per 16-byte word (txl[c][s] = (T_x(s, 2c), T_x(s, 2c + 1))):
-    // lanes read consecutive words, one ds_read_b128 per slot and pair
+    // the slots' T_x rows, pairs of components per word (txl[c][s] = (T_x(s, 2c), T_x(s, 2c + 1))):
+    // lanes read consecutive words, one ds_read_b128 (fp32: b64) per slot and pair
     constexpr int NXP = (NX + 1) / 2;
-    __shared__ double2 txl[NXP][NSLOT];
+    using TP = typename std::conditional<std::is_same<T, float>::value, float2, double2>::type;
+    __shared__ TP txl[NXP][NSLOT];
     for (int e = threadIdx.x; e < NXP * NSLOT; e += 64 * WPB) {
         const int c = e / NSLOT, s_ = e % NSLOT;
         const bool v = s_ < p.nslot;
-        txl[c][s_] = make_double2(v ? (double)p.s_tx[(size_t)s_ * NX + 2 * c] : 0.0,
-                                  v && 2 * c + 1 < NX ? (double)p.s_tx[(size_t)s_ * NX + 2 * c + 1] : 0.0);
+        TP w;
+        w.x = v ? p.s_tx[(size_t)s_ * NX + 2 * c] : T(0);
+        w.y = v && 2 * c + 1 < NX ? p.s_tx[(size_t)s_ * NX + 2 * c + 1] : T(0);
+        txl[c][s_] = w;
     }
     for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) {
         const int i = e / NZ, j = e % NZ;
@@ -1201,10 +1228,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         const bool hl = has_b(l), hu = has_b(u);
         slb[s] = l;
         sub[s] = u;
-        slo[s] = hl ? l - 1e-13 * (1.0 + fabs(l)) : -DBL_MAX;
-        shi[s] = hu ? u + 1e-13 * (1.0 + fabs(u)) : DBL_MAX;
-        sol[s] = hl ? l + 1e-7 * (1.0 + fabs(l)) : -DBL_MAX;
-        sou[s] = hu ? u - 1e-7 * (1.0 + fabs(u)) : DBL_MAX;
+        slo[s] = hl ? l - ClfTol<T>::viol * (1.0 + fabs(l)) : -DBL_MAX;
+        shi[s] = hu ? u + ClfTol<T>::viol * (1.0 + fabs(u)) : DBL_MAX;
+        sol[s] = hl ? l + ClfTol<T>::onb * (1.0 + fabs(l)) : -DBL_MAX;
+        sou[s] = hu ? u - ClfTol<T>::onb * (1.0 + fabs(u)) : DBL_MAX;
         sse[s] = v ? p.s_e[s] : -1;
         ssrc[s] = v ? p.s_src[s] : -1;
     }
@@ -1247,11 +1274,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 #pragma unroll
             for (int c = 0; c < NXP; c++) {
                 const double2 xx = *reinterpret_cast<const double2 *>(&L.xs[2 * c]);
+                const T x0 = (T)xx.x, x1 = (T)xx.y;
 #pragma unroll
                 for (int j = 0; j < EPL; j++) {
-                    const double2 tt = txl[c][j * 64 + lane];
-                    z[j] = fma((T)tt.x, (T)xx.x, z[j]);
-                    z1[j] = fma((T)tt.y, (T)xx.y, z1[j]);
+                    const TP tt = txl[c][j * 64 + lane];
+                    z[j] = fma(tt.x, x0, z[j]);
+                    z1[j] = fma(tt.y, x1, z1[j]);
                 }
             }
 #pragma unroll
@@ -1320,10 +1348,10 @@ __global__ __launch_bounds__(64 * WPB) void cl_lock_kernel(ClFastParams<T> p)
         const bool hl = has_b(l), hu = has_b(u);
         slb[s] = l;
         sub[s] = u;
-        slo[s] = hl ? l - 1e-13 * (1.0 + fabs(l)) : -DBL_MAX;
-        shi[s] = hu ? u + 1e-13 * (1.0 + fabs(u)) : DBL_MAX;
-        sol[s] = hl ? l + 1e-7 * (1.0 + fabs(l)) : -DBL_MAX;
-        sou[s] = hu ? u - 1e-7 * (1.0 + fabs(u)) : DBL_MAX;
+        slo[s] = hl ? l - ClfTol<T>::viol * (1.0 + fabs(l)) : -DBL_MAX;
+        shi[s] = hu ? u + ClfTol<T>::viol * (1.0 + fabs(u)) : DBL_MAX;
+        sol[s] = hl ? l + ClfTol<T>::onb * (1.0 + fabs(l)) : -DBL_MAX;
+        sou[s] = hu ? u - ClfTol<T>::onb * (1.0 + fabs(u)) : DBL_MAX;
         lohi[s] = make_double2(slo[s], shi[s]);
         onb[s] = make_double2(sol[s], sou[s]);
         sse[s] = v ? p.s_e[s] : -1;
@@ -1349,8 +1377,8 @@ __global__ __launch_bounds__(64 * WPB) void cl_lock_kernel(ClFastParams<T> p)
     const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
     const int wg_lo = (int)blockIdx.x * per_wg, wg_hi = min(p.B, wg_lo + per_wg);
 
-    // ================= phase 1: lockstep (the workgroup's last wavefront starts as a phase-2 worker when
-    // NMPC_LOCK_WORKERS_FIRST (p.lock_workers) is set: the queued chains start at once)
+    // ================= phase 1: lockstep (the workgroup's last p.lock_workers wavefronts start as phase-2
+    // workers, so the queued chains start at once: env NMPC_LOCK_WORKERS, default 1)
     if (wave < WPB - p.lock_workers) {
         // per-instance state, replicated on the 16 lanes of its slot
         int inst = -1, step = 0, t = 0, last_status = 0, nfail = 0, nst = 0;
@@ -1706,11 +1734,14 @@ template <typename T, class F>
 static bool clf_dispatch(int nx, int nu, int sid, bool lock, F &&f)
 {
     static const int var = std::getenv("NMPC_CLF_VARIANT") ? std::atoi(std::getenv("NMPC_CLF_VARIANT")) : 0;
-    if (lock) {
-        if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::Quad13Structure>{});
-        else if (nx == 13 && nu == 4) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::DenseStructure<13, 4>>{});
-        else return false;
-        return true;
+    if (lock) {   // fp64 only (the f64 MFMA tiles)
+        if constexpr (std::is_same<T, double>::value) {
+            if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::Quad13Structure>{});
+            else if (nx == 13 && nu == 4) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::DenseStructure<13, 4>>{});
+            else return false;
+            return true;
+        }
+        return false;
     }
     if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) {
         if (var == 1) f(Variant<T, 13, 4, 4, 16, 8, 4, lpc::Quad13Structure>{});
@@ -1730,16 +1761,18 @@ static bool clf_dispatch(int nx, int nu, int sid, bool lock, F &&f)
 
 // the workgroups of the shape's kernel that `device` holds at once (the persistent grid), queried for
 // the given device at nmpc_closed_loop_init and kept on the handle (no process-wide cache)
-int cl_fast_resident(int nx, int nu, int sid, bool lock, int device)
+int cl_fast_resident(int nx, int nu, int sid, bool lock, bool f64, int device)
 {
     int res = 0;
-    clf_dispatch<double>(nx, nu, sid, lock, [&](auto v) {
+    auto occ = [&](auto v) {
         using V = decltype(v);
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, V::kernel(), 64 * V::WPB, 0) != hipSuccess || per_cu < 1) return;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) return;
         res = per_cu * cus;
-    });
+    };
+    if (f64) clf_dispatch<double>(nx, nu, sid, lock, occ);
+    else clf_dispatch<float>(nx, nu, sid, lock, occ);
     return res;
 }
 
@@ -1759,5 +1792,6 @@ hipError_t cl_fast_launch(int nx, int nu, int sid, bool lock, const ClFastParams
 }
 
 template hipError_t cl_fast_launch<double>(int, int, int, bool, const ClFastParams<double> &, int, int, hipStream_t);
+template hipError_t cl_fast_launch<float>(int, int, int, bool, const ClFastParams<float> &, int, int, hipStream_t);
 
 }  // namespace nmpc

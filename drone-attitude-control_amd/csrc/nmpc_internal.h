@@ -125,7 +125,7 @@ struct ClFastParams {
     const T *vb;                  // [period][EPL * 64] v_t at the slots
     const T *vfull;               // [period][ne]
     const T *txfull;              // [ne][nx]
-    const T *W;                   // [ne][ne] projected inverse Hessian (lqr_wmat)
+    const double *W;              // [ne][ne] projected inverse Hessian (lqr_wmat), fp64 for both precisions
     const T *lbnd, *ubnd;         // [3][nz]
     const T *AB, *c;              // [nx][nz], [nx]: the controller model (plant 0, certificate)
     const T *wcl;                 // [ncl]
@@ -143,9 +143,9 @@ int cl_fast_wsmax(int nx, int nu);
 // whether the shape has the lockstep kernel cl_lock_kernel (four instances per wavefront, MFMA explicit form
 // and plant; the controller-model plant with the cost on x_0 only)
 bool cl_lock_shape(int nx, int nu);
-// workgroups of the shape's cl_fast_kernel (lock: cl_lock_kernel) that `device` holds at once (the
-// persistent grid), or 0
-int cl_fast_resident(int nx, int nu, int sid, bool lock, int device);
+// workgroups of the shape's cl_fast_kernel (lock: cl_lock_kernel, fp64 only) in the handle's precision
+// that `device` holds at once (the persistent grid), or 0
+int cl_fast_resident(int nx, int nu, int sid, bool lock, bool f64, int device);
 // grid = min(waves / wavefronts per workgroup, resident); waves = instances (lock: instances / 4)
 template <typename T>
 hipError_t cl_fast_launch(int nx, int nu, int sid, bool lock, const ClFastParams<T> &p, int waves, int resident,

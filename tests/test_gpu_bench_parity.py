@@ -83,6 +83,43 @@ def test_bench_closed_loop_matches_oracle(golden, model, N, B):
     np.testing.assert_allclose(A[-1, :, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
 
 
+TOL_CL32 = 1e-5   # fp32 lean loop, DESIGN.md §6 (measured 1.4e-6, f32b)
+
+
+@pytest.mark.timeout(300)
+def test_fp32_force_closed_loop_matches_oracle(golden):
+    """BASELINE config 3 (force N=20, B=8192, fp32) on the lean loop bench.py times: fp32 tables and
+    explicit form, fp64 set solves and acceptance (nmpc_cl_fast.hip ClfTol). Against the exact oracle
+    loop (mode 0, closed_loop_bench.npz, fp64) on the bench's own seed-42 workload and launch
+    boundaries: states at every region boundary within TOL_CL32 relative (the fp32 data's rounding
+    carried through the loop), cost / AED numerator within TOL_CL32, failed solves and step counts
+    exactly."""
+    from drone_attitude_control_amd.batched import ClosedLoop
+    key = "force_N20_B8192"
+    sel = golden[f"{key}_sel"]
+    loop = ClosedLoop("force", 8192, N=20, seed=42, precision="fp32")
+    info = loop.solver.launch_info()
+    assert info["closed_loop_kernel"] == "cl_fast_kernel", info
+    states, sums, parked = [], [], 0
+    for n in REGIONS:
+        loop.run(n)
+        parked += loop.stats()["parked"]
+        states.append(loop.state())
+        sums.append(loop.instance_stats())
+    S, A = np.array(states), np.array(sums)
+    Sg, Ag, Fg = golden[f"{key}_states"], golden[f"{key}_sums"], golden[f"{key}_failed"]
+    err = _rel(S[:, sel], Sg)
+    print(f"fp32 force closed loop: max state err {err.max():.3e}, median {np.median(err):.3e}, parked {parked}; "
+          f"per region {np.array2string(err.max(1), precision=2)}")
+    assert err.max() < TOL_CL32, (err.max(), sel[np.unravel_index(err.argmax(), err.shape)[1]])
+    fails_region = np.diff(np.concatenate([np.zeros((1, len(sel))), A[:, sel, 2]]), axis=0)
+    fails_gold = np.add.reduceat(Fg, np.concatenate([[0], np.cumsum(REGIONS)[:-1]]), axis=1).T
+    assert np.array_equal(fails_region, fails_gold)
+    assert np.array_equal(A[:, sel, 3], Ag[:, :, 3])
+    for j in (0, 1):
+        np.testing.assert_allclose(A[:, sel, j], Ag[:, :, j], rtol=TOL_CL32, atol=1e-9)
+
+
 @pytest.mark.timeout(300)
 def test_force_fused_loop_families_agree():
     """The force model's three closed-loop paths — the lean loop (nmpc_cl_fast.hip, the default, with
