@@ -223,6 +223,14 @@ struct nmpc_solver {
     void *d_clf_scratch = nullptr;         // its scratch when the handle's own family is another
     void *d_fsT = nullptr;                 // typed: s_lb, s_ub, s_tx, vb, uinit
     double *d_clw = nullptr;               // fp32 handles: the lean loop's W in fp64 (fp64 handles: the model's)
+    // fp32 handles: the solve's exact finish (fin32_z0_kernel + fin32_kernel, nmpc_cl_fast.hip)
+    bool fin32 = false;
+    int fin_m16 = 0, fin_kp = 0, fin_nslot = 0, fin_nfree = 0, fin_resident = 0;
+    float *d_fin_f = nullptr;              // s_lb, s_ub, uinit, M [m16][kp], vc [m16]
+    size_t fino[5] = {0, 0, 0, 0, 0};
+    int *d_fin_i = nullptr;                // s_e, s_free
+    size_t fini[2] = {0, 0};
+    float *d_z0 = nullptr;                 // [B][m16] unconstrained solutions of the batch
     size_t fso[5] = {0, 0, 0, 0, 0};
     int *d_fsI = nullptr;                  // s_e, s_src, eslot
     size_t fsi[4] = {0, 0, 0, 0};
@@ -230,7 +238,7 @@ struct nmpc_solver {
     int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
     int clf_resident = 0;                  // workgroups of cl_fast_kernel the handle's device holds at once
-    bool clf_lock = false;                 // the lockstep kernel (cl_lock_kernel) runs the lean loop
+    int clf_kind = 0;                      // nmpc::CLF_FAST / CLF_LOCK (cl_lock_kernel) / CLF_WLDS (W in LDS)
     int clf_parked = 0, clf_rounds = 0;    // the last run: parked solves (list-mode full solves), fast launches
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
     std::vector<float> tmp_x0f, tmp_yf;
@@ -498,7 +506,8 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_iters, h->d_table, h->d_state, h->d_plant, h->d_wcl, (void *)h->d_offsets,
                     (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
-                    (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw})
+                    (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw,
+                    (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -570,6 +579,9 @@ template <typename T>
 nmpc::ClParams<T> cl_params(nmpc_solver *h);
 
 constexpr int CL_FUSED_CHUNK = 64;   // closed-loop steps per fused solve launch
+
+int fin32_setup(nmpc_solver *h);
+hipError_t fin32_enqueue(nmpc_solver *h);
 
 // list mode of the lane-per-component kernel (the lean closed loop's fallback)
 struct ListArgs {
@@ -676,6 +688,8 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
     }
     hipEventRecord(e0 ? e0 : h->ev0, h->stream);
     hipError_t e = nmpc::ipm_launch<T>(kidx, p, h->stream);
+    // fp32 solves: the exact finish (inside the timed pair: it is part of the solve)
+    if (e == hipSuccess && cl_steps == 0 && !la && h->fin32) e = fin32_enqueue(h);
     hipEventRecord(e1 ? e1 : h->ev1, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "ipm kernel launch");
     if (sweep_cycles && h->d_cycles) {
@@ -1124,6 +1138,15 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         delete h;
         return r;
     }
+    if (!f64) {
+        const int r = fin32_setup(h);
+        if (r < 0) {
+            g_err = h->err;
+            free_all(h);
+            delete h;
+            return r;
+        }
+    }
     *out = h;
     return 0;
 }
@@ -1386,7 +1409,7 @@ int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
     const bool f64 = h->precision == NMPC_FP64;
     const int kind = h->cond ? 2 : f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
     const int sid = h->cond ? 0 : f64 ? nmpc::ipm_structure<double>(h->kidx) : nmpc::ipm_structure<float>(h->kidx);
-    const int v[8] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid, h->clf ? (h->clf_lock ? 2 : 1) : 0,
+    const int v[8] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid, h->clf ? (h->clf_kind == nmpc::CLF_LOCK ? 2 : 1) : 0,
                       h->clf ? nmpc::cl_fast_wsmax(h->nx, h->nu) : 0};
     for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
     return 0;
@@ -1514,6 +1537,164 @@ hipError_t put_typed(void *dst, const double *src, size_t n, bool f64)
     return hipMemcpy(dst, t.data(), n * sizeof(float), hipMemcpyHostToDevice);
 }
 
+// The lean loop's slot layout: the bounded elements of z in stage-major order (stage 0's inputs first; x_0
+// and stage N's inputs are not elements of the QP's decision), their bounds, and the unbounded decision
+// elements. false: a stage-0 input without both bounds (the failure output needs mid-box inputs).
+bool slot_layout(const nmpc_solver *h, std::vector<int> &el, std::vector<int> &fr, std::vector<double> &lb,
+                 std::vector<double> &ub, std::vector<double> &uinit)
+{
+    const int nx = h->nx, nu = h->nu, nz = nx + nu, N = h->N;
+    el.clear();
+    fr.clear();
+    lb.clear();
+    ub.clear();
+    for (int k = 0; k <= N; k++)
+        for (int r = 0; r < nz; r++) {
+            if ((k == 0 && r < nx) || (k == N && r >= nx)) continue;
+            const int ty = k == 0 ? 0 : (k == N ? 2 : 1);
+            const double l = h->lbnd[ty * nz + r], u_ = h->ubnd[ty * nz + r];
+            if (!has_bound(l) && !has_bound(u_)) {
+                fr.push_back(k * nz + r);
+                continue;
+            }
+            el.push_back(k * nz + r);
+            lb.push_back(l);
+            ub.push_back(u_);
+        }
+    uinit.assign(nu, 0.0);
+    for (int i = 0; i < nu; i++) {
+        if ((int)el.size() <= i || el[i] != nx + i) return false;
+        const double l = h->lbnd[nx + i], u_ = h->ubnd[nx + i];
+        if (!has_bound(l) || !has_bound(u_)) return false;
+        uinit[i] = 0.5 * (l + u_);
+    }
+    return true;
+}
+
+// fp32 handles: the lean machinery's W in fp64 (an ill-conditioned set's multipliers amplify W's rounding
+// by cond(W_SS), ~4e4 for force), shared by the solve finish and the lean closed loop
+int ensure_w64(nmpc_solver *h)
+{
+    if (h->d_clw) return 0;
+    std::vector<double> wm;
+    lqr_wmat(h->nx, h->nu, h->N, h->A, h->B, h->lqr_host, wm);
+    if (hipMalloc((void **)&h->d_clw, wm.size() * sizeof(double)) != hipSuccess)
+        return h->fail(NMPC_ENOMEM, "fp64 W table");
+    const hipError_t e = hipMemcpy(h->d_clw, wm.data(), wm.size() * sizeof(double), hipMemcpyHostToDevice);
+    return e == hipSuccess ? 0 : hip_fail(h, e, "fp64 W table upload");
+}
+
+// The exact finish of fp32 solves (nmpc_cl_fast.hip fin32_*): for the lean loop's shapes with diagonal
+// costs (env NMPC_FIN32=0: off). M = [T_x | V_y] and vc, the unconstrained solution's response to x0, to
+// each reference component (stage-stacked as h_yref) and to c, by unconstrained Riccati solves on the host.
+int fin32_setup(nmpc_solver *h)
+{
+    const char *env = std::getenv("NMPC_FIN32");
+    const int nx = h->nx, nu = h->nu, nz = nx + nu, N = h->N, ne = (N + 1) * nz;
+    if ((env && env[0] == '0') || h->cond || !h->g_diag || h->lqr_host.empty()) return 0;
+    std::vector<int> el, fr;
+    std::vector<double> lb, ub, uinit;
+    if (!slot_layout(h, el, fr, lb, ub, uinit) || nmpc::fin32_resident(nx, nu, (int)el.size(), h->device) <= 0) return 0;
+    const int ny = h->ny, nye = h->ny_e, ys = (int)h->ystride(), K = nx + ys;
+    const int m16 = (ne + 15) / 16 * 16, kp = (K + 3) / 4 * 4;
+    std::vector<double> M((size_t)m16 * kp, 0.0), vc(m16, 0.0), g(ne, 0.0), z(ne), e0(nx, 0.0);
+    for (int j = 0; j < nx; j++) {   // T_x
+        std::fill(e0.begin(), e0.end(), 0.0);
+        e0[j] = 1.0;
+        lqr_solve(nx, nu, N, h->A, h->B, h->c, h->lqr_host, g.data(), e0.data(), false, z.data());
+        for (int e = 0; e < ne; e++) M[(size_t)e * kp + j] = z[e];
+    }
+    std::fill(e0.begin(), e0.end(), 0.0);
+    for (int q = 0; q < ys; q++) {   // V_y: reference component q of the stage-stacked yref
+        const int k = q < N * ny ? q / ny : N, c_ = q < N * ny ? q % ny : q - N * ny;
+        const int n = k < N ? nz : nx, m = k < N ? ny : nye;
+        const double *Gm = k < N ? h->G.data() : h->Ge.data();
+        std::fill(g.begin(), g.end(), 0.0);
+        for (int i = 0; i < n; i++) g[(size_t)k * nz + i] = Gm[i * m + c_];
+        lqr_solve(nx, nu, N, h->A, h->B, h->c, h->lqr_host, g.data(), e0.data(), false, z.data());
+        for (int e = 0; e < ne; e++) M[(size_t)e * kp + nx + q] = z[e];
+    }
+    std::fill(g.begin(), g.end(), 0.0);   // vc: the response to c
+    lqr_solve(nx, nu, N, h->A, h->B, h->c, h->lqr_host, g.data(), e0.data(), true, z.data());
+    for (int e = 0; e < ne; e++) vc[e] = z[e];
+    const std::vector<double> *parts[5] = {&lb, &ub, &uinit, &M, &vc};
+    size_t tot = 0;
+    for (int i = 0; i < 5; i++) {
+        h->fino[i] = tot;
+        tot += (parts[i]->size() + 31) & ~(size_t)31;
+    }
+    const std::vector<int> *ip[2] = {&el, &fr};
+    size_t itot = 0;
+    for (int i = 0; i < 2; i++) {
+        h->fini[i] = itot;
+        itot += (ip[i]->size() + 63) & ~(size_t)63;
+    }
+    if (hipMalloc((void **)&h->d_fin_f, tot * sizeof(float)) != hipSuccess ||
+        hipMalloc((void **)&h->d_fin_i, itot * sizeof(int)) != hipSuccess ||
+        hipMalloc((void **)&h->d_z0, (size_t)h->batch * m16 * sizeof(float)) != hipSuccess)
+        return h->fail(NMPC_ENOMEM, "nmpc_create: fp32 finish tables");
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 5 && e == hipSuccess; i++) e = put_typed(h->d_fin_f + h->fino[i], parts[i]->data(), parts[i]->size(), false);
+    for (int i = 0; i < 2 && e == hipSuccess; i++)
+        if (!ip[i]->empty()) e = hipMemcpy(h->d_fin_i + h->fini[i], ip[i]->data(), ip[i]->size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_create: fp32 finish upload");
+    const int r = ensure_w64(h);
+    if (r < 0) return r;
+    h->fin_resident = nmpc::fin32_resident(nx, nu, (int)el.size(), h->device);
+    if (h->fin_resident <= 0) return 0;
+    h->fin_m16 = m16;
+    h->fin_kp = kp;
+    h->fin_nslot = (int)el.size();
+    h->fin_nfree = (int)fr.size();
+    h->fin32 = true;
+    return 0;
+}
+
+hipError_t fin32_enqueue(nmpc_solver *h)
+{
+    nmpc::Fin32Z0Params zp{};
+    zp.B = h->batch;
+    zp.nx = h->nx;
+    zp.ystride = (int)h->ystride();
+    zp.kp = h->fin_kp;
+    zp.m16 = h->fin_m16;
+    zp.M = h->d_fin_f + h->fino[3];
+    zp.vc = h->d_fin_f + h->fino[4];
+    zp.x0 = (const float *)h->d_x0;
+    zp.yref = (const float *)h->d_yref;
+    zp.z0 = h->d_z0;
+    hipError_t e = nmpc::fin32_z0_launch(zp, h->stream);
+    if (e != hipSuccess) return e;
+    nmpc::ClFastParams<float> p{};
+    const char *m = (const char *)h->d_model;
+    p.B = h->batch;
+    p.N = h->N;
+    p.ne = (h->N + 1) * (h->nx + h->nu);
+    p.nslot = h->fin_nslot;
+    p.polish_steps = h->polish_steps;
+    p.gi = 1;
+    p.s_lb = h->d_fin_f + h->fino[0];
+    p.s_ub = h->d_fin_f + h->fino[1];
+    p.uinit = h->d_fin_f + h->fino[2];
+    p.s_e = h->d_fin_i + h->fini[0];
+    p.s_free = h->d_fin_i + h->fini[1];
+    p.nfree = h->fin_nfree;
+    p.W = h->d_clw;
+    p.lbnd = (const float *)(m + h->off_lb);
+    p.ubnd = (const float *)(m + h->off_ub);
+    p.AB = (const float *)(m + h->off_AB);
+    p.c = (const float *)(m + h->off_c);
+    p.xout = (float *)h->d_x;
+    p.uout = (float *)h->d_u;
+    p.status = h->d_status;
+    p.iters = h->d_iters;
+    p.z0all = h->d_z0;
+    p.z0_ld = h->fin_m16;
+    p.x0in = (const float *)h->d_x0;
+    if (!nmpc::fin32_launch(h->nx, h->nu, 0, p, h->fin_resident, h->stream)) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 // The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, or fp32 (the tables
 // and the explicit form in fp32, the set solves and the acceptance in fp64), a compiled slot layout for
 // (nx, nu) (quad13, jerk, force: on by default; NMPC_CL_FAST=0 off). Its fallback is the
@@ -1548,30 +1729,11 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     const int fsid = f64 ? nmpc::ipm_structure<double>(fk) : nmpc::ipm_structure<float>(fk);
     const size_t es = h->esz();
     std::vector<int> el, fr;
-    std::vector<double> lb, ub;
-    for (int k = 0; k <= N; k++)
-        for (int r = 0; r < nz; r++) {
-            if ((k == 0 && r < nx) || (k == N && r >= nx)) continue;
-            const int ty = k == 0 ? 0 : (k == N ? 2 : 1);
-            const double l = h->lbnd[ty * nz + r], u_ = h->ubnd[ty * nz + r];
-            if (!has_bound(l) && !has_bound(u_)) {
-                fr.push_back(k * nz + r);
-                continue;
-            }
-            el.push_back(k * nz + r);
-            lb.push_back(l);
-            ub.push_back(u_);
-        }
+    std::vector<double> lb, ub, uinit;
+    // stage 0's inputs are slots 0..nu-1 (u0 broadcast), every input box two-sided (failure output)
+    if (!slot_layout(h, el, fr, lb, ub, uinit)) return 0;
     const int nslot = (int)el.size(), NS = epl * 64;
     if (nslot > NS) return 0;
-    // stage 0's inputs are slots 0..nu-1 (u0 broadcast), every input box two-sided (failure output)
-    std::vector<double> uinit(nu);
-    for (int i = 0; i < nu; i++) {
-        if (nslot <= i || el[i] != nx + i) return 0;
-        const double l = h->lbnd[nx + i], u_ = h->ubnd[nx + i];
-        if (!has_bound(l) || !has_bound(u_)) return 0;
-        uinit[i] = 0.5 * (l + u_);
-    }
     std::vector<int> eslot(ne, -1);
     for (int s = 0; s < nslot; s++) eslot[el[s]] = s;
     int x1slot = 0;
@@ -1607,7 +1769,7 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         itot += (ip[i]->size() + 63) & ~(size_t)63;
     }
     for (void **q : {&h->d_fsT, (void **)&h->d_fsI, (void **)&h->d_istep, (void **)&h->d_park, (void **)&h->d_flags,
-                     &h->d_clf_scratch, (void **)&h->d_clw})
+                     &h->d_clf_scratch})
         if (*q) {
             hipFree(*q);
             *q = nullptr;
@@ -1620,15 +1782,12 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     if (ok && fk != h->kidx)
         ok = hipMalloc(&h->d_clf_scratch, (f64 ? nmpc::ipm_scratch_elems<double>(fk, h->batch, N)
                                                 : nmpc::ipm_scratch_elems<float>(fk, h->batch, N)) * es) == hipSuccess;
-    // fp32 handles: W in fp64 (the set solves' multipliers amplify W's rounding by cond(W_SS), ~4e4 for force)
-    std::vector<double> wm;
-    if (ok && !f64) {
-        lqr_wmat(nx, nu, N, h->A, h->B, h->lqr_host, wm);
-        ok = hipMalloc((void **)&h->d_clw, wm.size() * sizeof(double)) == hipSuccess;
-    }
     if (!ok) return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: lean closed-loop tables");
+    if (!f64) {
+        const int r = ensure_w64(h);
+        if (r < 0) return r;
+    }
     hipError_t e = hipSuccess;
-    if (!wm.empty()) e = hipMemcpy(h->d_clw, wm.data(), wm.size() * sizeof(double), hipMemcpyHostToDevice);
     for (int i = 0; i < 5 && e == hipSuccess; i++)
         e = put_typed((char *)h->d_fsT + h->fso[i] * es, parts[i]->data(), parts[i]->size(), f64);
     for (int i = 0; i < 4 && e == hipSuccess; i++)
@@ -1640,14 +1799,20 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     // the lockstep kernel for the shapes that have one, with the controller-model plant and the cost on x_0
     // (env NMPC_CLF_LOCK=0: the one-instance-per-wavefront kernel)
     const char *lenv = std::getenv("NMPC_CLF_LOCK");
-    h->clf_lock = f64 && nmpc::cl_lock_shape(nx, nu) && d.plant == NMPC_PLANT_MODEL && d.cost_stage == 0 &&
-                  !(lenv && lenv[0] == '0');
+    const bool lock = f64 && nmpc::cl_lock_shape(nx, nu) && d.plant == NMPC_PLANT_MODEL && d.cost_stage == 0 &&
+                      !(lenv && lenv[0] == '0');
+    // W over the slots in LDS for the shapes that have the variant, env NMPC_CLF_WLDS=1 (tuning; off by default:
+    // force B = 1024 17.9M vs 19.0M, B = 8192 57.0M vs 80.5M steps/s — one workgroup per CU, and the rare
+    // path's steps are bound by their instruction chains, not by W's L2 latency; tools/ab_check.sh, wl1)
+    const char *wenv = std::getenv("NMPC_CLF_WLDS");
+    const bool wlds = nmpc::cl_wlds_shape(nx, nu) && wenv && wenv[0] == '1';
+    h->clf_kind = lock ? nmpc::CLF_LOCK : (wlds ? nmpc::CLF_WLDS : nmpc::CLF_FAST);
     // resident workgroups on this handle's device (nmpc_closed_loop_init runs on it: hipSetDevice above)
-    h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, h->clf_lock, f64, h->device);
+    h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, h->clf_kind, f64, h->device);
     // the lockstep kernel's per-workgroup queue holds at most 512 demoted instances
-    if (h->clf_lock && h->clf_resident > 0 && (h->batch + h->clf_resident - 1) / h->clf_resident > 512) {
-        h->clf_lock = false;
-        h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, false, f64, h->device);
+    if (lock && h->clf_resident > 0 && (h->batch + h->clf_resident - 1) / h->clf_resident > 512) {
+        h->clf_kind = nmpc::CLF_FAST;
+        h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, h->clf_kind, f64, h->device);
     }
     if (h->clf_resident <= 0) return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_init: lean closed-loop occupancy query");
     h->clf = true;
@@ -1800,7 +1965,7 @@ int clf_run(nmpc_solver *h, int steps)
         for (int round = 0; round <= n; round++) {
             if ((e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
             hipEventRecord(cl_event(h, 2 * launches), h->stream);
-            e = nmpc::cl_fast_launch<T>(h->nx, h->nu, h->clf_sid, h->clf_lock, fp, h->batch, h->clf_resident, h->stream);
+            e = nmpc::cl_fast_launch<T>(h->nx, h->nu, h->clf_sid, h->clf_kind, fp, h->batch, h->clf_resident, h->stream);
             hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
             launches++;
             h->clf_rounds++;

@@ -154,7 +154,7 @@ struct Lds {
     alignas(16) double vb1[WSM], vb2[WSM];
     double se_t[WSM], se_nu[WSM], wdg[WSM];
     int se_e[WSM], se_s[WSM], gi_slot[WSM], se_ord[WSM];
-    int cl_e[WSM];               // compacted element list of the active positions (w_combo_slots)
+    int cl_e[WSM], cl_s[WSM];    // compacted element / slot list of the active positions (w_combo_slots)
     double cl_c[WSM];            // ... and their coefficients
     unsigned long long vmax[NZ];
     int vslot[NZ];
@@ -173,6 +173,20 @@ struct SlotView {
     const double *lb_, *ub_, *lo_, *hi_, *onl_, *onu_;
     const int *e_, *src_;
     int lane;
+    // wl_: W over the slots in the workgroup's LDS (lower triangle, row s: wt_[s (s + 1) / 2 + s'], s' <= s);
+    // else W from the global table by element. W is symmetric. (A flag, not a null test: the compiler cannot
+    // null-test a generic pointer into LDS.)
+    const double *wt_ = nullptr;
+    bool wl_ = false;
+    template <typename T>
+    __device__ double w(const ClFastParams<T> &p, int ea, int sa, int eb, int sb) const
+    {
+        if (wl_) {
+            const int hi = sa > sb ? sa : sb, lo = sa > sb ? sb : sa;
+            return wt_[((hi * (hi + 1)) >> 1) + lo];
+        }
+        return p.W[(size_t)ea * p.ne + eb];
+    }
     __device__ double lb(int j) const { return lb_[j * 64 + lane]; }
     __device__ double ub(int j) const { return ub_[j * 64 + lane]; }
     __device__ double lo(int j) const { return lo_[j * 64 + lane]; }
@@ -227,14 +241,13 @@ __device__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, 
 // readlane, every other row eliminates column c, so at the end nu_i = t_i / (row i's pivot). Pivots get
 // fast_finish's regularisation (below 1e-9 of W_ii: + 1e-6 W_ii), i.e. the same regularised system the
 // oracle's Cholesky solves. The diagonal W_ii goes to L.wdg (the multiplier test). pd: every W_ii > 0.
-template <typename T, int WSM, class LdsT>
-__device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, int m, int lane, double t, bool &pd)
+template <typename T, int WSM, int EPL, class LdsT>
+__device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> &sv, int m, int lane, double t, bool &pd)
 {
-    const int ne = p.ne;
     double row[WSM];
-    const int ei = lane < m ? L.se_e[lane] : 0;
+    const int ei = lane < m ? L.se_e[lane] : 0, si = lane < m ? L.gi_slot[lane] : 0;
 #pragma unroll
-    for (int j = 0; j < WSM; j++) row[j] = (j < m && lane < m) ? (double)p.W[(size_t)L.se_e[j] * ne + ei] : 0.0;
+    for (int j = 0; j < WSM; j++) row[j] = (j < m && lane < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
     double wii = 1.0;
 #pragma unroll
     for (int j = 0; j < WSM; j++)
@@ -247,7 +260,7 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, int m, int lan
         const double d0 = bcast(row[c], c), wcc = bcast(wii, c), tc = bcast(t, c);
         pd = pd && wcc > 0.0;
         const double d = d0 > 1e-9 * wcc ? d0 : fmax(d0, 0.0) + 1e-6 * wcc;
-        const double f = lane != c ? row[c] / d : 0.0;
+        const double f = lane != c ? row[c] * rcp_nr(d) : 0.0;
 #pragma unroll
         for (int j = c + 1; j < WSM; j++) {
             if (j >= m) break;
@@ -272,17 +285,17 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, int m, int lan
 // fast_finish's regularisation: below 1e-9 W_kk it becomes max(d, 0) + 1e-6 W_kk, so the result is the
 // inverse of the same regularised system the Cholesky / Gauss-Jordan paths solve. H = W_SS^-1 goes to
 // L.hm (zero outside the m x m block), W_ii to L.wdg. false: a non-positive W_ii.
-template <typename T, int WSM, class LdsT>
-__device__ bool sweep_inverse(const ClFastParams<T> &p, LdsT &L, int m, int lane)
+template <typename T, int WSM, int EPL, class LdsT>
+__device__ bool sweep_inverse(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> &sv, int m, int lane)
 {
     constexpr int CPL = HGeom<WSM>::CPL;
-    const int i = lane % WSM, g = lane / WSM, ne = p.ne;
+    const int i = lane % WSM, g = lane / WSM;
     double a[CPL];
-    const int ei = i < m ? L.se_e[i] : 0;
+    const int ei = i < m ? L.se_e[i] : 0, si = i < m ? L.gi_slot[i] : 0;
 #pragma unroll
     for (int q = 0; q < CPL; q++) {
         const int j = g * CPL + q;
-        a[q] = (i < m && j < m) ? (double)p.W[(size_t)L.se_e[j] * ne + ei] : 0.0;
+        a[q] = (i < m && j < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < CPL; q++)
@@ -387,6 +400,7 @@ __device__ int compact_set(LdsT &L, unsigned am, int lane, double coef)
     if (act) {
         const int to = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
         L.cl_e[to] = L.se_e[lane];
+        L.cl_s[to] = L.gi_slot[lane];
         L.cl_c[to] = coef;
     }
     CLF_SYNC();
@@ -399,11 +413,10 @@ __device__ int compact_set(LdsT &L, unsigned am, int lane, double coef)
 // the sum runs in list order, in the accumulator's precision A (fp64 for both storage precisions: the
 // terms of an ill-conditioned set cancel)
 template <typename T, int EPL, typename A>
-__device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const SlotView<EPL> sv, const double *cf, int m,
-                              A (&acc)[EPL])
+__device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const int *sl, const SlotView<EPL> sv,
+                              const double *cf, int m, A (&acc)[EPL])
 {
     constexpr int QB = EPL <= 2 ? 8 : (EPL <= 4 ? 4 : 2);
-    const int ne = p.ne;
     int e[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; j++) e[j] = sv.e(j);
@@ -411,9 +424,9 @@ __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const Slo
         double w[QB][EPL];
 #pragma unroll
         for (int q = 0; q < QB; q++) {
-            const int row = i0 + q < m ? el[i0 + q] : 0;
+            const int row = i0 + q < m ? el[i0 + q] : 0, rs = i0 + q < m ? sl[i0 + q] : 0;
 #pragma unroll
-            for (int j = 0; j < EPL; j++) w[q][j] = (i0 + q < m && e[j] >= 0) ? p.W[(size_t)row * ne + e[j]] : 0.0;
+            for (int j = 0; j < EPL; j++) w[q][j] = (i0 + q < m && e[j] >= 0) ? sv.w(p, row, rs, e[j], j * 64 + sv.lane) : 0.0;
         }
 #pragma unroll
         for (int q = 0; q < QB; q++)
@@ -553,10 +566,10 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         double y;
         CLF_T(ts0);
         if (WSM <= 16 || m <= 16) {
-            y = solve_set_gj<T, (WSM < 16 ? WSM : 16)>(p, L, m, lane, lane < m ? L.se_t[lane] : 0.0, pd);
+            y = solve_set_gj<T, (WSM < 16 ? WSM : 16)>(p, L, sv, m, lane, lane < m ? L.se_t[lane] : 0.0, pd);
         } else {
             // sets of 17..WSM: the sweep's explicit inverse, nu = H (b - z_0)_S
-            pd = sweep_inverse<T, WSM>(p, L, m, lane);
+            pd = sweep_inverse<T, WSM>(p, L, sv, m, lane);
             if (lane < WSM) L.vb2[lane] = lane < m ? L.se_t[lane] : 0.0;
             CLF_SYNC();
             y = h_matvec<WSM>(L, L.vb2, lane);
@@ -587,7 +600,7 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
 #pragma unroll
         for (int j = 0; j < EPL; j++) zd[j] = (double)z0[j];
         CLF_T(tc0);
-        w_combo_slots<T, EPL>(p, L.se_e, sv, L.se_nu, m, zd);
+        w_combo_slots<T, EPL>(p, L.se_e, L.gi_slot, sv, L.se_nu, m, zd);
         CLF_TADD(L, 4, tc0);
         CLF_T(tk0);
 #pragma unroll
@@ -663,7 +676,7 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         wf = m <= WSM ? w0 : 0u;
         if (m > WSM) m = 0;
         if (m > 0) {
-            sweep_inverse<T, WSM>(p, L, m, lane);
+            sweep_inverse<T, WSM>(p, L, sv, m, lane);
             am = m == 32 ? 0xffffffffu : ((1u << m) - 1u);
         } else {
 #pragma unroll
@@ -689,7 +702,7 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         }
         if (am) {
             const int mc = compact_set<WSM>(L, am, lane, nu);
-            w_combo_slots<T, EPL>(p, L.cl_e, sv, L.cl_c, mc, z);
+            w_combo_slots<T, EPL>(p, L.cl_e, L.cl_s, sv, L.cl_c, mc, z);
             CLF_SYNC();
         }
     }
@@ -720,8 +733,8 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         CLF_T(tg_sol);
         // a = W[S, p] (occupied positions) and W_pp, loads issued together
         const bool occ = pl && ((am >> lane) & 1u);
-        const double ai = occ ? (double)p.W[(size_t)L.se_e[lane] * ne + ep] : 0.0;
-        const double wpp = (double)p.W[(size_t)ep * ne + ep];
+        const double ai = occ ? sv.w(p, L.se_e[lane], L.gi_slot[lane], ep, ps) : 0.0;
+        const double wpp = sv.w(p, ep, ps, ep, ps);
         double zc = 0.0;
 #pragma unroll
         for (int j = 0; j < EPL; j++)
@@ -749,11 +762,11 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
             double comb[EPL];
 #pragma unroll
             for (int j = 0; j < EPL; j++) comb[j] = 0.0;
-            w_combo_slots<T, EPL>(p, L.cl_e, sv, L.cl_c, mc, comb);
+            w_combo_slots<T, EPL>(p, L.cl_e, L.cl_s, sv, L.cl_c, mc, comb);
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 const int e = sv.e(j);
-                if (e >= 0) z[j] = fma(t, (double)sp * ((double)p.W[(size_t)ep * ne + e] - comb[j]), z[j]);
+                if (e >= 0) z[j] = fma(t, (double)sp * (sv.w(p, ep, ps, e, j * 64 + lane) - comb[j]), z[j]);
             }
             CLF_SYNC();
         }
@@ -937,15 +950,20 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<
 #pragma unroll 1
     for (int q = lane; q < p.nfree; q += 64) {
         const int e = p.s_free[q];
-        const T *tr = p.txfull + (size_t)e * NX;
-        double s0 = (double)p.vfull[(size_t)t * ne + e], s1 = 0.0;   // fp64 sums (the set's terms cancel)
+        double z;
+        if (p.z0all) {   // the solve finish: z_0 from the GEMM
+            z = (double)p.z0all[(size_t)inst * p.z0_ld + e];
+        } else {
+            const T *tr = p.txfull + (size_t)e * NX;
+            double s0 = (double)p.vfull[(size_t)t * ne + e], s1 = 0.0;   // fp64 sums (the set's terms cancel)
 #pragma unroll
-        for (int c = 0; c + 1 < NX; c += 2) {
-            s0 = fma((double)tr[c], L.xs[c], s0);
-            s1 = fma((double)tr[c + 1], L.xs[c + 1], s1);
+            for (int c = 0; c + 1 < NX; c += 2) {
+                s0 = fma((double)tr[c], L.xs[c], s0);
+                s1 = fma((double)tr[c + 1], L.xs[c + 1], s1);
+            }
+            if (NX % 2) s0 = fma((double)tr[NX - 1], L.xs[NX - 1], s0);
+            z = s0 + s1;
         }
-        if (NX % 2) s0 = fma((double)tr[NX - 1], L.xs[NX - 1], s0);
-        double z = s0 + s1;
         // W[S, e] nu in batches of 4 (the loads of a batch issued together)
         for (int i0 = 0; i0 < m; i0 += 4) {
             double wv[4];
@@ -1195,7 +1213,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
 
 // WPB wavefronts per workgroup (the slot tables in LDS are shared by them), MW the occupancy target
 // (waves per SIMD; 0: none)
-template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
+template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP, bool WL = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0 ? MW : 1, 8))) void cl_fast_kernel(ClFastParams<T> p)
 {
     constexpr int NZ = NX + NU, NSLOT = EPL * 64;
@@ -1235,6 +1253,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         sse[s] = v ? p.s_e[s] : -1;
         ssrc[s] = v ? p.s_src[s] : -1;
     }
+    // WL: W over the slots in LDS (lower triangle; the rare path's gathers and W[:, S] nu combinations
+    // then wait on LDS instead of L2 — the force shape, whose steps are mostly active-set steps)
+    constexpr int NTRI = WL ? NSLOT * (NSLOT + 1) / 2 : 1;
+    __shared__ double wtri[NTRI];
+    if constexpr (WL) {
+        for (int e = threadIdx.x; e < NTRI; e += 64 * WPB) {
+            int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);   // row of triangle entry e
+            while ((r + 1) * (r + 2) / 2 <= e) r++;
+            while (r * (r + 1) / 2 > e) r--;
+            const int c = e - r * (r + 1) / 2;
+            wtri[e] = (r < p.nslot && c < p.nslot) ? p.W[(size_t)p.s_e[r] * p.ne + p.s_e[c]] : 0.0;
+        }
+    }
     __shared__ int wg_next;   // the workgroup's next instance (offset into its range)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
@@ -1244,7 +1275,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 #endif
     if (threadIdx.x == 0) wg_next = 0;
     __syncthreads();
-    const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
+    const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane, wtri, WL};
 
     const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
     const double wl = lane < p.ncl ? (double)p.wcl[lane] : 0.0;   // this lane's cost weight
@@ -1285,6 +1316,127 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 #pragma unroll
             for (int j = 0; j < EPL; j++) z[j] += z1[j];
         });
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------------------
+// The exact finish of fp32 handles' solves (nmpc_solve / solve_async; fp64 handles finish inside the IPM
+// kernel). The fp32 IPM stops at tol_comp 1e-7 in fp32 arithmetic, 1e-3..1e-2 from the exact solution on
+// the force OCP (condition ~4e4); the finish takes its active bounds as the warm set and runs the lean
+// loop's machinery on them — PDAS on the projected inverse Hessian W (fp64), the dual fallback, the fp64
+// KKT acceptance — so an accepted solution is the exact QP solution of the fp32-stored problem data.
+//
+// Step 1 (fin32_z0_kernel): the unconstrained solution of every element, linear in the pinned state and the
+// reference, z_0 = M [x0; yref] + vc (M = [T_x | V_y], host-built from the unconstrained Riccati tables), as
+// a batched GEMM on v_mfma_f32_16x16x4_f32 (A[i][k] = lane 16k + i, B[k][j] = lane 16k + j, D[4 (l >> 4) +
+// r][l & 15]): rows = elements in tiles of 16, columns = 16 instances per workgroup, K = nx + the stage-
+// stacked reference in steps of 4; each wavefront of the workgroup takes every WPB-th element tile.
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void fin32_z0_kernel(Fin32Z0Params p)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int j = lane & 15, kl = lane >> 4;
+    const int ib = (int)blockIdx.x * 16 + j;   // this lane's instance (B operand column)
+    const bool iv = ib < p.B;
+    const int ntile = p.m16 / 16, K = p.nx + p.ystride;
+    for (int et = wave; et < ntile; et += WPB) {
+        using f4 = __attribute__((__vector_size__(4 * sizeof(float)))) float;
+        f4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; r++) acc[r] = p.vc[et * 16 + 4 * kl + r];
+        const float *mrow = p.M + (size_t)(et * 16 + j) * p.kp;   // A operand row (element et * 16 + j)
+        for (int k0 = 0; k0 < p.kp; k0 += 4) {
+            const int k = k0 + kl;
+            const float a = mrow[k];
+            float b = 0.f;
+            if (iv && k < K) b = k < p.nx ? p.x0[(size_t)ib * p.nx + k] : p.yref[(size_t)ib * p.ystride + (k - p.nx)];
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        }
+        if (iv) {
+            float4 v;
+            v.x = acc[0];
+            v.y = acc[1];
+            v.z = acc[2];
+            v.w = acc[3];
+            *reinterpret_cast<float4 *>(p.z0 + (size_t)ib * p.m16 + et * 16 + 4 * kl) = v;
+        }
+    }
+}
+
+// Step 2: one wavefront per instance (persistent). An instance the IPM did not solve (status != 0) keeps
+// its result. Otherwise: z_0 at the slots from step 1; the warm set = the bounds the IPM solution sits on
+// (within 1e-3 (1 + |b|) — the fp32 interior point's distance from an active bound); no set and z_0
+// feasible: the unconstrained solution; else slow_step (PDAS rounds, certificate, dual fallback). Accepted:
+// the outputs are rewritten from the exact solution (free elements z_0 + W[:, S] nu) and the finish's
+// active-set steps are added to qp_iter; not accepted: the IPM's solution stays.
+template <int NX, int NU, int EPL, int WSM, int WPB>
+__global__ __launch_bounds__(64 * WPB) void fin32_kernel(ClFastParams<float> p)
+{
+    using T = float;
+    constexpr int NZ = NX + NU, NSLOT = EPL * 64;
+    __shared__ Lds<NSLOT, NZ, WSM> lds_all[WPB];
+    __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT], slo[NSLOT], shi[NSLOT], sol[NSLOT], sou[NSLOT];
+    __shared__ int sse[NSLOT], ssrc[NSLOT];
+    for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) abl[e] = (double)p.AB[e];
+    for (int e = threadIdx.x; e < NX; e += 64 * WPB) cl[e] = (double)p.c[e];
+    for (int s = threadIdx.x; s < NSLOT; s += 64 * WPB) {
+        const bool v = s < p.nslot;
+        const double l = v ? (double)p.s_lb[s] : -1e30, u = v ? (double)p.s_ub[s] : 1e30;
+        const bool hl = has_b(l), hu = has_b(u);
+        slb[s] = l;
+        sub[s] = u;
+        slo[s] = hl ? l - ClfTol<T>::viol * (1.0 + fabs(l)) : -DBL_MAX;
+        shi[s] = hu ? u + ClfTol<T>::viol * (1.0 + fabs(u)) : DBL_MAX;
+        sol[s] = hl ? l + 1e-3 * (1.0 + fabs(l)) : -DBL_MAX;   // the IPM solution's active bounds
+        sou[s] = hu ? u - 1e-3 * (1.0 + fabs(u)) : DBL_MAX;
+        sse[s] = v ? p.s_e[s] : -1;
+        ssrc[s] = -1;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
+    if (lane < 32) L.xs[lane] = 0.0;
+#ifdef NMPC_CLF_TIMING
+    if (lane < CLF_NT) L.tacc[lane] = 0;
+#endif
+    __syncthreads();
+    const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
+    for (int inst = (int)blockIdx.x * WPB + wave; inst < p.B; inst += (int)gridDim.x * WPB) {
+        if (p.status[inst] != 0) continue;   // wave-uniform
+        if (lane < NX) L.xs[lane] = (double)p.x0in[(size_t)inst * NX + lane];
+        T z[EPL];
+        unsigned wf = 0;
+#pragma unroll
+        for (int j = 0; j < EPL; j++) {
+            const int e = sv.e(j);
+            z[j] = e >= 0 ? p.z0all[(size_t)inst * p.z0_ld + e] : T(0);
+            if (e >= 0) {
+                const int k = e / NZ, r = e % NZ;
+                const T zi = r < NX ? p.xout[((size_t)inst * (p.N + 1) + k) * NX + r]
+                                    : p.uout[((size_t)inst * p.N + k) * NU + (r - NX)];
+                wf |= (zi <= (T)sv.onl(j) ? 1u : (zi >= (T)sv.onu(j) ? 2u : 0u)) << (2 * j);
+            }
+        }
+        CLF_SYNC();
+        bool ok = false;
+        int m_acc = 0, steps = 0;
+        if (!__any(wf != 0)) {
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < EPL; j++) bad |= !(z[j] >= (T)sv.lo(j) && z[j] <= (T)sv.hi(j));
+            ok = !__any(bad);
+        }
+        if (!ok) {
+            const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, wf, false, false);
+            ok = ((sr >> 8) & 1) && (sr & 0xff) == 0;
+            m_acc = (sr >> 10) & 0xff;
+            steps = sr >> 18;
+        }
+        if (ok) {
+            write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, 0, 0, m_acc, z);
+            if (lane == 0) p.iters[inst] += steps;
+        }
+        CLF_SYNC();
     }
 }
 
@@ -1713,10 +1865,10 @@ int cl_fast_wsmax(int nx, int nu)
 }
 
 // one compiled variant per shape, as a tag type
-template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, int MW_, class SP_>
+template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, int MW_, class SP_, bool WL_ = false>
 struct Variant {
     static constexpr int WPB = WPB_;
-    static constexpr auto kernel() { return clf::cl_fast_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_>; }
+    static constexpr auto kernel() { return clf::cl_fast_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_, WL_>; }
 };
 // the lockstep kernel (four instances per wavefront, MFMA explicit form and plant)
 template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, class SP_>
@@ -1727,14 +1879,15 @@ struct LockVariant {
 
 // whether the shape has a lockstep kernel (controller-model plant, cost on x_0: checked by the host)
 bool cl_lock_shape(int nx, int nu) { return nx == 13 && nu == 4; }
+bool cl_wlds_shape(int nx, int nu) { return nx == 4 && nu == 2; }
 
 // calls f(Variant<...>{}) for the shape's compiled variant; false: none. NMPC_CLF_VARIANT=1 (tuning):
 // an occupancy target (quad13 4 waves per SIMD: spills, measured 10 % slower than the default)
 template <typename T, class F>
-static bool clf_dispatch(int nx, int nu, int sid, bool lock, F &&f)
+static bool clf_dispatch(int nx, int nu, int sid, int kind, F &&f)
 {
     static const int var = std::getenv("NMPC_CLF_VARIANT") ? std::atoi(std::getenv("NMPC_CLF_VARIANT")) : 0;
-    if (lock) {   // fp64 only (the f64 MFMA tiles)
+    if (kind == CLF_LOCK) {   // fp64 only (the f64 MFMA tiles)
         if constexpr (std::is_same<T, double>::value) {
             if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::Quad13Structure>{});
             else if (nx == 13 && nu == 4) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::DenseStructure<13, 4>>{});
@@ -1751,7 +1904,8 @@ static bool clf_dispatch(int nx, int nu, int sid, bool lock, F &&f)
     } else if (nx == 6 && nu == 2) {
         f(Variant<T, 6, 2, 5, 16, 8, 0, lpc::DenseStructure<6, 2>>{});
     } else if (nx == 4 && nu == 2) {
-        if (var == 1) f(Variant<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>{});
+        if (kind == CLF_WLDS) f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>, true>{});
+        else if (var == 1) f(Variant<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>{});
         else f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>{});
     } else {
         return false;
@@ -1761,7 +1915,7 @@ static bool clf_dispatch(int nx, int nu, int sid, bool lock, F &&f)
 
 // the workgroups of the shape's kernel that `device` holds at once (the persistent grid), queried for
 // the given device at nmpc_closed_loop_init and kept on the handle (no process-wide cache)
-int cl_fast_resident(int nx, int nu, int sid, bool lock, bool f64, int device)
+int cl_fast_resident(int nx, int nu, int sid, int kind, bool f64, int device)
 {
     int res = 0;
     auto occ = [&](auto v) {
@@ -1771,27 +1925,70 @@ int cl_fast_resident(int nx, int nu, int sid, bool lock, bool f64, int device)
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) return;
         res = per_cu * cus;
     };
-    if (f64) clf_dispatch<double>(nx, nu, sid, lock, occ);
-    else clf_dispatch<float>(nx, nu, sid, lock, occ);
+    if (f64) clf_dispatch<double>(nx, nu, sid, kind, occ);
+    else clf_dispatch<float>(nx, nu, sid, kind, occ);
     return res;
 }
 
 // grid: min(workgroups for one wavefront per instance, the resident workgroups)
 template <typename T>
-hipError_t cl_fast_launch(int nx, int nu, int sid, bool lock, const ClFastParams<T> &p, int waves, int resident,
+hipError_t cl_fast_launch(int nx, int nu, int sid, int kind, const ClFastParams<T> &p, int waves, int resident,
                           hipStream_t s)
 {
-    const bool ok = clf_dispatch<T>(nx, nu, sid, lock, [&](auto v) {
+    const bool ok = clf_dispatch<T>(nx, nu, sid, kind, [&](auto v) {
         using V = decltype(v);
         // the lockstep kernel: four instances per wavefront
-        const int wv = lock ? (waves + 3) / 4 : waves;
+        const int wv = kind == CLF_LOCK ? (waves + 3) / 4 : waves;
         const int blocks = std::max(1, std::min((wv + V::WPB - 1) / V::WPB, resident));
         hipLaunchKernelGGL(V::kernel(), dim3(blocks), dim3(64 * V::WPB), 0, s, p);
     });
     return ok ? hipGetLastError() : hipErrorInvalidValue;
 }
 
-template hipError_t cl_fast_launch<double>(int, int, int, bool, const ClFastParams<double> &, int, int, hipStream_t);
-template hipError_t cl_fast_launch<float>(int, int, int, bool, const ClFastParams<float> &, int, int, hipStream_t);
+template hipError_t cl_fast_launch<double>(int, int, int, int, const ClFastParams<double> &, int, int, hipStream_t);
+
+hipError_t fin32_z0_launch(const Fin32Z0Params &p, hipStream_t s)
+{
+    if (p.m16 % 16 || p.kp % 4 || p.B < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(clf::fin32_z0_kernel<4>, dim3((p.B + 15) / 16), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+// the finish's compiled shapes: the lean loop's slot layouts (one wavefront per instance), with more slots
+// per lane for longer horizons (force N <= 20 / 31 / 42, jerk N <= 40 / 56, quad13 N <= 20 / 30)
+template <class F>
+static bool fin32_dispatch(int nx, int nu, int nslot, F &&f)
+{
+    if (nx == 13 && nu == 4 && nslot <= 256) f(clf::fin32_kernel<13, 4, 4, 16, 8>, 8);
+    else if (nx == 13 && nu == 4 && nslot <= 384) f(clf::fin32_kernel<13, 4, 6, 16, 4>, 4);
+    else if (nx == 6 && nu == 2 && nslot <= 320) f(clf::fin32_kernel<6, 2, 5, 16, 8>, 8);
+    else if (nx == 6 && nu == 2 && nslot <= 448) f(clf::fin32_kernel<6, 2, 7, 16, 4>, 4);
+    else if (nx == 4 && nu == 2 && nslot <= 128) f(clf::fin32_kernel<4, 2, 2, 32, 4>, 4);
+    else if (nx == 4 && nu == 2 && nslot <= 192) f(clf::fin32_kernel<4, 2, 3, 32, 4>, 4);
+    else if (nx == 4 && nu == 2 && nslot <= 256) f(clf::fin32_kernel<4, 2, 4, 32, 4>, 4);
+    else return false;
+    return true;
+}
+
+int fin32_resident(int nx, int nu, int nslot, int device)
+{
+    int res = 0;
+    fin32_dispatch(nx, nu, nslot, [&](auto k, int wpb) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64 * wpb, 0) != hipSuccess || per_cu < 1) return;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) return;
+        res = per_cu * cus;
+    });
+    return res;
+}
+
+bool fin32_launch(int nx, int nu, int, const ClFastParams<float> &p, int resident, hipStream_t s)
+{
+    return fin32_dispatch(nx, nu, p.nslot, [&](auto k, int wpb) {
+        const int blocks = std::max(1, std::min((p.B + wpb - 1) / wpb, resident));
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, s, p);
+    });
+}
+template hipError_t cl_fast_launch<float>(int, int, int, int, const ClFastParams<float> &, int, int, hipStream_t);
 
 }  // namespace nmpc

@@ -135,7 +135,25 @@ struct ClFastParams {
     int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
     int *iter_log;                // optional [steps][B]: active-set steps (<= 255) | status << 8 | wall-clock ticks (<= 32767) << 16
     unsigned long long *cycles;   // diagnostic builds (NMPC_CLF_TIMING): [B][14] phase cycles / counts per instance
+    // the fp32 solve finish (fin32_kernel): z_0 of every element per instance ([B][z0_ld], fin32_z0_kernel),
+    // the pinned states x0 [B][nx]; the lean loop leaves them null (z_0 from T_x x + v_t)
+    const T *z0all;
+    int z0_ld;
+    const T *x0in;
 };
+// fp32 handles' exact finish of a solve (nmpc_cl_fast.hip): z_0 = M [x0; yref] + vc for every element on the
+// f32 matrix cores, then per instance the lean loop's active-set machinery (fp64 W, solves and acceptance)
+// from the IPM solution's active bounds. M: [m16 rows][kp] (rows = elements, zero-padded), vc [m16].
+struct Fin32Z0Params {
+    int B, nx, ystride, kp, m16;
+    const float *M, *vc, *x0, *yref;
+    float *z0;   // [B][m16]
+};
+hipError_t fin32_z0_launch(const Fin32Z0Params &p, hipStream_t s);
+// false: no compiled finish for the shape and slot count (p.nslot)
+bool fin32_launch(int nx, int nu, int sid, const ClFastParams<float> &p, int resident, hipStream_t s);
+// resident workgroups of the finish for (nx, nu, nslot) on `device`; 0: none compiled
+int fin32_resident(int nx, int nu, int nslot, int device);
 // compiled fast kernels: EPL slots per lane (0 if none for this shape)
 int cl_fast_epl(int nx, int nu);
 // largest active set of the fast path for the shape (oracle/cref.py WSMAX)
@@ -143,12 +161,16 @@ int cl_fast_wsmax(int nx, int nu);
 // whether the shape has the lockstep kernel cl_lock_kernel (four instances per wavefront, MFMA explicit form
 // and plant; the controller-model plant with the cost on x_0 only)
 bool cl_lock_shape(int nx, int nu);
+// whether the shape has a cl_fast_kernel variant with W over the slots in LDS (the force shape)
+bool cl_wlds_shape(int nx, int nu);
+// lean-loop kernel kinds: one instance per wavefront (W from L2 / from LDS), the lockstep kernel
+constexpr int CLF_FAST = 0, CLF_LOCK = 1, CLF_WLDS = 2;
 // workgroups of the shape's cl_fast_kernel (lock: cl_lock_kernel, fp64 only) in the handle's precision
 // that `device` holds at once (the persistent grid), or 0
-int cl_fast_resident(int nx, int nu, int sid, bool lock, bool f64, int device);
+int cl_fast_resident(int nx, int nu, int sid, int kind, bool f64, int device);
 // grid = min(waves / wavefronts per workgroup, resident); waves = instances (lock: instances / 4)
 template <typename T>
-hipError_t cl_fast_launch(int nx, int nu, int sid, bool lock, const ClFastParams<T> &p, int waves, int resident,
+hipError_t cl_fast_launch(int nx, int nu, int sid, int kind, const ClFastParams<T> &p, int waves, int resident,
                           hipStream_t s);
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);

@@ -4,8 +4,12 @@ Every test goes through the C-ABI (libnmpc_hip.so) via the façade. Expected val
 from the KKT-certified dense oracle (tests/golden/qp_cases.npz, oracle/qp.py) and the
 plain-C Riccati IPM (oracle/c). Tolerance (BASELINE.json north_star): 1e-6 relative on the
 x/u trajectories, measured as max|z_gpu - z_ref| / max(1, max|z_ref|) per instance, fp64.
-fp32 is a throughput configuration; its bar is 3e-2 relative (condition number of the
-force-model Hessian ~4e4, SURVEY §7 hard part 2).
+fp32 handles: the IPM in fp32, then the exact finish (nmpc_cl_fast.hip fin32_*: z_0 = [T_x | V_y][x0; yref]
++ v_c on the f32 matrix cores, PDAS / dual active-set steps on the fp64 W with fp64 acceptance). Their bar
+TOL32 = 2e-5: the finish returns the exact solution of the fp32-rounded data, whose
+distance from the fp64 solution is the rounding of z_0 (a few fp32 ulps of |T_x x0| + |V_y yref| ~ 1-10)
+carried through W[:, S] W_SS^-1 — not amplified by cond(W_SS) ~ 4e4, since W and the solves are fp64.
+Measured max 4.6e-6 (force), 1.6e-6 (jerk), 4.2e-6 (quad13); the fp32 IPM alone was 1e-4 .. 1e-2.
 """
 import os
 
@@ -20,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 KEYS = ["force_N20", "force_N30", "jerk_N40", "jerk_N30", "quad13_N20"]
 TOL64 = 1e-6
-TOL32 = 3e-2
+TOL32 = 2e-5
 
 
 @pytest.fixture(scope="module")
