@@ -37,11 +37,11 @@ if [ "${PROF:-1}" = "1" ]; then
   find $OUT/prof_${TAG} -name "*kernel_stats*" | head -3
 fi
 if [ "${PMC:-1}" = "1" ]; then
-  TAG=${TAG}_quad13_b8192_fp64 KERNEL=cl_fast_kernel BENCH_ARGS="" TRAFFIC=quad13,20,8192,fp64 bash tools/pmc_bench.sh || exit 1
+  TAG=${TAG}_quad13_b8192_fp64 KERNEL=cl_lock_kernel BENCH_ARGS="" TRAFFIC=quad13,20,8192,fp64 bash tools/pmc_bench.sh || exit 1
   TAG=${TAG}_force_b1024_fp64 KERNEL=cl_fast_kernel BENCH_ARGS="--model force --batch 1024" TRAFFIC=force,20,1024,fp64 bash tools/pmc_bench.sh || exit 1
   TAG=${TAG}_force_b8192_fp64 KERNEL=cl_fast_kernel BENCH_ARGS="--model force --batch 8192" TRAFFIC=force,20,8192,fp64 bash tools/pmc_bench.sh || exit 1
   TAG=${TAG}_jerk_b4096_fp64 KERNEL=cl_fast_kernel BENCH_ARGS="--model jerk --batch 4096" TRAFFIC=jerk,40,4096,fp64 bash tools/pmc_bench.sh || exit 1
-  TAG=${TAG}_force_b8192_fp32 KERNEL=${FP32_KERNEL:-ipm_lpc_kernel} BENCH_ARGS="--model force --batch 8192 --precision fp32" TRAFFIC=force,20,8192,fp32 bash tools/pmc_bench.sh || exit 1
+  TAG=${TAG}_force_b8192_fp32 KERNEL=${FP32_KERNEL:-cl_fast_kernel} BENCH_ARGS="--model force --batch 8192 --precision fp32" TRAFFIC=force,20,8192,fp32 bash tools/pmc_bench.sh || exit 1
   TAG=${TAG}_solve_quad13_b8192_fp64 KERNEL=ipm_lpc_kernel MODE=solve STEPS=5 BENCH_ARGS="" TRAFFIC=quad13,20,8192,fp64 bash tools/pmc_bench.sh || exit 1
 fi
 echo "r5 round done"
