@@ -92,6 +92,11 @@ def main():
                                                      if "SQ_INSTS_VALU_FLOPS_FP64" in means else None),
                              "fp32_flops_per_step": (64.0 * means["SQ_INSTS_VALU_FLOPS_FP32"] / a.steps_per_launch
                                                      if "SQ_INSTS_VALU_FLOPS_FP32" in means else None),
+                             # MFMA utilisation inputs: f64 MFMA instructions, the MFMA pipe's busy cycles
+                             # (summed over SIMDs) and GRBM_GUI_ACTIVE (summed over the 8 XCDs: / 8 = cycles)
+                             "mfma_f64_insts_per_launch": means.get("SQ_INSTS_VALU_MFMA_F64"),
+                             "mfma_busy_cycles_per_launch": means.get("SQ_VALU_MFMA_BUSY_CYCLES"),
+                             "gui_active_per_launch": means.get("GRBM_GUI_ACTIVE"),
                              "wait_any_frac": (means["SQ_WAIT_ANY"] / means["SQ_WAVE_CYCLES"]
                                                if means.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in means else None),
                              "source": os.path.relpath(out, ROOT)})
