@@ -158,6 +158,24 @@ def min_bytes_per_instance_step(nx, nu, precision):
     return (2 * nx + nu) * w + 4
 
 
+def mfma_block(pmc, kernel_ms, spl):
+    """MFMA use of the timed kernel from the committed PMC pass at this launch length: the f64 matrix
+    instructions (the lockstep kernel's v_mfma_f64_4x4x4_4b_f64: 4 blocks x 4x4x4 x 2 = 512 flops each), their
+    flops against the FP64 matrix peak at this run's kernel time, and the MFMA pipe's busy fraction
+    (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)."""
+    n = pmc.get("mfma_f64_insts_per_launch")
+    if n is None:
+        return None
+    fl = 512.0 * n / spl   # per closed-loop step
+    busy, gui = pmc.get("mfma_busy_cycles_per_launch"), pmc.get("gui_active_per_launch")
+    return {"f64_insts_per_step": n / spl, "f64_flops_per_step": fl,
+            "achieved_tflops": fl / (kernel_ms * 1e-3) / 1e12,
+            "frac_of_fp64_matrix_peak": fl / (kernel_ms * 1e-3) / 1e12 / PEAK_TFLOPS["fp64"],
+            "pipe_busy_frac": (busy / (gui / 8.0 * 1024.0)) if busy and gui else None,
+            "wait_any_frac": pmc.get("wait_any_frac"),
+            "note": "from the committed rocprofv3 PMC pass at this launch length (" + str(pmc.get("source")) + ")"}
+
+
 def python_loop_rate(N, steps):
     """BASELINE config 1: the reference's single-trajectory closed loop (force_model/controller.py
     :25-54) as the drop-in sees it — per step 31 yref set() calls, lbx/ubx, solve(), get(), the
@@ -334,6 +352,7 @@ def main():
                                           f"lanes included; {pmc.get('source', 'no PMC pass for this config and launch length')}) "
                                           "/ this run's kernel time / peak",
                          "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
+                         "mfma": mfma_block(pmc, kernel_ms, spl),
                          "traffic": traffic,
                          "min_bytes_per_step": min_b,
                          "traffic_vs_min_bytes": traffic / min_b if traffic else None,

@@ -1799,8 +1799,13 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     // the lockstep kernel for the shapes that have one, with the controller-model plant and the cost on x_0
     // (env NMPC_CLF_LOCK=0: the one-instance-per-wavefront kernel)
     const char *lenv = std::getenv("NMPC_CLF_LOCK");
-    const bool lock = f64 && nmpc::cl_lock_shape(nx, nu) && d.plant == NMPC_PLANT_MODEL && d.cost_stage == 0 &&
-                      !(lenv && lenv[0] == '0');
+    // (the controller-model plant, or the jerk shape with its converter plant; the cost on x_0 or x_1). The jerk
+    // shape's lockstep variant is opt-in (NMPC_CLF_LOCK=1): its 20 tiles of z and v_t spill 130 VGPRs at 2 waves
+    // per SIMD and it measured 200-202M against cl_fast_kernel's 253M steps/s (jerk B = 4096, tools/ab_check.sh lk4)
+    const bool jerk = nx == 6 && nu == 2;
+    const bool lock = f64 && nmpc::cl_lock_shape(nx, nu) && d.cost_stage <= 1 &&
+                      (d.plant == NMPC_PLANT_MODEL || (jerk && d.plant == NMPC_PLANT_CRAZYFLIE_JERK)) &&
+                      (jerk ? (lenv && lenv[0] == '1') : !(lenv && lenv[0] == '0'));
     // W over the slots in LDS for the shapes that have the variant, env NMPC_CLF_WLDS=1 (tuning; off by default:
     // force B = 1024 17.9M vs 19.0M, B = 8192 57.0M vs 80.5M steps/s — one workgroup per CU, and the rare
     // path's steps are bound by their instruction chains, not by W's L2 latency; tools/ab_check.sh, wl1)
@@ -1894,6 +1899,9 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     // one wavefront per workgroup starts in phase 2 (drains demoted instances while the others still run
     // lockstep): quad13 B = 8192 415M (0) -> 458-463M (1), 452-457M (2), 405-412M (3) steps/s (tools/lock_ab.sh, ab1/ab2)
     p.lock_workers = lw ? std::max(0, std::min(4, std::atoi(lw))) : 1;
+    // the force shape claims its instances device-wide (env NMPC_CLF_GCLAIM=0 / 1 overrides)
+    const char *gc = std::getenv("NMPC_CLF_GCLAIM");
+    p.claim_global = gc ? (gc[0] == '1') : (h->nx == 4 && h->nu == 2);
     return p;
 }
 

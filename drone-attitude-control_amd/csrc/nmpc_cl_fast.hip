@@ -1287,11 +1287,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // next one from a counter in LDS until none is left (an instance's cost varies 10x with its active
     // sets; every wavefront reaches the exit). Against one device-wide counter: jerk +14 %, force
     // B = 8192 -6 % (less balancing across workgroups), quad13 unchanged (r4e / r4f)
+    // (p.claim_global: one device-wide counter instead, p.park_count[1] — the force shape, whose instances'
+    // costs vary most, balances across workgroups)
     const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int wg_lo = (int)blockIdx.x * per_wg, wg_hi = min(p.B, wg_lo + per_wg);
+    const int wg_lo = p.claim_global ? 0 : (int)blockIdx.x * per_wg, wg_hi = p.claim_global ? p.B : min(p.B, wg_lo + per_wg);
     for (;;) {
         int next = 0;
-        if (lane == 0) next = atomicAdd(&wg_next, 1);
+        if (lane == 0) next = p.claim_global ? atomicAdd(p.park_count + 1, 1) : atomicAdd(&wg_next, 1);
         const int inst = wg_lo + __builtin_amdgcn_readfirstlane(next);
         if (inst >= wg_hi) break;
         // explicit unconstrained solution at the lane's slots: T_x pairs from LDS against x pairs broadcast
@@ -1726,21 +1728,68 @@ __global__ __launch_bounds__(64 * WPB) void cl_lock_kernel(ClFastParams<T> p)
             if (adv && step + 1 < p.target) fetch_v(tn);
             CLF_TADD(L, 18, tk_ld);
             CLF_T(tk_pl);
-            // ---- cost (controller.py:40-41) at x_0 and the AED numerator: lanes 16 k + n (block 0)
+            // ---- cost (controller.py:40-41) at x_0, or at x_1 (the jerk loop, cost_stage 1: x_1's components
+            // are the slots x1_slot + c < 64, z of tile (s >> 4) on lane 16 (s & 3) + 4 ((s >> 2) & 3) + n, clamped
+            // as run_instance's z0c), and the AED numerator at x_0: lanes 16 k + n (block 0)
+            double xo[KC];
+#pragma unroll
+            for (int kc = 0; kc < KC; kc++) xo[kc] = xr[kc];
+            if constexpr (NX == 6 && NU == 2) {
+              if (p.cost_stage != 0) {   // wave-uniform
+#pragma unroll
+                for (int kc = 0; kc < KC; kc++) {
+                    const int c = 4 * kc + ti, s_ = p.x1_slot + (c < NX ? c : 0);
+                    const int src = 16 * (s_ & 3) + 4 * ((s_ >> 2) & 3) + n;
+                    double v = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4 && q < NT; q++) {
+                        const double zq = __shfl((double)z[q], src);
+                        if ((s_ >> 4) == q) v = zq;
+                    }
+                    xo[kc] = s_ < NSLOT ? fmin(fmax(v, slb[s_]), sub[s_]) : 0.0;
+                }
+              }
+            }
             if (adv && tb == 0) {
 #pragma unroll
                 for (int kc = 0; kc < KC; kc++) {
                     const int c = 4 * kc + ti;
                     if (c < NX) {
-                        const double e = xr[kc] - xrf[kc];
+                        const double e = xo[kc] - xrf[kc];
                         if (c < p.ncl) cost = fma((double)p.wcl[c] * e, e, cost);
                         if (c < p.aed_dims) aed += fabs(xrf[kc] - xr[kc]);
                     }
                 }
             }
+            if constexpr (NX == 6 && NU == 2) {
+                if (p.plant == 2) {
+                    // ---- the jerk converter plant (plant_step's arithmetic, src/plant.py): every lane of
+                    // instance n evaluates it on the instance's gathered state and inputs
+                    double x4[4], f[4];
+#pragma unroll
+                    for (int c = 0; c < 4; c++) x4[c] = __shfl(xr[0], 16 * c + n);
+                    double a0 = __shfl(xr[1], n), a1 = __shfl(xr[1], 16 + n);
+                    const double h0 = __shfl(u0v, n), h1 = __shfl(u0v, 16 + n), inv_m = 1.0 / p.mass;
+                    for (int j = 0; j < p.substeps; j++) {
+                        a0 = a0 + h0 * p.dt_conv;
+                        a1 = a1 + h1 * p.dt_conv;
+                        crazyflie_rhs(x4, p.mass * a0, p.mass * a1, 1.0, inv_m, p.g, f);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) x4[i] += p.dt_conv * f[i];
+                    }
+                    if (adv) {
+                        double x0n = 0.0;
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (ti == i) x0n = x4[i] + w;
+                        xr[0] = x0n;
+                        xr[1] = ti == 0 ? a0 : (ti == 1 ? a1 : 0.0);
+                    }
+                }
+            }
             // ---- plant X' = [A B] [X; U] + c + noise on the matrix cores: A operand [A B] (row prow, columns
             // 4 kc + (lane >> 4); the inputs' chunk last) from the workgroup's copy, C = c + noise
-            {
+            if (p.plant == 0) {
                 double d = (drow < NX ? cl[drow] : 0.0) + ((drow < p.noise_dims && drow < NX) ? w : 0.0);
 #pragma unroll
                 for (int kc = 0; kc < KC; kc++) {
@@ -1877,8 +1926,9 @@ struct LockVariant {
     static constexpr auto kernel() { return clf::cl_lock_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, SP_>; }
 };
 
-// whether the shape has a lockstep kernel (controller-model plant, cost on x_0: checked by the host)
-bool cl_lock_shape(int nx, int nu) { return nx == 13 && nu == 4; }
+// whether the shape has a lockstep kernel (quad13; jerk, whose plant may be its converter and whose cost may
+// sit on x_1: the host checks plant and cost stage)
+bool cl_lock_shape(int nx, int nu) { return (nx == 13 && nu == 4) || (nx == 6 && nu == 2); }
 bool cl_wlds_shape(int nx, int nu) { return nx == 4 && nu == 2; }
 
 // calls f(Variant<...>{}) for the shape's compiled variant; false: none. NMPC_CLF_VARIANT=1 (tuning):
@@ -1891,6 +1941,7 @@ static bool clf_dispatch(int nx, int nu, int sid, int kind, F &&f)
         if constexpr (std::is_same<T, double>::value) {
             if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::Quad13Structure>{});
             else if (nx == 13 && nu == 4) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::DenseStructure<13, 4>>{});
+            else if (nx == 6 && nu == 2) f(LockVariant<T, 6, 2, 5, 16, 8, lpc::DenseStructure<6, 2>>{});
             else return false;
             return true;
         }

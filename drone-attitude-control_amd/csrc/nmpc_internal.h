@@ -109,6 +109,7 @@ struct ClFastParams {
     int polish_steps;             // active-set rounds of the fast path
     int gi;                       // 1: the dual active-set fallback runs; 0 (test knob): such steps park
     int lock_workers;             // lockstep kernel: wavefronts per workgroup that start in phase 2
+    int claim_global;             // cl_fast_kernel: instances from one device-wide counter (park_count[1])
     int x1_slot;                  // slot (lane, j = 0) of x_1[0] (cost of the jerk loop: cost_stage 1)
     const T *table;               // reference table [rows][table_cols]
     const int *offset;            // [B]
@@ -158,8 +159,8 @@ int fin32_resident(int nx, int nu, int nslot, int device);
 int cl_fast_epl(int nx, int nu);
 // largest active set of the fast path for the shape (oracle/cref.py WSMAX)
 int cl_fast_wsmax(int nx, int nu);
-// whether the shape has the lockstep kernel cl_lock_kernel (four instances per wavefront, MFMA explicit form
-// and plant; the controller-model plant with the cost on x_0 only)
+// whether the shape has the lockstep kernel cl_lock_kernel (four instances per wavefront, MFMA explicit form;
+// quad13 with the controller-model plant, jerk with the model or its converter plant; cost on x_0 or x_1)
 bool cl_lock_shape(int nx, int nu);
 // whether the shape has a cl_fast_kernel variant with W over the slots in LDS (the force shape)
 bool cl_wlds_shape(int nx, int nu);

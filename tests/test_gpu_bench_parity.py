@@ -51,7 +51,7 @@ def test_bench_closed_loop_matches_oracle(golden, model, N, B):
     loop = ClosedLoop(model, B, N=N, seed=42)             # bench.py's workload and defaults
     info = loop.solver.launch_info()
     assert info["kernel"] in ("ipm_lpc_kernel", "ipm_kernel")
-    # the lean loop bench.py times (quad13: its lockstep MFMA kernel)
+    # the lean loop bench.py times (quad13: the lockstep MFMA kernel)
     assert info["closed_loop_kernel"] == ("cl_lock_kernel" if model == "quad13" else "cl_fast_kernel")
     states, sums = [], []
     for n in REGIONS:
@@ -81,6 +81,34 @@ def test_bench_closed_loop_matches_oracle(golden, model, N, B):
     assert err.max() < 1e-6, (err.max(), int(err.argmax()))
     assert np.array_equal(A[-1, :, 2:], ref.acc[:, 2:])
     np.testing.assert_allclose(A[-1, :, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.timeout(300)
+def test_jerk_lockstep_variant_matches_oracle():
+    """The jerk shape's lockstep kernel (opt-in, NMPC_CLF_LOCK=1: cl_lock_kernel with the jerk converter plant
+    evaluated per instance in the four-instance layout and the cost on x_1 gathered from the MFMA tiles;
+    src/jerk_model/controller.py:26-56) on a ragged batch of 1030 over 43 steps (3 + 40): states, sums and
+    failure counts against the C restatement of the GPU's algorithm (mode 1) over the whole batch."""
+    from drone_attitude_control_amd.batched import ClosedLoop, workload
+    from oracle import cref, models
+    from drone_attitude_control_amd.models import OCPS
+    os.environ["NMPC_CLF_LOCK"] = "1"
+    try:
+        cl = ClosedLoop("jerk", 1030, N=40, seed=7)
+        assert cl.solver.launch_info()["closed_loop_kernel"] == "cl_lock_kernel"
+        cl.run(3)
+        cl.run(40)
+        x, acc = cl.state(), cl.instance_stats()
+    finally:
+        os.environ.pop("NMPC_CLF_LOCK", None)
+    table, off, x0 = workload("jerk", 40, 1030, 7)
+    o = OCPS["jerk"](40).solver_options
+    ref = cref.ClosedLoopRef(models.jerk_model(40), "jerk", table, off, x0, mode=1, seed=7,
+                             tol_comp=o.qp_solver_tol_comp, tol_res=o.qp_solver_tol_stat)
+    ref.run(43)
+    assert _rel(x, ref.state).max() < 1e-6, _rel(x, ref.state).max()
+    assert np.array_equal(acc[:, 2:], ref.acc[:, 2:])
+    np.testing.assert_allclose(acc[:, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
 
 
 TOL_CL32 = 1e-5   # fp32 lean loop, DESIGN.md §6 (measured 1.4e-6, f32b)
