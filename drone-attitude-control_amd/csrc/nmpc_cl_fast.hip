@@ -1472,8 +1472,8 @@ __global__ __launch_bounds__(64 * WPB) void fin32_kernel(ClFastParams<float> p)
 // summation order of the explicit form and the plant differs (rounding).
 constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host checks B / grid <= LOCK_QCAP)
 
-template <typename T, int NX, int NU, int EPL, int WSM, int WPB, class SP>
-__global__ __launch_bounds__(64 * WPB) void cl_lock_kernel(ClFastParams<T> p)
+template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0 ? MW : 1, MW > 0 ? MW : 8))) void cl_lock_kernel(ClFastParams<T> p)
 {
     constexpr int NZ = NX + NU, NSLOT = EPL * 64, NT = NSLOT / 16, KC = (NX + 3) / 4, KU = (NU + 3) / 4;
     static_assert(NX <= 16 && NU <= 4 && NZ <= 64 && NT <= 32, "lockstep layout: states in 4 chunks, inputs in one");
@@ -1920,10 +1920,10 @@ struct Variant {
     static constexpr auto kernel() { return clf::cl_fast_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_, WL_>; }
 };
 // the lockstep kernel (four instances per wavefront, MFMA explicit form and plant)
-template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, class SP_>
+template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, int MW_, class SP_>
 struct LockVariant {
     static constexpr int WPB = WPB_;
-    static constexpr auto kernel() { return clf::cl_lock_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, SP_>; }
+    static constexpr auto kernel() { return clf::cl_lock_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_>; }
 };
 
 // whether the shape has a lockstep kernel (quad13; jerk, whose plant may be its converter and whose cost may
@@ -1939,9 +1939,11 @@ static bool clf_dispatch(int nx, int nu, int sid, int kind, F &&f)
     static const int var = std::getenv("NMPC_CLF_VARIANT") ? std::atoi(std::getenv("NMPC_CLF_VARIANT")) : 0;
     if (kind == CLF_LOCK) {   // fp64 only (the f64 MFMA tiles)
         if constexpr (std::is_same<T, double>::value) {
-            if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::Quad13Structure>{});
-            else if (nx == 13 && nu == 4) f(LockVariant<T, 13, 4, 4, 16, 8, lpc::DenseStructure<13, 4>>{});
-            else if (nx == 6 && nu == 2) f(LockVariant<T, 6, 2, 5, 16, 8, lpc::DenseStructure<6, 2>>{});
+            if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, 0, lpc::Quad13Structure>{});
+            else if (nx == 13 && nu == 4) f(LockVariant<T, 13, 4, 4, 16, 8, 0, lpc::DenseStructure<13, 4>>{});
+            // jerk: 20 tiles of z and v_t per lane — one wavefront per SIMD with the whole register file (four
+            // per workgroup; B = 4096 is one round of 1024 wavefronts)
+            else if (nx == 6 && nu == 2) f(LockVariant<T, 6, 2, 5, 16, 4, 1, lpc::DenseStructure<6, 2>>{});
             else return false;
             return true;
         }
