@@ -519,6 +519,15 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         CLF_SYNC();
     };
     auto add_states = [&](const double (&v)[EPL], unsigned sgn, unsigned &w) {
+        // no violated state bound anywhere: nothing to add (the argmax's LDS atomics and three wave syncs
+        // skipped; the slowest quad13 instances spend a third of a PDAS round there)
+        bool sv_ = false;
+#pragma unroll
+        for (int j = 0; j < EPL; j++) {
+            const int r = comp(j);
+            sv_ |= r >= 0 && r < NX && v[j] > 0.0;
+        }
+        if (!__any(sv_)) return;
         argmax_states(v);
 #pragma unroll
         for (int j = 0; j < EPL; j++) {
