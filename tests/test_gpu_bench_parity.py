@@ -115,17 +115,18 @@ TOL_CL32 = 1e-5   # fp32 lean loop, DESIGN.md §6 (measured 1.4e-6, f32b)
 
 
 @pytest.mark.timeout(300)
-def test_fp32_force_closed_loop_matches_oracle(golden):
-    """BASELINE config 3 (force N=20, B=8192, fp32) on the lean loop bench.py times: fp32 tables and
-    explicit form, fp64 set solves and acceptance (nmpc_cl_fast.hip ClfTol). Against the exact oracle
+@pytest.mark.parametrize("model,N,B", [("force", 20, 8192), ("quad13", 20, 8192), ("jerk", 40, 4096)])
+def test_fp32_closed_loop_matches_oracle(golden, model, N, B):
+    """fp32 handles on the lean loop (BASELINE config 3 is force N=20, B=8192, fp32): fp32 tables and
+    explicit form, fp64 W, set solves and acceptance (nmpc_cl_fast.hip ClfTol). Against the exact oracle
     loop (mode 0, closed_loop_bench.npz, fp64) on the bench's own seed-42 workload and launch
     boundaries: states at every region boundary within TOL_CL32 relative (the fp32 data's rounding
     carried through the loop), cost / AED numerator within TOL_CL32, failed solves and step counts
     exactly."""
     from drone_attitude_control_amd.batched import ClosedLoop
-    key = "force_N20_B8192"
+    key = f"{model}_N{N}_B{B}"
     sel = golden[f"{key}_sel"]
-    loop = ClosedLoop("force", 8192, N=20, seed=42, precision="fp32")
+    loop = ClosedLoop(model, B, N=N, seed=42, precision="fp32")
     info = loop.solver.launch_info()
     assert info["closed_loop_kernel"] == "cl_fast_kernel", info
     states, sums, parked = [], [], 0
@@ -137,7 +138,7 @@ def test_fp32_force_closed_loop_matches_oracle(golden):
     S, A = np.array(states), np.array(sums)
     Sg, Ag, Fg = golden[f"{key}_states"], golden[f"{key}_sums"], golden[f"{key}_failed"]
     err = _rel(S[:, sel], Sg)
-    print(f"fp32 force closed loop: max state err {err.max():.3e}, median {np.median(err):.3e}, parked {parked}; "
+    print(f"fp32 {key} closed loop: max state err {err.max():.3e}, median {np.median(err):.3e}, parked {parked}; "
           f"per region {np.array2string(err.max(1), precision=2)}")
     assert err.max() < TOL_CL32, (err.max(), sel[np.unravel_index(err.argmax(), err.shape)[1]])
     fails_region = np.diff(np.concatenate([np.zeros((1, len(sel))), A[:, sel, 2]]), axis=0)
