@@ -1900,6 +1900,8 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     // lockstep): quad13 B = 8192 415M (0) -> 458-463M (1), 452-457M (2), 405-412M (3) steps/s (tools/lock_ab.sh, ab1/ab2)
     // (the jerk shape's lockstep variant, four wavefronts per workgroup and rarely a demotion: none)
     p.lock_workers = lw ? std::max(0, std::min(4, std::atoi(lw))) : (h->nx == 6 && h->nu == 2 ? 0 : 1);
+    const char *lp = std::getenv("NMPC_LOCK_PRIO");
+    p.lock_prio = lp ? (lp[0] == '1') : 1;
     // the force shape claims its instances device-wide (env NMPC_CLF_GCLAIM=0 / 1 overrides)
     const char *gc = std::getenv("NMPC_CLF_GCLAIM");
     p.claim_global = gc ? (gc[0] == '1') : (h->nx == 4 && h->nu == 2);

@@ -1848,6 +1848,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 #endif
     }
     if (lane == 0) atomicAdd(&ph1_done, 1);
+    // phase 2 carries the launch's critical chains (an instance with an active-set step at most steps sets
+    // the launch time): its wavefronts issue ahead of the lockstep ones sharing their SIMD (env
+    // NMPC_LOCK_PRIO=0: equal priority)
+    if (p.lock_prio) __builtin_amdgcn_s_setprio(3);
 
     // ================= phase 2: the demoted instances, one at a time on the whole wavefront
     for (;;) {

@@ -109,6 +109,7 @@ struct ClFastParams {
     int polish_steps;             // active-set rounds of the fast path
     int gi;                       // 1: the dual active-set fallback runs; 0 (test knob): such steps park
     int lock_workers;             // lockstep kernel: wavefronts per workgroup that start in phase 2
+    int lock_prio;                // lockstep kernel: phase-2 wavefronts at raised issue priority
     int claim_global;             // cl_fast_kernel: instances from one device-wide counter (park_count[1])
     int x1_slot;                  // slot (lane, j = 0) of x_1[0] (cost of the jerk loop: cost_stage 1)
     const T *table;               // reference table [rows][table_cols]
