@@ -120,7 +120,9 @@ typedef struct nmpc_ocp_desc {
      * where the IPM multiplier exceeds the slack), then one refinement step; accepted when the
      * QP's KKT sign and bound conditions hold, else the IPM goes on and the next run waits for
      * mu to drop 100-fold. 0: 1 (first run at the start for the default mu0; fp64 handles only,
-     * fp32 handles never run it); < 0: off */
+     * fp32 handles never run it); < 0: off. fp32 handles instead end each solve in their own
+     * exact finish (the IPM's active bounds as the warm set of active-set steps on the fp64
+     * projected inverse Hessian, fp64 KKT acceptance; env NMPC_FIN32=0 off) */
     double qp_solver_polish_mu;
     int qp_solver_polish_steps; /* <= 0: 12 */
 } nmpc_ocp_desc;
@@ -227,7 +229,8 @@ typedef struct nmpc_closed_loop_desc {
 int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d);
 /* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion.
  * Paths (the same results on every one; the choice may change from run to run on one handle):
- *   - the lean loop (nmpc_cl_fast.hip; quad13 / jerk / force shapes, fp64, the default): launches of at
+ *   - the lean loop (nmpc_cl_fast.hip; quad13 / jerk / force shapes, fp64 and fp32 — fp32: fp32 tables
+ *     and explicit form, fp64 W, set solves and acceptance — the default): launches of at
  *     most 64 steps; after each launch the host reads the count of parked instances (a step the fast
  *     path could not solve) and runs their full solve in list mode. That read waits for the launch, so
  *     the lean loop returns only when its last launch is done, whatever `sync` says;
