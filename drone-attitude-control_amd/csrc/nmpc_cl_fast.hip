@@ -181,9 +181,9 @@ struct SlotView {
     template <typename T>
     __device__ double w(const ClFastParams<T> &p, int ea, int sa, int eb, int sb) const
     {
-        if (wl_) {
+        if (wl_) {   // (24-bit multiply: full rate, the 32-bit one is quarter rate)
             const int hi = sa > sb ? sa : sb, lo = sa > sb ? sb : sa;
-            return wt_[((hi * (hi + 1)) >> 1) + lo];
+            return wt_[(int)(__umul24((unsigned)hi, (unsigned)(hi + 1)) >> 1) + lo];
         }
         return p.W[(size_t)ea * p.ne + eb];
     }
