@@ -323,8 +323,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "fp64" else "f32",
             "dtype_note": None if args.precision == "fp64" or not lean else
-            "fp32 handle on the lean loop: fp32 storage (tables, W, state, trajectories), explicit form and fast-path "
-            "bound tests in fp32; active-set solves, W[:, S] nu combinations and KKT acceptance in fp64",
+            "fp32 handle on the lean loop: fp32 storage (explicit-form tables, bounds, state, trajectories), explicit "
+            "form and fast-path bound tests in fp32; W kept in fp64, and active-set solves, W[:, S] nu combinations, "
+            "set targets and KKT acceptance in fp64",
             "data": "synthetic (seeded closed-loop Monte-Carlo instances on the reference circle)",
             "config": {"workload": workload_label(model, tols, cpu and cpu.get("paths_per_step")),
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,

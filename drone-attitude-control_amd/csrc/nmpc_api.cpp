@@ -1778,7 +1778,7 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
               hipMalloc((void **)&h->d_fsI, itot * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_istep, (size_t)h->batch * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_park, (size_t)(h->batch + 2) * sizeof(int)) == hipSuccess &&
-              hipMalloc((void **)&h->d_flags, (size_t)h->batch * nslot) == hipSuccess;
+              hipMalloc((void **)&h->d_flags, (size_t)h->batch * (nslot + 1)) == hipSuccess;   // + the order bytes
     if (ok && fk != h->kidx)
         ok = hipMalloc(&h->d_clf_scratch, (f64 ? nmpc::ipm_scratch_elems<double>(fk, h->batch, N)
                                                 : nmpc::ipm_scratch_elems<float>(fk, h->batch, N)) * es) == hipSuccess;
@@ -1794,7 +1794,7 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         if (!ip[i]->empty())
             e = hipMemcpy(h->d_fsI + h->fsi[i], ip[i]->data(), ip[i]->size() * sizeof(int), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(h->d_istep, 0, (size_t)h->batch * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * nslot);
+    if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * (nslot + 1));
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_init lean tables");
     // the lockstep kernel for the shapes that have one, with the controller-model plant and the cost on x_0
     // (env NMPC_CLF_LOCK=0: the one-instance-per-wavefront kernel)
@@ -1905,6 +1905,11 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     // the force shape claims its instances device-wide (env NMPC_CLF_GCLAIM=0 / 1 overrides)
     const char *gc = std::getenv("NMPC_CLF_GCLAIM");
     p.claim_global = gc ? (gc[0] == '1') : (h->nx == 4 && h->nu == 2);
+    // the instances demoted (lockstep) or on the rare path (cl_fast_kernel) in the previous launch claimed first
+    // (their chains start at the launch's beginning; env NMPC_CLF_ORDER=0: instance order)
+    const char *lo = std::getenv("NMPC_CLF_ORDER");
+    p.demoted = (lo && lo[0] == '0') ? nullptr : (unsigned char *)h->d_flags + (size_t)h->batch * h->clf_nslot;
+    p.order_buckets = (lo && lo[0] == '2') ? 1 : 0;
     return p;
 }
 

@@ -1073,6 +1073,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
     double cost = 0.0, aed = 0.0;   // this lane's terms (component lane), summed over the wave at the end
     int nfail = 0, nst = 0;
     int last_status = step > 0 ? st_prev : 0, last_iters = 0;
+    int nslow = 0;          // rare-path steps of this launch (the next launch claims such instances first)
     bool last_gi = false;   // the previous step of this launch ran the dual fallback
     bool parked = false;
     // v_t at the slots one step ahead (the step's first dependency); the reference component and the
@@ -1128,6 +1129,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
         CLF_TCNT(L, 13, 1);
         if (!ok) {
             CLF_TCNT(L, 12, 1);
+            nslow++;
             const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, wf, last_status == 4, gi_prev);
             status = sr & 0xff;
             last_gi = (sr >> 9) & 1;
@@ -1192,6 +1194,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
         unsafeAtomicAdd(p.acc + (size_t)inst * 4 + lane, lane == 0 ? cost : lane == 1 ? aed : lane == 2 ? (double)nfail : (double)nst);
     if (lane == 0) {
         p.istep[inst] = step;
+        if (p.demoted) p.demoted[inst] = (unsigned char)(nslow < 255 ? nslow : 255);
         if (parked) {
             const int pos = atomicAdd(p.park_count, 1);
             p.park_list[pos] = inst;
@@ -1218,6 +1221,31 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
     if (lane < CLF_NT) L.tacc[lane] = 0;
 #endif
     CLF_SYNC();   // L.xs / L.fl of this instance are read before the next one overwrites them
+}
+
+constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host checks B / grid <= LOCK_QCAP)
+
+// A workgroup's claim order over its range [lo, lo + cnt) (cnt <= 65536), by one wavefront, longest
+// first: `hard` holds each instance's rare-path steps in the previous launch (capped at 255); with
+// buckets = 0 the instances with any come first, otherwise in the groups >= 8, 4-7, 2-3, 1; then the
+// rest. Instance order within a group (hard null: instance order)
+__device__ inline void claim_order(unsigned short *ord, const unsigned char *hard, int lo, int cnt, int lane, int buckets)
+{
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int nb = hard ? (buckets ? 5 : 2) : 1;
+    int pos = 0;
+    for (int b = 0; b < nb; b++) {
+        // group b: [mn, mx] of the byte
+        const int mn = nb == 1 ? 0 : (b == nb - 1 ? 0 : (nb == 2 ? 1 : (8 >> b))), mx = nb == 1 ? 255 : (b == nb - 1 ? 0 : (b == 0 ? 255 : (16 >> b) - 1));
+        for (int c = 0; c < cnt; c += 64) {
+            const bool in = c + lane < cnt;
+            const int h = in && hard ? (int)hard[lo + c + lane] : 0;
+            const bool d = in && h >= mn && h <= mx;
+            const unsigned long long m = __ballot(d);
+            if (d) ord[pos + __popcll(m & lt)] = (unsigned short)(c + lane);
+            pos += __popcll(m);
+        }
+    }
 }
 
 // WPB wavefronts per workgroup (the slot tables in LDS are shared by them), MW the occupancy target
@@ -1276,6 +1304,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         }
     }
     __shared__ int wg_next;   // the workgroup's next instance (offset into its range)
+    __shared__ unsigned short ord[LOCK_QCAP];   // claim order (offsets into the workgroup's range)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
     if (lane < 32) L.xs[lane] = 0.0;
@@ -1283,6 +1312,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     if (lane < CLF_NT) L.tacc[lane] = 0;
 #endif
     if (threadIdx.x == 0) wg_next = 0;
+    const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int wg_lo = p.claim_global ? 0 : (int)blockIdx.x * per_wg, wg_hi = p.claim_global ? p.B : min(p.B, wg_lo + per_wg);
+    // the previous launch's rare-path instances first (longest first: the workgroup's makespan), when the
+    // range fits the order table
+    const bool ordered = !p.claim_global && p.demoted && wg_hi - wg_lo <= LOCK_QCAP;
+    if (ordered && wave == 0) claim_order(ord, p.demoted, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane, wtri, WL};
 
@@ -1298,13 +1333,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // B = 8192 -6 % (less balancing across workgroups), quad13 unchanged (r4e / r4f)
     // (p.claim_global: one device-wide counter instead, p.park_count[1] — the force shape, whose instances'
     // costs vary most, balances across workgroups)
-    const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int wg_lo = p.claim_global ? 0 : (int)blockIdx.x * per_wg, wg_hi = p.claim_global ? p.B : min(p.B, wg_lo + per_wg);
     for (;;) {
         int next = 0;
         if (lane == 0) next = p.claim_global ? atomicAdd(p.park_count + 1, 1) : atomicAdd(&wg_next, 1);
-        const int inst = wg_lo + __builtin_amdgcn_readfirstlane(next);
-        if (inst >= wg_hi) break;
+        next = __builtin_amdgcn_readfirstlane(next);
+        if (wg_lo + next >= wg_hi) break;
+        const int inst = wg_lo + (ordered ? (int)ord[next] : next);
         // explicit unconstrained solution at the lane's slots: T_x pairs from LDS against x pairs broadcast
         run_instance<T, NX, NU, EPL, WSM, SP>(p, L, sv, lane, abl, cl, inst, [&](T(&z)[EPL], const T(&vt)[EPL]) {
             T z1[EPL];
@@ -1479,7 +1513,6 @@ __global__ __launch_bounds__(64 * WPB) void fin32_kernel(ClFastParams<float> p)
 // and the queue is empty (all of a workgroup's wavefronts are co-resident: the wait always ends).
 // Same decisions, thresholds and outputs as cl_fast_kernel (oracle/c/riccati_ipm.c mode 1); only the
 // summation order of the explicit form and the plant differs (rounding).
-constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host checks B / grid <= LOCK_QCAP)
 
 template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0 ? MW : 1, MW > 0 ? MW : 8))) void cl_lock_kernel(ClFastParams<T> p)
@@ -1494,6 +1527,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     __shared__ double txA[NT][KC][64];                  // T_x in A-operand order
     __shared__ double2 lohi[NSLOT], onb[NSLOT];         // (lo, hi) violation / (onl, onu) on-bound thresholds
     __shared__ int dq[LOCK_QCAP];                       // demoted instances (-1: slot not yet written)
+    __shared__ unsigned short ord[LOCK_QCAP];           // claim order (offsets into the workgroup's range)
     __shared__ int wg_next, dq_tail, dq_head, ph1_done;
     for (int e = threadIdx.x; e < NT * KC * 64; e += 64 * WPB) {
         const int t = e / (KC * 64), kc = (e / 64) % KC, l = e % 64;
@@ -1530,15 +1564,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     if (lane < CLF_NT) L.tacc[lane] = 0;
 #endif
     if (threadIdx.x == 0) wg_next = dq_tail = dq_head = ph1_done = 0;
+    // the workgroup's contiguous instance range (persistent grid)
+    const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int wg_lo = (int)blockIdx.x * per_wg, wg_hi = min(p.B, wg_lo + per_wg);
+    // claim order: the instances the previous launch demoted first (the launch's longest chains start at its
+    // beginning, not behind the lockstep ones), then the rest, each group in instance order. Only the
+    // schedule changes: an instance runs lockstep until its first rare step wherever it is claimed
+    if (wave == 0) claim_order(ord, p.demoted, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
     const int n = lane & 3, ti = lane >> 4, tb = (lane >> 2) & 3;   // instance slot; D-layout slot offset
     const int prow = lane & 15, drow = 4 * tb + ti;                 // plant A-operand row; D row
     auto slot_of = [&](int q) { return 16 * q + 4 * tb + ti; };
-
-    // the workgroup's contiguous instance range (persistent grid)
-    const int per_wg = (p.B + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int wg_lo = (int)blockIdx.x * per_wg, wg_hi = min(p.B, wg_lo + per_wg);
 
     // ================= phase 1: lockstep (the workgroup's last p.lock_workers wavefronts start as phase-2
     // workers, so the queued chains start at once: env NMPC_LOCK_WORKERS, default 1)
@@ -1566,8 +1603,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             if (lane < 4 && want) nx_ = atomicAdd(&wg_next, 1);
             nx_ = __shfl(nx_, n);
             if (!want) return;
-            const int ni = wg_lo + nx_;
-            inst = ni < wg_hi ? ni : -1;
+            inst = nx_ < wg_hi - wg_lo ? wg_lo + (int)ord[nx_] : -1;
             flany = false;
             cost = aed = 0.0;
             nfail = nst = 0;
@@ -1619,6 +1655,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 }
                 p.istep[inst] = step;
                 p.status[inst] = last_status;
+                if (p.demoted) p.demoted[inst] = demote ? 1 : 0;
                 if (!demote) p.iters[inst] = 1;
                 if (p.iter_log && !demote) {
                     p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(inst_t0 & 0x7fffffff);
