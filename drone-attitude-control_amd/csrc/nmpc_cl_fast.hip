@@ -1186,6 +1186,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
     }
     // ---- write back: state, sums, step, flags, status
     CLF_T(tb0);
+    const bool fl_end = __any(fl != 0u);   // the next launch's first step starts from a nonempty warm set
     cost = wave_sum(cost);
     aed = wave_sum(aed);
     if (lane < NX) p.state[(size_t)inst * NX + lane] = (T)xl;
@@ -1194,7 +1195,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
         unsafeAtomicAdd(p.acc + (size_t)inst * 4 + lane, lane == 0 ? cost : lane == 1 ? aed : lane == 2 ? (double)nfail : (double)nst);
     if (lane == 0) {
         p.istep[inst] = step;
-        if (p.demoted) p.demoted[inst] = (unsigned char)(nslow < 255 ? nslow : 255);
+        if (p.demoted) p.demoted[inst] = (unsigned char)((nslow < 127 ? nslow : 127) | (fl_end ? 128 : 0));
         if (parked) {
             const int pos = atomicAdd(p.park_count, 1);
             p.park_list[pos] = inst;
@@ -1226,17 +1227,19 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
 constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host checks B / grid <= LOCK_QCAP)
 
 // A workgroup's claim order over its range [lo, lo + cnt) (cnt <= 65536), by one wavefront, longest
-// first: `hard` holds each instance's rare-path steps in the previous launch (capped at 255); with
-// buckets = 0 the instances with any come first, otherwise in the groups >= 8, 4-7, 2-3, 1; then the
-// rest. Instance order within a group (hard null: instance order)
+// first. `hard` holds one byte per instance from the previous launch: bit 7 = its last solution left
+// bounds active (a nonempty warm start: its first step takes the rare path), bits 0-6 = its rare-path
+// steps (capped). Groups: bit 7 set, then any rare-path steps, then the rest (buckets = 1: each of the
+// first two split by the rare-path steps, >= 8 / 1-7 / 0 and >= 8 / 1-7); instance order within a group
+// (hard null: instance order)
 __device__ inline void claim_order(unsigned short *ord, const unsigned char *hard, int lo, int cnt, int lane, int buckets)
 {
     const unsigned long long lt = (1ull << lane) - 1ull;
-    const int nb = hard ? (buckets ? 5 : 2) : 1;
+    constexpr int MN[2][6] = {{128, 1, 0, 0, 0, 0}, {136, 129, 128, 8, 1, 0}}, MX[2][6] = {{255, 127, 0, 0, 0, 0}, {255, 135, 128, 127, 7, 0}};
+    const int nb = hard ? (buckets ? 6 : 3) : 1;
     int pos = 0;
     for (int b = 0; b < nb; b++) {
-        // group b: [mn, mx] of the byte
-        const int mn = nb == 1 ? 0 : (b == nb - 1 ? 0 : (nb == 2 ? 1 : (8 >> b))), mx = nb == 1 ? 255 : (b == nb - 1 ? 0 : (b == 0 ? 255 : (16 >> b) - 1));
+        const int mn = nb == 1 ? 0 : MN[buckets ? 1 : 0][b], mx = nb == 1 ? 255 : MX[buckets ? 1 : 0][b];
         for (int c = 0; c < cnt; c += 64) {
             const bool in = c + lane < cnt;
             const int h = in && hard ? (int)hard[lo + c + lane] : 0;
@@ -1655,7 +1658,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 }
                 p.istep[inst] = step;
                 p.status[inst] = last_status;
-                if (p.demoted) p.demoted[inst] = demote ? 1 : 0;
+                if (p.demoted) p.demoted[inst] = demote ? 1 : (flany ? 128 : 0);
                 if (!demote) p.iters[inst] = 1;
                 if (p.iter_log && !demote) {
                     p.iter_log[(size_t)(p.target - p.step0) * p.B + inst] = (int)(inst_t0 & 0x7fffffff);

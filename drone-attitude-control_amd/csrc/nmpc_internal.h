@@ -111,8 +111,9 @@ struct ClFastParams {
     int lock_workers;             // lockstep kernel: wavefronts per workgroup that start in phase 2
     int lock_prio;                // lockstep kernel: phase-2 wavefronts at raised issue priority
     int claim_global;             // cl_fast_kernel: instances from one device-wide counter (park_count[1])
-    unsigned char *demoted;       // [B] the previous launch's rare-path steps (lockstep: 1 at demotion), or null
-    int order_buckets;            // claim order: 0 rare-path instances first; 1 longest first in four groups
+    unsigned char *demoted;       // [B] the previous launch's rare-path steps | 128 if its last solution left bounds
+                                  // active (lockstep: 1 at demotion), or null: the claim order's key
+    int order_buckets;            // claim order: 0 three groups (warm start, rare path, rest); 1 six
     int x1_slot;                  // slot (lane, j = 0) of x_1[0] (cost of the jerk loop: cost_stage 1)
     const T *table;               // reference table [rows][table_cols]
     const int *offset;            // [B]
