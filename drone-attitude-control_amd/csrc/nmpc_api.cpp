@@ -253,6 +253,7 @@ struct nmpc_solver {
     int *d_iter_log = nullptr;    // fused closed loop, env NMPC_ITER_LOG: per-step finish steps | IPM iterations << 8 | status << 16 [64][B]
     int iter_log_steps = 0;       // steps in the log (the last fused launch; the lean loop: the last run)
     size_t iter_log_cap = 0;      // capacity of d_iter_log (ints)
+    int *h_park = nullptr;        // pinned host word: the lean loop's parked count per round
     std::vector<hipEvent_t> cl_events;
     double cl_last_ms = 0.0;
     double cost_s = 1.0;  // stage cost factor (time step or 1)
@@ -510,6 +511,7 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0})
         if (p) hipFree(p);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
+    if (h->h_park) hipHostFree(h->h_park);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
@@ -1956,6 +1958,11 @@ int clf_run(nmpc_solver *h, int steps)
             if (hipMalloc((void **)&h->d_iter_log, cap * sizeof(int)) == hipSuccess) h->iter_log_cap = cap;
         }
     }
+    // the parked count comes back through a pinned word (a pageable destination is a staged copy)
+    if (!h->h_park && hipHostMalloc((void **)&h->h_park, 4 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        h->h_park = nullptr;
+        return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: pinned park word");
+    }
     int launches = 0;
     h->clf_parked = h->clf_rounds = 0;
     // env NMPC_CLF_CYCLES=<file> with a timing build (-DNMPC_CLF_TIMING): per-instance phase cycles of the
@@ -1967,7 +1974,8 @@ int clf_run(nmpc_solver *h, int steps)
     for (int done = 0; done < steps;) {
         const int n = std::min(CLF_CHUNK, steps - done), target = h->cl_step + n;
         nmpc::ClParams<T> cp = cl_params<T>(h);
-        hipError_t e = nmpc::cl_noise_launch<T>(cp, h->cl_step, n, h->d_fnoise, h->stream);
+        // (the noise kernel also zeroes the park count and claim counter of the chunk's first round)
+        hipError_t e = nmpc::cl_noise_launch<T>(cp, h->cl_step, n, h->d_fnoise, h->stream, h->d_park);
         if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
         nmpc::ClFastParams<T> fp = clf_params<T>(h, target, h->cl_step, n);
         fp.cycles = d_cyc;
@@ -1979,17 +1987,18 @@ int clf_run(nmpc_solver *h, int steps)
             h->iter_log_steps = n + 2;   // + the instance start / end rows
         }
         for (int round = 0; round <= n; round++) {
-            if ((e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess) return hip_fail(h, e, "park reset");
+            if (round > 0 && (e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess)
+                return hip_fail(h, e, "park reset");
             hipEventRecord(cl_event(h, 2 * launches), h->stream);
             e = nmpc::cl_fast_launch<T>(h->nx, h->nu, h->clf_sid, h->clf_kind, fp, h->batch, h->clf_resident, h->stream);
             hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
             launches++;
             h->clf_rounds++;
             if (e != hipSuccess) return hip_fail(h, e, "lean closed-loop kernel launch");
-            int parked = 0;
-            e = hipMemcpyAsync(&parked, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+            e = hipMemcpyAsync(h->h_park, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
             if (e != hipSuccess) return hip_fail(h, e, "lean closed loop (fast kernel)");
+            const int parked = h->h_park[0];
             if (dbg) std::fprintf(stderr, "[nmpc clf] steps %d..%d round %d: %d parked\n", h->cl_step, target, round, parked);
             if (parked <= 0) break;
             h->clf_parked += parked;

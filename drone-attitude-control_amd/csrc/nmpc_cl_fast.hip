@@ -835,7 +835,18 @@ __device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, const 
     double a[NX];
 #pragma unroll
     for (int j = 0; j < NX; j++) a[j] = abl[i * NZ + j];
-    bool infeas = false;
+    // the stage-invariant operands ahead of the stage chain (the same arithmetic, in the same order): the
+    // input box's midpoint and radius terms, the state bounds of the inner stages and of the last one
+    double bu[NU], bm[NU], br[NU];
+#pragma unroll
+    for (int j = 0; j < NU; j++) {
+        const double l = p.lbnd[NX + j], h = p.ubnd[NX + j];
+        const bool bb = has_b(l) && has_b(h);
+        bu[j] = abl[i * NZ + NX + j];
+        bm[j] = bb ? 0.5 * (l + h) : 0.0;
+        br[j] = bb ? 0.5 * (h - l) : (double)INFINITY;
+    }
+    const double lb1 = p.lbnd[NZ + i], ub1 = p.ubnd[NZ + i], lb2 = p.lbnd[2 * NZ + i], ub2 = p.ubnd[2 * NZ + i];
     for (int k = 0; k < p.N; k++) {
         double s = cl[i], tr = 0.0;
 #pragma unroll
@@ -846,22 +857,22 @@ __device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, const 
         }
 #pragma unroll
         for (int j = 0; j < NU; j++) {
-            const double b = abl[i * NZ + NX + j], l = p.lbnd[NX + j], h = p.ubnd[NX + j];
-            const bool bb = has_b(l) && has_b(h);
-            s = fma(b, bb ? 0.5 * (l + h) : 0.0, s);
-            if (b != 0.0) tr = fma(fabs(b), bb ? 0.5 * (h - l) : (double)INFINITY, tr);
+            s = fma(bu[j], bm[j], s);
+            if (bu[j] != 0.0) tr = fma(fabs(bu[j]), br[j], tr);
         }
-        const int ty = k + 1 == p.N ? 2 : 1;
-        const double lb = p.lbnd[ty * NZ + i], ub = p.ubnd[ty * NZ + i];
+        const bool last = k + 1 == p.N;
+        const double lb = last ? lb2 : lb1, ub = last ? ub2 : ub1;
         double lo = s - tr, hi = s + tr;
         if (has_b(lb) && lb > lo) lo = lb;
         if (has_b(ub) && ub < hi) hi = ub;
-        infeas |= lane < NX && lo > hi + 1e-9 * (1.0 + fabs(hi));
+        // the first empty intersection proves it (the oracle's first infeasible stage): the remaining
+        // stages of the chain are not run
+        if (__any(lane < NX && lo > hi + 1e-9 * (1.0 + fabs(hi)))) return true;
         const bool fin = isfinite(lo) && isfinite(hi);
         m = fin ? 0.5 * (lo + hi) : s;
         r = fin ? 0.5 * (hi - lo) : tr;
     }
-    return __any(infeas);
+    return false;
 }
 
 // plant step + noise, lane-distributed: lane i < NX returns x_i after the step (nmpc_cl_device.h

@@ -63,8 +63,10 @@ __global__ __launch_bounds__(256) void cl_model_advance_kernel(ClParams<T> p)
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void cl_noise_kernel(ClParams<T> p, int step0, int nsteps, double *out)
+__global__ __launch_bounds__(256) void cl_noise_kernel(ClParams<T> p, int step0, int nsteps, double *out, int *zero2)
 {
+    // (zero2: two counters of the next kernel reset here, one stream operation fewer than a memset)
+    if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
     const size_t total = (size_t)p.B * nsteps;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
          idx += (size_t)gridDim.x * blockDim.x) {
@@ -80,11 +82,11 @@ __global__ __launch_bounds__(256) void cl_noise_kernel(ClParams<T> p, int step0,
 }
 
 template <typename T>
-hipError_t cl_noise_launch(const ClParams<T> &p, int step0, int nsteps, double *out, hipStream_t s)
+hipError_t cl_noise_launch(const ClParams<T> &p, int step0, int nsteps, double *out, hipStream_t s, int *zero2)
 {
     const size_t total = (size_t)p.B * nsteps;
-    const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(cl_noise_kernel<T>, dim3(blocks), dim3(256), 0, s, p, step0, nsteps, out);
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>((total + 255) / 256, 4096));
+    hipLaunchKernelGGL(cl_noise_kernel<T>, dim3(blocks), dim3(256), 0, s, p, step0, nsteps, out, zero2);
     return hipGetLastError();
 }
 
@@ -112,7 +114,7 @@ template hipError_t cl_prepare_launch<double>(const ClParams<double> &, hipStrea
 template hipError_t cl_prepare_launch<float>(const ClParams<float> &, hipStream_t);
 template hipError_t cl_advance_launch<double>(const ClParams<double> &, hipStream_t);
 template hipError_t cl_advance_launch<float>(const ClParams<float> &, hipStream_t);
-template hipError_t cl_noise_launch<double>(const ClParams<double> &, int, int, double *, hipStream_t);
-template hipError_t cl_noise_launch<float>(const ClParams<float> &, int, int, double *, hipStream_t);
+template hipError_t cl_noise_launch<double>(const ClParams<double> &, int, int, double *, hipStream_t, int *);
+template hipError_t cl_noise_launch<float>(const ClParams<float> &, int, int, double *, hipStream_t, int *);
 
 }  // namespace nmpc

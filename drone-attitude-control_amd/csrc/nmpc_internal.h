@@ -254,7 +254,7 @@ hipError_t cl_prepare_launch(const ClParams<T> &p, hipStream_t s);
 // noise draws of steps [step0, step0 + nsteps) for every instance: out[b][s] (cl_advance_instance's
 // draw: the user table if given, else Philox / Box-Muller, else 0)
 template <typename T>
-hipError_t cl_noise_launch(const ClParams<T> &p, int step0, int nsteps, double *out, hipStream_t s);
+hipError_t cl_noise_launch(const ClParams<T> &p, int step0, int nsteps, double *out, hipStream_t s, int *zero2 = nullptr);
 template <typename T>
 hipError_t cl_advance_launch(const ClParams<T> &p, hipStream_t s);
 
