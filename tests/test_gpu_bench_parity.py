@@ -111,6 +111,33 @@ def test_jerk_lockstep_variant_matches_oracle():
     np.testing.assert_allclose(acc[:, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("model,N,B", [("quad13", 20, 4096), ("jerk", 40, 2048)])
+def test_claim_order_changes_only_the_schedule(model, N, B):
+    """The lean loop's claim order (NMPC_CLF_ORDER, read per run: the previous launch's warm-start and
+    rare-path instances first; nmpc_cl_fast.hip claim_order) moves instances between wavefronts and
+    rounds, never between paths: each instance runs lockstep (quad13: cl_lock_kernel) until its first
+    rare step, or whole on one wavefront (jerk: cl_fast_kernel), whatever its place in the order. Five
+    launches in each order from the same workload: states and per-instance sums bit for bit."""
+    from drone_attitude_control_amd.batched import ClosedLoop
+    out = []
+    for order in ("0", "1"):
+        os.environ["NMPC_CLF_ORDER"] = order
+        try:
+            cl = ClosedLoop(model, B, N=N, seed=11)
+            kernel = cl.solver.launch_info()["closed_loop_kernel"]
+            assert kernel == ("cl_lock_kernel" if model == "quad13" else "cl_fast_kernel")
+            for n in (3, 20, 20, 20, 20):
+                cl.run(n)
+            out.append((cl.state(), cl.instance_stats(), cl.stats()["parked"]))
+        finally:
+            os.environ.pop("NMPC_CLF_ORDER", None)
+    (x0, a0, p0), (x1, a1, p1) = out
+    assert np.array_equal(x0, x1), np.abs(x0 - x1).max()
+    assert np.array_equal(a0, a1), np.abs(a0 - a1).max()
+    assert p0 == p1
+
+
 TOL_CL32 = 1e-5        # fp32 lean loop, force (BASELINE config 3), DESIGN.md §6 (measured 1.4e-6)
 TOL_CL32_LOOP = 1e-3   # fp32 lean loop, quad13 / jerk: a few loop-sensitive instances (measured 2.6e-4 / 5.2e-4)
 
