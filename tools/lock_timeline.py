@@ -5,8 +5,10 @@ what the latest-finishing ones ran.
     python tools/lock_timeline.py --model quad13 --batch 8192 --steps 20
 
 The log's last two rows hold each instance's start and end in the launch (wall_clock64 ticks, 100 MHz,
-low 31 bits); the step rows hold the steps run by run_instance (the lockstep kernel's phase 2 or
-cl_fast_kernel): active-set steps, status and the step's ticks. One JSON line."""
+low 31 bits); the step rows hold every step's record: 1 + its active-set steps, status and ticks
+(lockstep steps record 1 and their ticks, so `slow_steps` counts the rare-path steps, which only
+run_instance takes). The per-workgroup figures assume --per-wg instances per workgroup (quad13 B=8192:
+32; jerk B=4096: 16). One JSON line."""
 import argparse
 import json
 import os
@@ -47,7 +49,7 @@ def main():
     start, end = raw[steps], raw[steps + 1]
     t0 = start.min()
     s_us, e_us = (start - t0) * TICK_US, (end - t0) * TICK_US
-    tick = c[:steps].astype(np.int64)            # per-step ticks of run_instance steps (0: not logged)
+    tick = c[:steps].astype(np.int64)            # per-step ticks (0: not logged)
     act = a[:steps].astype(np.int64)
     ph2 = (tick > 0).any(axis=0)
     n2 = (tick > 0).sum(axis=0)
