@@ -198,7 +198,9 @@ def init_dist(args):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = local_rank
-    if world > 1:
+    # a process group whenever torch.distributed.run launched us (RANK in the environment), also at
+    # world size 1: the RCCL reduction of the statistics then runs on a real communicator
+    if world > 1 or "RANK" in os.environ:
         # torch first: its HIP runtime (soname libamdhip64.so.7) is then shared by libnmpc_hip
         import torch
         import torch.distributed as dist
@@ -211,6 +213,15 @@ def init_dist(args):
     return world, rank, dist, device
 
 
+def parallelism_label(dist, world):
+    """config.parallelism: the sharding and the backend of the process group that reduced the statistics
+    (dist.get_backend() of the live group: "nccl" is RCCL on ROCm)."""
+    if dist is None:
+        return f"instance-sharded x{world}, single process (no collective)"
+    be = dist.get_backend()
+    return f"instance-sharded x{world}, {'RCCL' if be == 'nccl' else be} stats reduce ({be} process group)"
+
+
 def timing_block(regions, elapsed, note):
     return {"regions": len(regions), "value_from": "median region",
             "region_ms": [round(float(r) * 1e3, 4) for r in regions],
@@ -219,15 +230,20 @@ def timing_block(regions, elapsed, note):
             "note": note}
 
 
-def workload_label(model, tols, paths):
-    """config.workload: what the timed step runs, with the path mix of the CPU run of the same
-    algorithm over the same steps (None on multi-rank runs, which skip the CPU baseline)."""
+def workload_label(model, tols, paths, kernel):
+    """config.workload: what the timed step runs (`kernel`: the closed-loop kernel launch_info reports),
+    with the path mix of the CPU run of the same algorithm over the same steps (None on multi-rank runs,
+    which skip the CPU baseline)."""
     mix = ("path mix not measured in this run (the CPU baseline, which counts it, runs at N=1 only)" if paths is None
            else f"of the solves {paths['fast_unconstrained']:.2%} the explicit unconstrained solution, "
                 f"{paths['fast_set']:.2%} warm-started active-set steps on W (incl. the dual active-set fallback), "
                 f"{paths['full']:.3%} the full IPM + exact finish, {paths['failed']:.3%} certified infeasible "
                 f"(status 4) — counted by the CPU run of the same algorithm over the timed steps")
-    return (f"{model} closed-loop NMPC step on the lean loop (cl_fast_kernel): yref window from the shared "
+    what = {"cl_lock_kernel": "the lockstep lean loop (cl_lock_kernel: 4 instances per wavefront on the f64 matrix "
+                              "cores, demoted instances on the single-instance path)",
+            "cl_fast_kernel": "the lean loop (cl_fast_kernel: one wavefront per instance)"}.get(
+        kernel, f"the fused closed loop ({kernel})")
+    return (f"{model} closed-loop NMPC step on {what}: yref window from the shared "
             f"reference table + x0 pin + the QP solved to its exact, KKT-checked solution ({mix}; "
             f"full-solve options tol_comp {tols[0]:g}, tol_res {tols[1]:g}) + plant/noise advance + cost/AED")
 
@@ -327,11 +343,12 @@ def main():
             "form and fast-path bound tests in fp32; W kept in fp64, and active-set solves, W[:, S] nu combinations, "
             "set targets and KKT acceptance in fp64",
             "data": "synthetic (seeded closed-loop Monte-Carlo instances on the reference circle)",
-            "config": {"workload": workload_label(model, tols, cpu and cpu.get("paths_per_step")),
+            "config": {"workload": workload_label(model, tols, cpu and cpu.get("paths_per_step"), kernel),
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B,
-                       "global_batch": B * world, "parallelism": f"instance-sharded x{world}, "
-                                                                    f"{'gloo' if args.dist_backend == 'gloo' else 'RCCL'} stats reduce",
-                       "instances_per_wave": info["instances_per_wave"], "steps_per_launch": spl},
+                       "global_batch": B * world, "parallelism": parallelism_label(dist, world),
+                       "instances_per_wave": {"cl_lock_kernel": 4, "cl_fast_kernel": 1}.get(
+                           kernel, info["instances_per_wave"]),
+                       "steps_per_launch": spl},
             "timing": dict(timing_block(regions, elapsed, "each region is one closed-loop launch of --steps steps whose "
                                                           "time is set by its slowest wavefront; region-to-region "
                                                           "differences below the IQR are not resolved"),
@@ -473,7 +490,7 @@ def main_solve(args, world, rank, dist, device):
                                    f"stage-stacked yref window and x0 resident in HBM; full Mehrotra IPM + exact "
                                    f"active-set finish, no shared table, no warm start ({info['kernel']})",
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"instance-sharded x{world}", "instances_per_wave": info["instances_per_wave"]},
+                       "parallelism": parallelism_label(dist, world), "instances_per_wave": info["instances_per_wave"]},
             "timing": dict(timing_block(regions, elapsed, "each region enqueues --steps batched solves back to back"),
                            steps_per_region=args.steps),
             "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32", "kernel": info["kernel"],

@@ -26,12 +26,14 @@ def _port():
     return p
 
 
-def _bench(args, world, **env_extra):
+def _bench(args, world, backend="gloo", launcher=None, **env_extra):
+    """bench.py as one process (world 1, no launcher) or under torch.distributed.run with `world`
+    ranks and the given process-group backend."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
-    if world > 1:
+    if world > 1 or launcher == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
-               *args, "--dist-backend", "gloo"]
+               *args, "--dist-backend", backend]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **env_extra)
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -78,3 +80,20 @@ def test_config4_eight_ranks_reduce_equals_one_process():
     assert a["failed_solves"] == b["failed_solves"]
     assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=1e-10)
     assert a["aed"] == pytest.approx(b["aed"], rel=1e-10)
+
+
+@pytest.mark.timeout(300)
+def test_rccl_reduce_on_one_gpu_equals_no_dist():
+    """The RCCL leg of BASELINE config 4 on the one-GPU box: bench.py under torch.distributed.run with
+    one rank and the "nccl" backend (RCCL on ROCm) initialises a real communicator before any GPU call
+    of libnmpc_hip, runs the closed loop in that process and reduces the statistics with all_reduce on
+    device tensors (sharding.reduce_run). The reduced cost / AED / failure / step statistics equal a
+    run without any process group bit for bit (one rank: the reduction is the identity)."""
+    common = ["--model", "force", "--batch", "4096", "--steps", "4", "--warmup", "2", "--repeats", "2",
+              "--no-cpu-baseline"]
+    rccl = _bench(common, 1, backend="nccl", launcher="torchrun")
+    plain = _bench(common, 1)
+    assert rccl["config"]["parallelism"] == "instance-sharded x1, RCCL stats reduce (nccl process group)"
+    assert plain["config"]["parallelism"] == "instance-sharded x1, single process (no collective)"
+    assert rccl["closed_loop"] == plain["closed_loop"]
+    assert rccl["closed_loop"]["instance_steps"] == 4096 * (2 + 2 * 4)

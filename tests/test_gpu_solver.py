@@ -268,6 +268,35 @@ def test_bench_size_batch_matches_certified_sample(name, N, B, precision, golden
     assert e.max() < (TOL64 if precision == "fp64" else TOL32), e.max()
 
 
+def test_force_acados_recorded_states_batch(golden_dir):
+    """The 239 force steps acados recorded (experiment_data/img/example_acc_trajectory_component.pdf,
+    tests/golden/reference_plots.npz), each QP posed from acados's own plotted state with the window at
+    its sample (src/force_model/ocp.py:117-122, controller.py:29-32), solved as one GPU batch: x/u match
+    the oracle's certified exact solutions to 1e-6. tests/test_reference_plots.py shows that acados's u0
+    at each of these steps is an interior point of the same QP with complementarity <= 1e-6, so the
+    engine returns, step by step, the exact solution of the QP acados solved."""
+    from oracle import acados_termination as AT
+    plots = np.load(os.path.join(golden_dir, "reference_plots.npz"))
+    ref = np.load(os.path.join(golden_dir, "circle_ref.npz"))["nh30_nx6"]
+    spec = models.force_model(30)
+    X0, Y, Xr, Ur = [], [], [], []
+    for t, x, _ in AT.force_recorded_steps(plots):
+        y, ye = qp.yref_window(ref[:, :4], ref[:, 4:6], t, 30)
+        m = AT.StepModel(spec, x, y, ye)
+        X0.append(x)
+        Y.append(np.concatenate([y.ravel(), ye]))
+        Xr.append(m.Q.states(m.U))
+        Ur.append(m.U.reshape(30, 2))
+    assert len(X0) == 239
+    s = AcadosOcpSolver(OCPS["force"](30), batch=len(X0))
+    s.set_batch("x0", np.array(X0))
+    s.set_batch("yref", np.array(Y))
+    assert s.solve() == 0
+    e = rel_err(s.get_batch("x"), s.get_batch("u"), np.array(Xr), np.array(Ur))
+    print(f"acados-recorded force states: max rel err {e.max():.3e} ({s.launch_info()['kernel']})")
+    assert e.max() < TOL64, e.max()
+
+
 EDGE_KERNELS = [("lpc", "fp64"), ("wave", "fp64"), ("lpc", "fp32"), ("wave", "fp32")]
 
 

@@ -104,6 +104,82 @@ def test_force_closed_loop_vs_acados_run(plots, gold):
         assert np.abs(X[i, col] - y).max() < 1e-2
 
 
+@pytest.fixture(scope="module")
+def force_steps(plots, golden_dir):
+    """Every recorded force sample re-posed from acados's own state: [(t, StepModel, u0_acados)]."""
+    from oracle import acados_termination as AT
+    ref = np.load(os.path.join(golden_dir, "circle_ref.npz"))["nh30_nx6"]
+    spec = models.force_model(30)
+    out = []
+    for t, x, u in AT.force_recorded_steps(plots):
+        yref, ye = qp.yref_window(ref[:, :4], ref[:, 4:6], t, 30)
+        out.append((t, AT.StepModel(spec, x, yref, ye), u))
+    return out
+
+
+ACADOS_TOL_COMP = 1e-6     # acados's default complementarity tolerance [ext]
+
+
+def test_force_u0_bound_gaps_every_step(force_steps):
+    """Every recorded step at which the exact QP (re-posed from acados's plotted state) holds an input
+    of u0 on its bound: acados's u0 lies inside that bound (to plot precision) at a gap t with
+    t * lambda* <= acados's complementarity tolerance. 196 such (step, bound) pairs over 239 steps;
+    the largest product is 8.8e-7 (step 146)."""
+    assert len(force_steps) == 239
+    prods = []
+    for t, m, u in force_steps:
+        nC = m.Q.C.shape[0]
+        for c in range(m.nu):
+            for row, gap in ((c, u[c] - m.Q.lo[c]), (nC + c, m.Q.hi[c] - u[c])):
+                if m.lam[row] > 0:
+                    assert gap > -2e-8, (t, c, gap)
+                    prods.append(gap * m.lam[row])
+    assert len(prods) == 196
+    assert max(prods) <= ACADOS_TOL_COMP
+
+
+def test_force_every_step_is_an_acados_interior_point(force_steps):
+    """The per-step pin of the force oracle to acados: at every one of the 239 recorded
+    samples, acados's u0 equals the u0 of an interior point of the oracle's exact QP whose complementarity
+    s_i * lambda_i is at most 1e-6 at every one-sided bound (the first-order fit refined by Gauss-Newton on
+    the nonlinear weighted KKT system), to 1e-8 (plot quantisation ~3e-8). acados therefore solved the same
+    QP as the oracle and stopped at its default tolerance; the trajectory drift of
+    test_force_closed_loop_vs_acados_run is that stopping point carried through the loop."""
+    worst, n_exact = 0.0, 0
+    for t, m, u in force_steps:
+        e, mu, (U, s, lam) = m.interior_point_fit(u, ACADOS_TOL_COMP)
+        assert e < 1e-8, (t, e)
+        assert (s * lam).max() <= ACADOS_TOL_COMP * (1 + 1e-9) and s.min() > 0 and lam.min() > 0
+        worst = max(worst, e)
+        n_exact += np.abs(m.u0 - u).max() < 1e-6
+    assert n_exact == 21        # steps where acados's u0 is the exact solution to 1e-6 outright
+
+
+def test_force_acados_tolerance_is_tight(force_steps):
+    """The fit needs acados's tolerance: with complementarity capped at 5e-7, the hardest steps (largest
+    measured t * lambda) cannot be reproduced — 29 of the 239 steps fail at that cap."""
+    by_t = {t: (m, u) for t, m, u in force_steps}
+    for t in (146, 36, 106):
+        m, u = by_t[t]
+        e, _, _ = m.interior_point_fit(u, 5e-7)
+        assert e > 1e-5, (t, e)
+
+
+def test_force_step_fit_rejects_a_wrong_oracle(plots, golden_dir):
+    """Control: the same fit against an oracle with the other cost scaling (SURVEY App. B.1 'none')
+    fails — acados's inputs are not an interior point of that QP at tolerance 1e-6."""
+    from oracle import acados_termination as AT
+    ref = np.load(os.path.join(golden_dir, "circle_ref.npz"))["nh30_nx6"]
+    spec = models.force_model(30, cost_scaling="none")
+    bad = 0
+    steps = AT.force_recorded_steps(plots)[:8]
+    for t, x, u in steps:
+        yref, ye = qp.yref_window(ref[:, :4], ref[:, 4:6], t, 30)
+        e, _, _ = AT.StepModel(spec, x, yref, ye).interior_point_fit(u, ACADOS_TOL_COMP, iters=10)
+        bad += e > 1e-6
+    assert bad >= 7
+
+
 def test_force_step1_is_acados_termination(plots, golden_dir):
     """Step 1: the state acados reached equals ours (to 1e-8), so both solve the same QP.
     The exact solution has F_x on its lower bound with multiplier ~2.3e-4; acados's plotted
