@@ -41,6 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_TFLOPS = {"fp64": 78.6, "fp32": 157.3}   # MI355X vector = matrix peaks (MI355X_MICROARCH)
+HBM_PEAK_GBS = 8000.0                           # MI355X HBM3E spec peak (MI355X_MICROARCH: 6.29 TB/s measured copy)
 
 
 def parse():
@@ -400,8 +401,11 @@ def main_solve(args, world, rank, dist, device):
     """--mode solve: the general batched solve (nmpc_solve_async on the handle's device buffers) of B
     QPs per GPU with per-instance yref windows staged in HBM — what the reference's per-step pattern
     (set(k, 'yref') for every stage, set(0, 'lbx'/'ubx'), solve(); src/force_model/ocp.py:117-122,
-    controller.py:29-32) hits, with no shared reference table and no warm start: every QP is solved
-    cold by the full IPM + exact finish (ipm_lpc_kernel / ipm_kernel). The QPs are the closed loop's
+    controller.py:29-32) hits, with no shared reference table and no warm start. fp64: the fast solve
+    (sf_kernel: every instance's unconstrained solution by the Riccati recursion on the shared factorisation,
+    on the f64 matrix cores, with the bound test; fin64_kernel: primal-dual active-set steps on W and the dual
+    fallback for the instances with a violated bound; the full IPM + exact finish only for what they leave);
+    NMPC_SOLVE_FAST=0 (or fp32): the full IPM + exact finish for every QP. The QPs are the closed loop's
     first-step QPs of the bench workload (batched.first_step_qps). A step = one batched solve."""
     from drone_attitude_control_amd.acados import AcadosOcpSolver
     from drone_attitude_control_amd.batched import DEFAULT_N, first_step_qps, flops_per_iter
@@ -419,28 +423,41 @@ def main_solve(args, world, rank, dist, device):
     s.set_batch("yref", Y)
     s.solve()                                   # uploads the windows once; they stay resident in HBM
     nx, nu = s.nx, s.nu
+    info = s.launch_info()
+    fast = info["solve_kernel"] == "sf_kernel"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cref, models
         ref = cref.RiccatiIpmRef.for_options(models.MODELS[model](N), ocp.solver_options, args.precision)
+
+        def run(n, threads):
+            if fast:   # the same algorithm (riccati_ipm_solve_batch_fast); its tables are built once, untimed
+                ref.solve_fast(x0[:1], Y[:1], wsmax=cref.WSMAX[model], nthreads=1)
+                t0 = time.perf_counter()
+                _, _, st_c, it_c, cnt = ref.solve_fast(x0[:n], Y[:n], wsmax=cref.WSMAX[model], nthreads=threads)
+            else:
+                t0 = time.perf_counter()
+                _, _, st_c, it_c = ref.solve(x0[:n], Y[:n], nthreads=threads)
+                cnt = None
+            return time.perf_counter() - t0, st_c, it_c, cnt
+
         n0 = min(B, 256)
-        t0 = time.perf_counter()
-        ref.solve(x0[:n0], Y[:n0])
-        el0 = time.perf_counter() - t0
+        el0 = run(n0, ref.max_threads())[0]
         n = int(min(B, max(n0, n0 / max(el0, 1e-6) * args.cpu_seconds)))
-        t0 = time.perf_counter()
-        _, _, st_c, it_c = ref.solve(x0[:n], Y[:n])
-        el = time.perf_counter() - t0
+        el, st_c, it_c, cnt = run(n, ref.max_threads())
         n1 = min(n, 128)
-        t1 = time.perf_counter()
-        ref.solve(x0[:n1], Y[:n1], nthreads=1)
-        e1 = time.perf_counter() - t1
+        e1 = run(n1, 1)[0]
+        algo = ("riccati_ipm_solve_batch_fast (the GPU's algorithm: unconstrained solution on the shared "
+                "factorisation, active-set steps on W, the dual fallback, the full IPM + exact finish for what is "
+                "left; fp64)" if fast else "riccati_ipm_solve_batch (the same cold IPM + exact finish, fp64)")
         cpu = {"value": n / el, "unit": "QP solves/s", "cores": ref.max_threads(), "kind": "port",
-               "sample": f"{n} of the {B} QPs in {el:.2f} s: oracle/c/riccati_ipm.c riccati_ipm_solve_batch (the same "
-                         f"cold IPM + exact finish, fp64), OpenMP over instances",
+               "sample": f"{n} of the {B} QPs in {el:.2f} s: oracle/c/riccati_ipm.c {algo}, OpenMP over instances",
                "mean_newton_systems": float(np.mean(it_c)), "failed": int((st_c != 0).sum()),
                "single_core": {"value": n1 / e1, "cores": 1, "sample": f"{n1} QPs in {e1:.2f} s"}}
+        if cnt:
+            cpu["paths"] = {k: cnt[k] / max(1.0, cnt["solves"]) for k in ("unconstrained", "set", "full", "failed")}
+            cpu["flops_per_qp"] = cnt["flops"] / max(1.0, cnt["solves"])
 
     def barrier():
         if dist is not None:
@@ -471,12 +488,54 @@ def main_solve(args, world, rank, dist, device):
     elapsed = float(regions[med])
     kernel_ms = float(np.median(kms))
     if rank == 0:
-        info = s.launch_info()
-        n_newton = cpu["mean_newton_systems"] if cpu else float(red[1] / max(1.0, red[2]))
-        fl_solve = flops_per_iter(nx, nu, N) * n_newton
-        achieved = fl_solve * B / (kernel_ms * 1e-3) / 1e12
+        kernel = info["solve_kernel"]
+        w = 8 if args.precision == "fp64" else 4
+        min_b = float(B * (nx + N * (nx + nu) + nx + N * nu + (N + 1) * nx) * w)
+        pmc = load_pmc(model, N, B, args.precision, kernel, 1, mode="solve")
+        traffic = pmc.get("hbm_bytes_per_step")
         peak = PEAK_TFLOPS[args.precision]
-        pmc = load_pmc(model, N, B, args.precision, info["kernel"], 1, mode="solve")
+        if fast and cpu and cpu.get("flops_per_qp"):
+            fl_solve = cpu["flops_per_qp"]
+            credit = ("FP64 flops per QP of the CPU run of the same algorithm on the same QPs (riccati_ipm_solve_batch_"
+                      "fast, counted per path: gradient G yref, the Riccati recursion on the shared factorisation, "
+                      "active-set steps m^3/3 + 2 m^2 + 2 ne m, full solves F_iter per Newton system) x B / kernel time")
+        else:
+            n_newton = cpu["mean_newton_systems"] if cpu else float(red[1] / max(1.0, red[2]))
+            fl_solve = flops_per_iter(nx, nu, N) * n_newton
+            credit = ("SURVEY 8d F_iter (one Riccati factorisation + predictor/corrector sweeps + box elementwise per "
+                      "Newton system) x the CPU baseline's mean Newton systems per QP on the same QPs x B / kernel time")
+        achieved = fl_solve * B / (kernel_ms * 1e-3) / 1e12
+        hbm_achieved = min_b / (kernel_ms * 1e-3) / 1e9
+        # the fast solve reads each window once and writes each trajectory once: its roof is HBM (the algorithmic
+        # bytes per launch over the launch time, against 8 TB/s); the full IPM's is the FP64 pipe
+        if fast:
+            roof = {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm_achieved / HBM_PEAK_GBS,
+                    "algorithmic_bytes_per_launch": min_b,
+                    "bytes_note": "x0 + yref window in, the full x / u trajectories out per QP (SURVEY 8d) x B",
+                    "fp64": {"achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                             "credit": credit, "flops_per_solve": fl_solve}}
+        else:
+            roof = {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32",
+                    "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                    "credit": credit, "flops_per_solve": fl_solve,
+                    "hbm": {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": hbm_achieved / HBM_PEAK_GBS}}
+        roof.update({"kernel": kernel, "kernel_ms": kernel_ms,
+                     "executed_fp64_flops_per_step": pmc.get("fp64_flops_per_step"),
+                     "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
+                     "traffic": traffic, "min_bytes_per_step": min_b,
+                     "traffic_vs_min_bytes": traffic / min_b if traffic else None,
+                     "traffic_note": "FETCH_SIZE + WRITE_SIZE per batched solve from the committed PMC pass "
+                                     f"({pmc.get('source', 'none for this config')}); min bytes = x0 + yref window "
+                                     "in, full x/u trajectories out (SURVEY 8d)",
+                     "kernel_ms_note": "HIP events around the solve's launches (fast solve: sf_kernel + fin64_kernel "
+                                       "and, when any instance parks, the full solve of the parked ones)",
+                     "gpu_mean_qp_iter": float(red[1] / max(1.0, red[2]))})
+        what = (f"fp64 fast solve (sf_kernel: unconstrained solution by the Riccati recursion on the shared "
+                f"factorisation on the f64 matrix cores + bound test; fin64_kernel: active-set steps on W and the dual "
+                f"fallback for the violated ones; full IPM + exact finish for what they leave)" if fast else
+                f"full Mehrotra IPM + exact active-set finish ({kernel})")
         line = {
             "metric": f"QP solves/sec (batched nmpc_solve, per-instance yref windows), N={N} nx={nx} nu={nu} ({model})",
             "value": world * B * args.steps / elapsed,
@@ -487,26 +546,14 @@ def main_solve(args, world, rank, dist, device):
             "dtype": "f64" if args.precision == "fp64" else "f32",
             "data": "synthetic (the bench workload's first-step QPs, per-instance yref windows)",
             "config": {"workload": f"{model} batched cold QP solve: {B} independent QPs per GPU, each with its own "
-                                   f"stage-stacked yref window and x0 resident in HBM; full Mehrotra IPM + exact "
-                                   f"active-set finish, no shared table, no warm start ({info['kernel']})",
+                                   f"stage-stacked yref window and x0 resident in HBM, no shared table, no warm "
+                                   f"start; {what}",
                        "model": model, "nx": nx, "nu": nu, "horizon_N": N, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": parallelism_label(dist, world), "instances_per_wave": info["instances_per_wave"]},
+                       "parallelism": parallelism_label(dist, world),
+                       "instances_per_wave": (16 // (1 if nx <= 4 else 2 if nx <= 8 else 4)) if fast else info["instances_per_wave"]},
             "timing": dict(timing_block(regions, elapsed, "each region enqueues --steps batched solves back to back"),
                            steps_per_region=args.steps),
-            "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32", "kernel": info["kernel"],
-                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "credit": "SURVEY 8d F_iter (one Riccati factorisation + predictor/corrector sweeps + box "
-                                   "elementwise per Newton system) x the CPU baseline's mean Newton systems per QP on "
-                                   "the same QPs x B / kernel time",
-                         "flops_per_solve": fl_solve, "kernel_ms": kernel_ms,
-                         "executed_fp64_flops_per_step": pmc.get("fp64_flops_per_step"),
-                         "traffic": pmc.get("hbm_bytes_per_step"),
-                         "min_bytes_per_step": float(B * (nx + N * (nx + nu) + nx + N * nu + (N + 1) * nx)
-                                                     * (8 if args.precision == "fp64" else 4)),
-                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per batched solve from the committed PMC pass "
-                                         f"({pmc.get('source', 'none for this config')}); min bytes = x0 + yref window "
-                                         "in, full x/u trajectories out (SURVEY 8d)",
-                         "gpu_mean_qp_iter": float(red[1] / max(1.0, red[2]))},
+            "roofline": roof,
             "failed_solves": int(red[0]),
             "cpu_baseline": cpu,
         }

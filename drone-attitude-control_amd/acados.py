@@ -416,13 +416,17 @@ class AcadosOcpSolver:
         return self._check(self.lib.nmpc_set_stream(self._h, ctypes.c_void_p(stream_ptr)), "set_stream")
 
     def launch_info(self):
-        out = (ctypes.c_int * 8)()
-        self._check(self.lib.nmpc_get_launch_info(self._h, out, 8), "launch_info")
+        out = (ctypes.c_int * 9)()
+        self._check(self.lib.nmpc_get_launch_info(self._h, out, 9), "launch_info")
         return {"instances_per_wave": out[0], "workgroups": out[1], "threads": out[2], "lds_bytes": out[3],
                 "kernel": {0: "ipm_kernel", 1: "ipm_lpc_kernel", 2: "cond_ipm_kernel", 3: "ipm_lpi_kernel"}.get(out[4], str(out[4])),
                 "structure": {0: "dense", 1: "force", 2: "jerk", 3: "quad13"}.get(out[5], str(out[5])),
                 "closed_loop_kernel": {0: "fused", 1: "cl_fast_kernel", 2: "cl_lock_kernel"}.get(out[6], str(out[6])),
-                "active_set_max": out[7]}
+                "active_set_max": out[7],
+                # what nmpc_solve runs: the fp64 fast path (sf_kernel: unconstrained solution on the shared
+                # factorisation, fin64_kernel: active-set finish; full IPM only for what they leave) or `kernel`
+                "solve_kernel": "sf_kernel" if out[8] else {0: "ipm_kernel", 1: "ipm_lpc_kernel", 2: "cond_ipm_kernel",
+                                                            3: "ipm_lpi_kernel"}.get(out[4], str(out[4]))}
 
     def discrete_model(self):
         A = np.zeros((self.nx, self.nx))

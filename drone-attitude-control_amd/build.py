@@ -12,7 +12,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "lib", "libnmpc_hip.so")
 SOURCES = ["nmpc_ipm.hip", "nmpc_ipm_lpc.hip", "nmpc_ipm_lpi.hip", "nmpc_cond.hip", "nmpc_plant.hip", "nmpc_closed_loop.hip",
-           "nmpc_cl_fast.hip", "nmpc_api.cpp", "nmpc_cond_host.cpp"]
+           "nmpc_cl_fast.hip", "nmpc_solve_fast.hip", "nmpc_api.cpp", "nmpc_cond_host.cpp"]
 HEADERS = ["nmpc_internal.h", "nmpc_lpc_geom.h", "nmpc_cl_device.h", os.path.join("..", "..", "include", "nmpc.h")]
 ARCH = os.environ.get("NMPC_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value",

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/nmpc.h"
@@ -235,6 +236,20 @@ struct nmpc_solver {
     int *d_fsI = nullptr;                  // s_e, s_src, eslot
     size_t fsi[4] = {0, 0, 0, 0};
     int clf_nfree = 0;
+    // fp64 general solve on the shared factorisation (nmpc_solve_fast.hip sf_kernel + fin64_kernel; sf_setup)
+    bool sfast = false, sf_pending = false;
+    double *d_sf = nullptr;                // per-stage tables [N][ts], gradient diagonal [nz + nx]
+    size_t sf_gd = 0;                      // offset of the gradient diagonal in d_sf
+    double *d_f64 = nullptr;               // fin64 slot tables: s_lb, s_ub, uinit
+    size_t f64o[3] = {0, 0, 0};
+    int *d_f64i = nullptr;                 // s_e, s_free
+    size_t f64i[2] = {0, 0};
+    int f64_nslot = 0, f64_nfree = 0, f64_resident = 0;
+    int *d_sfl = nullptr;                  // [0] listed count, [1] parked count, [2..2+B) list, [2+B..2+2B) parked
+    int *h_sfpark = nullptr;               // pinned: the parked count of the last fast solve
+    int sf_kidx = -1;                      // lane-per-component kernel of the parked instances' full solves
+    void *d_sf_scratch = nullptr;          // its scratch when the handle's own family is another
+    hipEvent_t ev_fb = nullptr;            // start of the parked instances' full solve
     int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
     int clf_resident = 0;                  // workgroups of cl_fast_kernel the handle's device holds at once
@@ -508,8 +523,11 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_acc, (void *)h->d_noise, (void *)h->d_cycles, h->d_cond, (void *)h->d_cond_i,
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
                     (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw,
-                    (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0})
+                    (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0, (void *)h->d_sf, (void *)h->d_f64,
+                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch})
         if (p) hipFree(p);
+    if (h->h_sfpark) hipHostFree(h->h_sfpark);
+    if (h->ev_fb) hipEventDestroy(h->ev_fb);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->h_park) hipHostFree(h->h_park);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -584,25 +602,34 @@ constexpr int CL_FUSED_CHUNK = 64;   // closed-loop steps per fused solve launch
 
 int fin32_setup(nmpc_solver *h);
 hipError_t fin32_enqueue(nmpc_solver *h);
+int sf_setup(nmpc_solver *h);
+int sf_resolve(nmpc_solver *h);
 
-// list mode of the lane-per-component kernel (the lean closed loop's fallback)
+// list mode of the lane-per-component kernel: the lean closed loop's fallback (a full solve + plant step per
+// listed instance, cl_steps = 1) or the fast general solve's (a cold full solve per listed instance, cl_steps = 0)
 struct ListArgs {
     int count, step0, noise_ld;
+    const int *list;
+    int kidx;
+    void *scratch;
 };
 
 // cl_steps > 0: fused closed loop of that many steps (lane-per-component / wavefront kernels)
+int sf_enqueue(nmpc_solver *h);
+
 template <typename T>
 int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0, const ListArgs *la = nullptr)
 {
     if (h->cond) return launch_cond<T>(h, e0, e1);
+    if (std::is_same<T, double>::value && h->sfast && cl_steps == 0 && !la) return sf_enqueue(h);
     nmpc::IpmParams<T> p{};
     int kidx = h->kidx;
     void *scratch = h->d_scratch;
     p.cl_steps = cl_steps;
     if (la) {
-        kidx = h->clf_kidx;
-        if (h->d_clf_scratch) scratch = h->d_clf_scratch;
-        p.cl_list = h->d_park + 2;
+        kidx = la->kidx;
+        if (la->scratch) scratch = la->scratch;
+        p.cl_list = la->list;
         p.cl_count = la->count;
         p.cl_istep = h->d_istep;
         p.cl_noise_ld = la->noise_ld;
@@ -1140,8 +1167,8 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
         delete h;
         return r;
     }
-    if (!f64) {
-        const int r = fin32_setup(h);
+    {
+        const int r = f64 ? sf_setup(h) : fin32_setup(h);
         if (r < 0) {
             g_err = h->err;
             free_all(h);
@@ -1297,6 +1324,9 @@ int nmpc_synchronize(nmpc_solver *h)
     if (!h) return NMPC_EINVAL;
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize");
+    const int r = sf_resolve(h);   // the last fast solve's parked instances (full solves), if any
+    if (r < 0) return r;
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize");
     hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1);
     return 0;
 }
@@ -1325,6 +1355,7 @@ int nmpc_solve(nmpc_solver *h)
     }
     int r = h->precision == NMPC_FP64 ? launch<double>(h) : launch<float>(h);
     if (r < 0) return r;
+    if ((r = sf_resolve(h)) < 0) return r;   // fast solve: full solves of the parked instances, if any
     const size_t nxo = h->h_x.size(), nuo = h->h_u.size();
     if (h->precision == NMPC_FP64) {
         hipMemcpyAsync(h->h_x.data(), h->d_x, nxo * sizeof(double), hipMemcpyDeviceToHost, h->stream);
@@ -1411,9 +1442,9 @@ int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n)
     const bool f64 = h->precision == NMPC_FP64;
     const int kind = h->cond ? 2 : f64 ? nmpc::ipm_kind<double>(h->kidx) : nmpc::ipm_kind<float>(h->kidx);
     const int sid = h->cond ? 0 : f64 ? nmpc::ipm_structure<double>(h->kidx) : nmpc::ipm_structure<float>(h->kidx);
-    const int v[8] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid, h->clf ? (h->clf_kind == nmpc::CLF_LOCK ? 2 : 1) : 0,
-                      h->clf ? nmpc::cl_fast_wsmax(h->nx, h->nu) : 0};
-    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
+    const int v[9] = {h->ipw, (waves + h->wpb - 1) / h->wpb, 64 * h->wpb, h->lds, kind, sid, h->clf ? (h->clf_kind == nmpc::CLF_LOCK ? 2 : 1) : 0,
+                      h->clf ? nmpc::cl_fast_wsmax(h->nx, h->nu) : 0, h->sfast ? 1 : 0};
+    for (int i = 0; i < n && i < 9; i++) out[i] = v[i];
     return 0;
 }
 
@@ -1695,6 +1726,217 @@ hipError_t fin32_enqueue(nmpc_solver *h)
     p.x0in = (const float *)h->d_x0;
     if (!nmpc::fin32_launch(h->nx, h->nu, 0, p, h->fin_resident, h->stream)) return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+// The fp64 general solve on the shared factorisation (nmpc_solve_fast.hip sf_kernel, nmpc_cl_fast.hip
+// fin64_kernel): for the compiled shapes with diagonal LINEAR_LS maps and the exact finish on (env
+// NMPC_SOLVE_FAST=0: off, every solve runs the full IPM). Tables per stage k from the factorisation
+// (lqr_table: K_k, F_uu,k^-1, P_{k+1}, P_{k+1} c): Acl_k' = (A + B K_k)', K_k', -F^-1 B', -F^-1, K_k,
+// Acl_k' P_{k+1} c and -F^-1 B' P_{k+1} c, in sf::Tab's compact layout; the gradient diagonal; the slot tables
+// of fin64_kernel (the lean loop's slot layout: bounded elements, bounds, unbounded elements, mid-box inputs).
+int sf_setup(nmpc_solver *h)
+{
+    // (an explicit kernel family, env NMPC_KERNEL, selects that family's full solve as well)
+    const char *env = std::getenv("NMPC_SOLVE_FAST");
+    const int nx = h->nx, nu = h->nu, nz = nx + nu, N = h->N, W = lqr_words(nx, nu);
+    const int ts = nmpc::sf_table_words(nx, nu);
+    if ((env && env[0] == '0') || std::getenv("NMPC_KERNEL") || h->cond || !h->g_diag || h->lqr_host.empty() || ts <= 0 ||
+        nmpc::sf_lds_bytes(nx, nu, N) > 160 * 1024)
+        return 0;
+    std::vector<int> el, fr;
+    std::vector<double> lb, ub, uinit;
+    if (!slot_layout(h, el, fr, lb, ub, uinit)) return 0;
+    const int res = nmpc::fin64_resident(nx, nu, (int)el.size(), h->device);
+    if (res <= 0) return 0;
+    // the parked instances' full solves: the handle's kernel if it is of the lane-per-component family, else
+    // that family's kernel with its own scratch
+    int fk = h->kidx;
+    if (nmpc::ipm_kind<double>(h->kidx) != 1) {
+        fk = nmpc::ipm_find_family<double>(nx, nu, 1);
+        if (fk < 0) return 0;
+        std::vector<double> ABh((size_t)nx * nz);
+        for (int r = 0; r < nx; r++) {
+            for (int q = 0; q < nx; q++) ABh[r * nz + q] = h->A[r * nx + q];
+            for (int q = 0; q < nu; q++) ABh[r * nz + nx + q] = h->B[r * nu + q];
+        }
+        fk = nmpc::ipm_refine<double>(fk, ABh.data(), h->H.data(), h->He.data());
+    }
+    const int bpg = nx <= 4 ? 1 : (nx <= 8 ? 2 : 4), R = 4 * bpg;
+    const int o_aclt = 0, o_kt = o_aclt + bpg * R * 4, o_fibt = o_kt + R * 4, o_nfi = o_fibt + bpg * 16, o_kk = o_nfi + 16,
+              o_cp = o_kk + bpg * 16, o_cf = o_cp + R;
+    if (o_cf + 4 != ts) return h->fail(NMPC_EUNSUPPORTED, "sf_setup: table layout mismatch");
+    std::vector<double> tab((size_t)N * ts, 0.0), K((size_t)nu * nx), Fi((size_t)nu * nu), Pc(nx), Acl((size_t)nx * nx),
+        FiBt((size_t)nu * nx);
+    for (int k = 0; k < N; k++) {
+        const double *t = &h->lqr_host[(size_t)k * nz * W];
+        for (int r = 0; r < nx; r++) {
+            for (int i = 0; i < nu; i++) K[i * nx + r] = t[r * W + nx + i];
+            Pc[r] = t[r * W + nz];
+        }
+        for (int u = 0; u < nu; u++)
+            for (int i = 0; i < nu; i++) Fi[u * nu + i] = t[(nx + u) * W + i];
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < nx; j++) {
+                double s_ = h->A[i * nx + j];
+                for (int l = 0; l < nu; l++) s_ += h->B[i * nu + l] * K[l * nx + j];
+                Acl[i * nx + j] = s_;
+            }
+        for (int i = 0; i < nu; i++)
+            for (int j = 0; j < nx; j++) {
+                double s_ = 0.0;
+                for (int l = 0; l < nu; l++) s_ -= Fi[i * nu + l] * h->B[j * nu + l];
+                FiBt[i * nx + j] = s_;
+            }
+        double *d = &tab[(size_t)k * ts];
+        for (int kc = 0; kc < bpg; kc++)
+            for (int row = 0; row < R; row++)
+                for (int q = 0; q < 4; q++) {
+                    const int col = 4 * kc + q;
+                    d[o_aclt + (kc * R + row) * 4 + q] = (row < nx && col < nx) ? Acl[col * nx + row] : 0.0;
+                }
+        for (int row = 0; row < nx; row++)
+            for (int q = 0; q < nu; q++) d[o_kt + row * 4 + q] = K[q * nx + row];
+        for (int kc = 0; kc < bpg; kc++)
+            for (int i = 0; i < nu; i++)
+                for (int q = 0; q < 4; q++) {
+                    const int col = 4 * kc + q;
+                    if (col >= nx) continue;
+                    d[o_fibt + (kc * 4 + i) * 4 + q] = FiBt[i * nx + col];
+                    d[o_kk + (kc * 4 + i) * 4 + q] = K[i * nx + col];
+                }
+        for (int i = 0; i < nu; i++)
+            for (int q = 0; q < nu; q++) d[o_nfi + i * 4 + q] = -Fi[i * nu + q];
+        for (int row = 0; row < nx; row++) {
+            double s_ = 0.0;
+            for (int j = 0; j < nx; j++) s_ += Acl[j * nx + row] * Pc[j];
+            d[o_cp + row] = s_;
+        }
+        for (int i = 0; i < nu; i++) {
+            double s_ = 0.0;
+            for (int j = 0; j < nx; j++) s_ += FiBt[i * nx + j] * Pc[j];
+            d[o_cf + i] = s_;
+        }
+    }
+    std::vector<double> gd(nz + nx, 0.0);
+    for (int i = 0; i < nz; i++) gd[i] = h->G[i * h->ny + i];
+    for (int i = 0; i < nx; i++) gd[nz + i] = h->Ge[i * h->ny_e + i];
+    h->sf_gd = ((size_t)N * ts + 31) & ~(size_t)31;
+    const std::vector<double> *fp[3] = {&lb, &ub, &uinit};
+    size_t ftot = 0;
+    for (int i = 0; i < 3; i++) {
+        h->f64o[i] = ftot;
+        ftot += (fp[i]->size() + 31) & ~(size_t)31;
+    }
+    const std::vector<int> *ipp[2] = {&el, &fr};
+    size_t itot = 0;
+    for (int i = 0; i < 2; i++) {
+        h->f64i[i] = itot;
+        itot += (ipp[i]->size() + 63) & ~(size_t)63;
+    }
+    const size_t sc = fk != h->kidx ? nmpc::ipm_scratch_elems<double>(fk, h->batch, N) * sizeof(double) : 0;
+    if (hipMalloc((void **)&h->d_sf, (h->sf_gd + gd.size()) * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&h->d_f64, ftot * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&h->d_f64i, itot * sizeof(int)) != hipSuccess ||
+        hipMalloc((void **)&h->d_sfl, (2 + 2 * (size_t)h->batch) * sizeof(int)) != hipSuccess ||
+        (sc && hipMalloc(&h->d_sf_scratch, sc) != hipSuccess) ||
+        hipHostMalloc((void **)&h->h_sfpark, 4 * sizeof(int), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreate(&h->ev_fb) != hipSuccess)
+        return h->fail(NMPC_ENOMEM, "nmpc_create: fast-solve tables");
+    hipError_t e = hipMemcpy(h->d_sf, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->d_sf + h->sf_gd, gd.data(), gd.size() * sizeof(double), hipMemcpyHostToDevice);
+    for (int i = 0; i < 3 && e == hipSuccess; i++)
+        if (!fp[i]->empty()) e = hipMemcpy(h->d_f64 + h->f64o[i], fp[i]->data(), fp[i]->size() * sizeof(double), hipMemcpyHostToDevice);
+    for (int i = 0; i < 2 && e == hipSuccess; i++)
+        if (!ipp[i]->empty()) e = hipMemcpy(h->d_f64i + h->f64i[i], ipp[i]->data(), ipp[i]->size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(h, e, "nmpc_create: fast-solve upload");
+    h->h_sfpark[0] = 0;
+    h->f64_nslot = (int)el.size();
+    h->f64_nfree = (int)fr.size();
+    h->f64_resident = res;
+    h->sf_kidx = fk;
+    h->sfast = true;
+    return 0;
+}
+
+// one fast solve on the handle's stream: list / park counters reset, sf_kernel, fin64_kernel, the parked count
+// to the pinned host word (sf_resolve reads it once the stream has drained)
+int sf_enqueue(nmpc_solver *h)
+{
+    const int nx = h->nx, nu = h->nu, nz = nx + nu;
+    const char *m = (const char *)h->d_model;
+    nmpc::SfParams sp{};
+    sp.B = h->batch;
+    sp.N = h->N;
+    sp.ny = h->ny;
+    sp.ystride = (int)h->ystride();
+    sp.tab = h->d_sf;
+    sp.gd = h->d_sf + h->sf_gd;
+    sp.AB = (const double *)(m + h->off_AB);
+    sp.c = (const double *)(m + h->off_c);
+    sp.lbnd = (const double *)(m + h->off_lb);
+    sp.ubnd = (const double *)(m + h->off_ub);
+    sp.x0 = (const double *)h->d_x0;
+    sp.yref = (const double *)h->d_yref;
+    sp.xout = (double *)h->d_x;
+    sp.uout = (double *)h->d_u;
+    sp.status = h->d_status;
+    sp.iters = h->d_iters;
+    sp.list_count = h->d_sfl;
+    sp.list = h->d_sfl + 2;
+    nmpc::ClFastParams<double> p{};
+    p.B = h->batch;
+    p.N = h->N;
+    p.ne = (h->N + 1) * nz;
+    p.nslot = h->f64_nslot;
+    p.polish_steps = h->polish_steps;
+    // env NMPC_CLF_NO_GI=1 (test knob): no dual fallback, so unsettled instances park and take the full solve
+    const char *nogi = std::getenv("NMPC_CLF_NO_GI");
+    p.gi = (nogi && nogi[0] == '1') ? 0 : 1;
+    p.s_lb = h->d_f64 + h->f64o[0];
+    p.s_ub = h->d_f64 + h->f64o[1];
+    p.uinit = h->d_f64 + h->f64o[2];
+    p.s_e = h->d_f64i + h->f64i[0];
+    p.s_free = h->d_f64i + h->f64i[1];
+    p.nfree = h->f64_nfree;
+    p.W = (const double *)(m + h->off_lqrw);
+    p.lbnd = sp.lbnd;
+    p.ubnd = sp.ubnd;
+    p.AB = sp.AB;
+    p.c = sp.c;
+    p.xout = sp.xout;
+    p.uout = sp.uout;
+    p.status = h->d_status;
+    p.iters = h->d_iters;
+    p.park_count = h->d_sfl + 1;
+    p.park_list = h->d_sfl + 2 + h->batch;
+    p.x0in = sp.x0;
+    p.work_list = sp.list;
+    p.work_count = sp.list_count;
+    p.z0_xu = 1;
+    hipEventRecord(h->ev0, h->stream);
+    hipError_t e = hipMemsetAsync(h->d_sfl, 0, 2 * sizeof(int), h->stream);
+    if (e == hipSuccess) e = nmpc::sf_launch(nx, nu, sp, h->stream);
+    if (e == hipSuccess) e = nmpc::fin64_launch(nx, nu, p, h->f64_resident, h->stream) ? hipGetLastError() : hipErrorInvalidValue;
+    hipEventRecord(h->ev1, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->h_sfpark, h->d_sfl + 1, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "fast solve launch");
+    h->sf_pending = true;
+    return 0;
+}
+
+// after a fast solve: waits for it; the instances fin64_kernel parked (certified-infeasible QPs, sets the
+// active-set finish did not settle) get the full IPM + exact finish (ipm_lpc_kernel in list mode, cold), timed
+// into the solve's event pair
+int sf_resolve(nmpc_solver *h)
+{
+    if (!h->sf_pending) return 0;
+    h->sf_pending = false;
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "fast solve");
+    const int parked = h->h_sfpark[0];
+    if (parked <= 0) return 0;
+    const ListArgs la{parked, 0, 0, h->d_sfl + 2 + h->batch, h->sf_kidx, h->d_sf_scratch};
+    return launch<double>(h, h->ev_fb, h->ev1, 0, &la);
 }
 
 // The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, or fp32 (the tables
@@ -2003,7 +2245,7 @@ int clf_run(nmpc_solver *h, int steps)
             if (parked <= 0) break;
             h->clf_parked += parked;
             // the fallback: one full solve + plant step for every parked instance
-            const ListArgs la{parked, h->cl_step, n};
+            const ListArgs la{parked, h->cl_step, n, h->d_park + 2, h->clf_kidx, h->d_clf_scratch};
             const int r = launch<T>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
             launches++;
             if (r < 0) return r;

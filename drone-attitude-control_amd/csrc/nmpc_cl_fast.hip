@@ -937,6 +937,15 @@ __device__ __forceinline__ double plant_step(const ClFastParams<T> &p, const dou
     return xl;
 }
 
+// z_0 of element e = k nz + r as sf_kernel wrote it (the unconstrained solution, unclamped)
+template <typename T, int NX, int NU>
+__device__ __forceinline__ T z0_from_outputs(const ClFastParams<T> &p, int inst, int e)
+{
+    constexpr int NZ = NX + NU;
+    const int k = e / NZ, r = e % NZ;
+    return r < NX ? p.xout[((size_t)inst * (p.N + 1) + k) * NX + r] : p.uout[((size_t)inst * p.N + k) * NU + (r - NX)];
+}
+
 // trajectory outputs of an instance's last solve: x_0 the state, the bounded elements the lane's slots
 // (z of the accepted solve — held bounds exact — clamped onto the bounds), the unbounded decision
 // elements (p.s_free) z_0 from the full tables plus the accepted active-set step W[:, S] nu; a failed
@@ -973,6 +982,8 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<
         double z;
         if (p.z0all) {   // the solve finish: z_0 from the GEMM
             z = (double)p.z0all[(size_t)inst * p.z0_ld + e];
+        } else if (p.z0_xu) {   // the fp64 solve's finish: z_0 as sf_kernel wrote it
+            z = (double)z0_from_outputs<T, NX, NU>(p, inst, e);
         } else {
             const T *tr = p.txfull + (size_t)e * NX;
             double s0 = (double)p.vfull[(size_t)t * ne + e], s1 = 0.0;   // fp64 sums (the set's terms cancel)
@@ -1494,6 +1505,73 @@ __global__ __launch_bounds__(64 * WPB) void fin32_kernel(ClFastParams<float> p)
         if (ok) {
             write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, 0, 0, m_acc, z);
             if (lane == 0) p.iters[inst] += steps;
+        }
+        CLF_SYNC();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// The finish of the fp64 general solve: the instances sf_kernel (nmpc_solve_fast.hip) listed because their
+// unconstrained solution violates a bound, one wavefront per instance (persistent over the list): z_0 at the
+// slots from the outputs sf_kernel wrote, then slow_step from an empty warm set (the first set from z_0's
+// violations; PDAS rounds on W, the certificate, the dual fallback; oracle/c/riccati_ipm.c
+// riccati_ipm_solve_batch_fast). Accepted: the outputs are rewritten from the exact solution, status 0,
+// qp_iter = 1 + the active-set steps. Otherwise (a certified-infeasible QP or no settled set) the instance is
+// parked for the full IPM (ipm_lpc_kernel in list mode).
+template <int NX, int NU, int EPL, int WSM, int WPB>
+__global__ __launch_bounds__(64 * WPB) void fin64_kernel(ClFastParams<double> p)
+{
+    using T = double;
+    constexpr int NZ = NX + NU, NSLOT = EPL * 64;
+    const int cnt = __builtin_amdgcn_readfirstlane(*p.work_count);
+    if ((int)blockIdx.x * WPB >= cnt) return;   // nothing for this workgroup: no table setup
+    __shared__ Lds<NSLOT, NZ, WSM> lds_all[WPB];
+    __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT], slo[NSLOT], shi[NSLOT], sol[NSLOT], sou[NSLOT];
+    __shared__ int sse[NSLOT], ssrc[NSLOT];
+    for (int e = threadIdx.x; e < NX * NZ; e += 64 * WPB) abl[e] = p.AB[e];
+    for (int e = threadIdx.x; e < NX; e += 64 * WPB) cl[e] = p.c[e];
+    for (int s = threadIdx.x; s < NSLOT; s += 64 * WPB) {
+        const bool v = s < p.nslot;
+        const double l = v ? p.s_lb[s] : -1e30, u = v ? p.s_ub[s] : 1e30;
+        const bool hl = has_b(l), hu = has_b(u);
+        slb[s] = l;
+        sub[s] = u;
+        slo[s] = hl ? l - ClfTol<T>::viol * (1.0 + fabs(l)) : -DBL_MAX;
+        shi[s] = hu ? u + ClfTol<T>::viol * (1.0 + fabs(u)) : DBL_MAX;
+        sol[s] = hl ? l + ClfTol<T>::onb * (1.0 + fabs(l)) : -DBL_MAX;
+        sou[s] = hu ? u - ClfTol<T>::onb * (1.0 + fabs(u)) : DBL_MAX;
+        sse[s] = v ? p.s_e[s] : -1;
+        ssrc[s] = -1;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
+    if (lane < 32) L.xs[lane] = 0.0;
+#ifdef NMPC_CLF_TIMING
+    if (lane < CLF_NT) L.tacc[lane] = 0;
+#endif
+    __syncthreads();
+    const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
+    for (int w = (int)blockIdx.x * WPB + wave; w < cnt; w += (int)gridDim.x * WPB) {
+        const int inst = __builtin_amdgcn_readfirstlane(p.work_list[w]);
+        if (lane < NX) L.xs[lane] = p.x0in[(size_t)inst * NX + lane];
+        T z[EPL];
+#pragma unroll
+        for (int j = 0; j < EPL; j++) {
+            const int e = sv.e(j);
+            z[j] = e >= 0 ? z0_from_outputs<T, NX, NU>(p, inst, e) : T(0);
+        }
+        CLF_SYNC();
+        const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, 0u, false, false);
+        const bool ok = ((sr >> 8) & 1) && (sr & 0xff) == 0;
+        if (ok) {
+            write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, 0, 0, (sr >> 10) & 0xff, z);
+            if (lane == 0) {
+                p.status[inst] = 0;
+                p.iters[inst] = sr >> 18;
+            }
+        } else if (lane == 0) {
+            const int pos = atomicAdd(p.park_count, 1);
+            p.park_list[pos] = inst;
         }
         CLF_SYNC();
     }
@@ -2097,6 +2175,42 @@ int fin32_resident(int nx, int nu, int nslot, int device)
         res = per_cu * cus;
     });
     return res;
+}
+
+// the fp64 solve finish's shapes: as fin32 (the lean loop's slot layouts)
+template <class F>
+static bool fin64_dispatch(int nx, int nu, int nslot, F &&f)
+{
+    if (nx == 13 && nu == 4 && nslot <= 256) f(clf::fin64_kernel<13, 4, 4, 16, 8>, 8);
+    else if (nx == 13 && nu == 4 && nslot <= 384) f(clf::fin64_kernel<13, 4, 6, 16, 4>, 4);
+    else if (nx == 6 && nu == 2 && nslot <= 320) f(clf::fin64_kernel<6, 2, 5, 16, 8>, 8);
+    else if (nx == 6 && nu == 2 && nslot <= 448) f(clf::fin64_kernel<6, 2, 7, 16, 4>, 4);
+    else if (nx == 4 && nu == 2 && nslot <= 128) f(clf::fin64_kernel<4, 2, 2, 32, 4>, 4);
+    else if (nx == 4 && nu == 2 && nslot <= 192) f(clf::fin64_kernel<4, 2, 3, 32, 4>, 4);
+    else if (nx == 4 && nu == 2 && nslot <= 256) f(clf::fin64_kernel<4, 2, 4, 32, 4>, 4);
+    else return false;
+    return true;
+}
+
+int fin64_resident(int nx, int nu, int nslot, int device)
+{
+    int res = 0;
+    fin64_dispatch(nx, nu, nslot, [&](auto k, int wpb) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64 * wpb, 0) != hipSuccess || per_cu < 1) return;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) return;
+        res = per_cu * cus;
+    });
+    return res;
+}
+
+// grid: the resident workgroups (the list's length is known on the device only; idle workgroups exit at once)
+bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, hipStream_t s)
+{
+    return fin64_dispatch(nx, nu, p.nslot, [&](auto k, int wpb) {
+        const int blocks = std::max(1, std::min((p.B + wpb - 1) / wpb, resident));
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, s, p);
+    });
 }
 
 bool fin32_launch(int nx, int nu, int, const ClFastParams<float> &p, int resident, hipStream_t s)

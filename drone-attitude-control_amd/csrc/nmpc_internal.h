@@ -145,6 +145,10 @@ struct ClFastParams {
     const T *z0all;
     int z0_ld;
     const T *x0in;
+    // the fp64 general solve's finish (fin64_kernel): the instances sf_kernel listed (work_list[0 .. *work_count)),
+    // whose unconstrained solutions z_0 sf_kernel wrote to xout / uout (z0_xu = 1: z_0 read from there)
+    const int *work_list, *work_count;
+    int z0_xu;
 };
 // fp32 handles' exact finish of a solve (nmpc_cl_fast.hip): z_0 = M [x0; yref] + vc for every element on the
 // f32 matrix cores, then per instance the lean loop's active-set machinery (fp64 W, solves and acceptance)
@@ -159,6 +163,27 @@ hipError_t fin32_z0_launch(const Fin32Z0Params &p, hipStream_t s);
 bool fin32_launch(int nx, int nu, int sid, const ClFastParams<float> &p, int resident, hipStream_t s);
 // resident workgroups of the finish for (nx, nu, nslot) on `device`; 0: none compiled
 int fin32_resident(int nx, int nu, int nslot, int device);
+// The fp64 general solve's common path (nmpc_solve_fast.hip sf_kernel): the unconstrained solution of every
+// instance by the Riccati recursion on the shared factorisation (f64 MFMA, four instances per block group),
+// x / u written unclamped, the bound test; instances with a violated bound listed for fin64_kernel.
+struct SfParams {
+    int B, N, ny, ystride;
+    const double *tab;            // [N][sf_table_words] per-stage matrices / vectors (nmpc_api.cpp sf_setup)
+    const double *gd;             // [nz] diagonal gradient map G_rr, then [nx] Ge_rr
+    const double *AB, *c;         // [nx][nz], [nx]
+    const double *lbnd, *ubnd;    // [3][nz]
+    const double *x0, *yref;      // [B][nx], [B][ystride]
+    double *xout, *uout;
+    int *status, *iters;
+    int *list_count, *list;       // instances whose unconstrained solution violates a bound
+};
+// per-stage table words for (nx, nu) (0: no compiled sf_kernel), its dynamic LDS bytes at horizon N
+int sf_table_words(int nx, int nu);
+size_t sf_lds_bytes(int nx, int nu, int N);
+hipError_t sf_launch(int nx, int nu, const SfParams &p, hipStream_t s);
+// the active-set finish of the instances sf_kernel listed (fp64; shapes and slot counts as fin32)
+bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, hipStream_t s);
+int fin64_resident(int nx, int nu, int nslot, int device);
 // compiled fast kernels: EPL slots per lane (0 if none for this shape)
 int cl_fast_epl(int nx, int nu);
 // largest active set of the fast path for the shape (oracle/cref.py WSMAX)

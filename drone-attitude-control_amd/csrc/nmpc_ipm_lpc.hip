@@ -2304,8 +2304,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
         }
         LPC_STICK(7);
     }
-    if (lmode) {
+    if (lmode && fused) {
         // the lean loop's state of the instance: its solution's active flags by slot, the next step
+        // (the fast general solve's list mode, cl_steps = 0, is a plain cold solve per listed instance)
         if (inst_ok) {
             for (int k = 0; k <= N; k++) {
                 if ((k == N && ul) || (k == 0 && xl)) continue;

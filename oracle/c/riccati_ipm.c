@@ -994,21 +994,24 @@ static void fast_free(fast_tables *f)
 /* element (k, i) is a decision variable of the QP (x_0 pinned; stage N has no inputs) */
 static int valid_el(int nx, int N, int k, int i) { return !(k == 0 && i < nx) && (k < N || i < nx); }
 
-/* tuning aid: env RIC_DEBUG_INST=<instance> prints the PDAS rounds of that instance (run with 1 thread) */
+/* tuning aid: env RIC_DEBUG_INST=<instance> prints the PDAS rounds of that instance (run with 1 thread);
+ * one flag per OpenMP thread (each thread sets it for the instance it is on) */
 static int ric_dbg = 0;
+#pragma omp threadprivate(ric_dbg)
 
 /* The fast finish of one step (mode 1). wf: the warm set (shifted flags, in), the set reached
  * (out). Returns 1 and the solution in z (clamped onto the bounds) when accepted, else why not:
  * -2 a set larger than WSMAX, -3 a non-positive diagonal of W (never for a decision variable), -4
  * polish_steps rounds without acceptance. Counts the active-set steps and the
  * FP64 work. */
+static int fast_finish_z0(const ocp_ref_desc *d, const fast_tables *f, signed char *wf, const double *z0, double *z,
+                          int *wsteps, double *flops, int wsmax, int rounds);
+
 static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double *x0, int t, signed char *wf,
                        double *z0, double *z, int *wsteps, double *flops, int wsmax, int rounds)
 {
     const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
     const double *vt = f->v + (size_t)t * ne;
-    int nbad = 0;
-    *wsteps = 0;
     for (int k = 0; k <= N; k++)
         for (int i = 0; i < nz; i++) {
             const int e = k * nz + i;
@@ -1019,6 +1022,17 @@ static int fast_finish(const ocp_ref_desc *d, const fast_tables *f, const double
             z0[e] = s;
             *flops += 2.0 * nx;
         }
+    return fast_finish_z0(d, f, wf, z0, z, wsteps, flops, wsmax, rounds);
+}
+
+/* fast_finish from a given unconstrained solution z0 (the closed loop's explicit form, or the general
+ * solve's recursion on the shared factorisation, riccati_ipm_solve_batch_fast) */
+static int fast_finish_z0(const ocp_ref_desc *d, const fast_tables *f, signed char *wf, const double *z0, double *z,
+                          int *wsteps, double *flops, int wsmax, int rounds)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
+    int nbad = 0;
+    *wsteps = 0;
     for (int ws = 0, first = 1; ws < rounds; first = 0) {
         int S[WSMAX], m = 0;
         for (int e = 0; e < ne; e++)
@@ -1651,5 +1665,136 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
     fast_free(f);
     if (counters)
         for (int i = 0; i < 10; i++) counters[i] += cnt[i];
+    return nfail;
+}
+
+/* ======================================================================================
+ * The general batched solve on the shared factorisation (TEST INFRASTRUCTURE / CPU BASELINE of
+ * `bench.py --mode solve`): what the engine's fp64 nmpc_solve runs (nmpc_solve_fast.hip sf_kernel +
+ * nmpc_cl_fast.hip fin64_kernel), one instance at a time. Per instance (its own x0 and yref window, the
+ * reference's set(k, 'yref') / solve() pattern, src/force_model/ocp.py:117-122, controller.py:29-32):
+ *   the unconstrained solution z_0 by the Riccati recursion on the shared factorisation (lqr_solve_ref:
+ *   gradient g = G yref, backward kff / p, forward u = kff + K x, x+ = A x + B u + c); done if every bound
+ *   holds to 1e-13; else fast_finish_z0's primal-dual active-set rounds on W from z_0's violations (at most
+ *   PDAS_ROUNDS), and when they do not settle, unless the interval certificate proves the QP infeasible,
+ *   the dual active-set fallback (gi_set) and one more PDAS run on its set (polish_steps rounds); what is
+ *   still unsolved (and the certified-infeasible QPs) takes solve_one cold (IPM + exact finish).
+ * counters (added): [0] solves, [1] unconstrained, [2] active-set accepted, [3] active-set steps and
+ * fallback iterations, [4] full solves, [5] failures, [6] FP64 flops of the paths taken, [7] Newton
+ * systems of the full solves.
+ * ====================================================================================== */
+/* the shared factorisation and W of the general solve (riccati_ipm_solve_batch_fast), built once per OCP */
+void *riccati_fast_tables_create(const ocp_ref_desc *d)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = (N + 1) * nz;
+    if (nx + nu > NZMAX || ne > NZMAX * 64) return NULL;
+    fast_tables *f = (fast_tables *)calloc(1, sizeof(fast_tables));
+    f->ne = ne;
+    f->K = (double *)malloc(sizeof(double) * N * nu * nx);
+    f->Fi = (double *)malloc(sizeof(double) * N * nu * nu);
+    f->P = (double *)malloc(sizeof(double) * N * nx * nx);
+    f->W = (double *)calloc((size_t)ne * ne, sizeof(double));
+    lqr_factor(d, f);
+    double *g = (double *)calloc(ne, sizeof(double)), *z = (double *)malloc(sizeof(double) * ne), e0[NZMAX];
+    for (int i = 0; i < nx; i++) e0[i] = 0.0;
+    for (int e1 = 0; e1 < ne; e1++) {
+        const int k1 = e1 / nz, r1 = e1 % nz;
+        if ((k1 == 0 && r1 < nx) || (k1 == N && r1 >= nx)) continue;
+        for (int e = 0; e < ne; e++) g[e] = e == e1;
+        lqr_solve_ref(d, f, g, e0, 0, z);
+        for (int e = 0; e < ne; e++) f->W[(size_t)e1 * ne + e] = (e < nx || (e / nz == N && e % nz >= nx)) ? 0.0 : -z[e];
+    }
+    free(g);
+    free(z);
+    return f;
+}
+
+void riccati_fast_tables_free(void *f) { fast_free((fast_tables *)f); }
+
+int riccati_ipm_solve_batch_fast(const ocp_ref_desc *d, const void *tables, int batch, const double *x0,
+                                 const double *yref, double *xout, double *uout, int *status, int *iters,
+                                 double *counters, int wsmax_in, int nthreads)
+{
+    const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ny = d->ny, nye = d->ny_e, ne = (N + 1) * nz;
+    if (!tables || nx + nu > NZMAX || nx < 1 || nu < 1 || N < 1 || ny != nz || nye != nx || ne > NZMAX * 64) return -1;
+    const size_t ystride = (size_t)N * ny + nye;
+    const fast_tables *f = (const fast_tables *)tables;
+    const double fi = f_iter(nx, nu, N);
+    const int wsmax = wsmax_in > 0 ? (wsmax_in < WSMAX ? wsmax_in : WSMAX) : 16;
+    double cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int nfail = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+    nthreads = 1;
+#endif
+#pragma omp parallel num_threads(nthreads) reduction(+ : nfail, cnt[:8])
+    {
+        const size_t S = (size_t)(N + 1) * nz;
+        double *buf = (double *)malloc(sizeof(double) * (9 * S + (size_t)N * (2 * nx + nu * nu + nx * nu + nu)) + S);
+        ws_t w;
+        w.z = buf; w.ll = w.z + S; w.lu = w.ll + S; w.dza = w.lu + S; w.dz = w.dza + S;
+        w.gc = w.dz + S; w.gf = w.gc + S; w.gh = w.gf + S;
+        w.re = w.gh + S; w.Pr = w.re + (size_t)N * nx; w.Luu = w.Pr + (size_t)N * nx;
+        w.Lxu = w.Luu + (size_t)N * nu * nu; w.lu_vec = w.Lxu + (size_t)N * nx * nu;
+        w.sg = w.lu_vec + (size_t)N * nu;
+        w.act = (signed char *)(w.sg + S);
+        double *g = (double *)malloc(sizeof(double) * ne), *z0 = (double *)malloc(sizeof(double) * ne),
+               *zf = (double *)malloc(sizeof(double) * ne);
+        signed char *wf = (signed char *)malloc(ne), *w0 = (signed char *)calloc(ne, 1);
+#pragma omp for schedule(dynamic, 16)
+        for (int b = 0; b < batch; b++) {
+            const double *xb = x0 + (size_t)b * nx, *yb = yref + (size_t)b * ystride;
+            double *xo = xout + (size_t)b * (N + 1) * nx, *uo = uout + (size_t)b * N * nu;
+            /* gradient G yref (stage-stacked; stage N: Ge yref_N) */
+            for (int k = 0; k <= N; k++) {
+                const int n = k < N ? nz : nx, m = k < N ? ny : nye;
+                const double *Gm = k < N ? d->G : d->Ge;
+                for (int i = 0; i < nz; i++) g[k * nz + i] = 0.0;
+                for (int i = 0; i < n; i++) {
+                    double s = 0.0;
+                    for (int q = 0; q < m; q++) s += Gm[i * m + q] * yb[(size_t)k * ny + q];
+                    g[k * nz + i] = s;
+                }
+                cnt[6] += 2.0 * n * m;
+            }
+            lqr_solve_ref(d, f, g, xb, 1, z0);
+            cnt[6] += N * (2.0 * nx * nx + 2.0 * nx * nz + 2.0 * nu * nu + 4.0 * nu * nx + 2.0 * nx * nz);
+            memset(wf, 0, (size_t)ne);
+            int wst = 0, git = 0, ok, it = 0, st = 0;
+            const int r0 = d->polish_steps < PDAS_ROUNDS ? d->polish_steps : PDAS_ROUNDS;
+            ok = fast_finish_z0(d, f, wf, z0, zf, &wst, &cnt[6], wsmax, r0) > 0;
+            it += wst;
+            if (!ok && infeasible_stage(d, xb) == 0) {
+                if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
+                    ok = fast_finish_z0(d, f, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
+                    it += wst;
+                }
+                it += git;
+            }
+            cnt[3] += it;
+            if (ok) {
+                cnt[it == 0 ? 1 : 2] += 1;
+                for (int k = 0; k <= N; k++) {
+                    for (int i = 0; i < nx; i++) xo[k * nx + i] = zf[k * nz + i];
+                    if (k < N)
+                        for (int i = 0; i < nu; i++) uo[k * nu + i] = zf[k * nz + nx + i];
+                }
+                it += 1;
+            } else {
+                st = solve_one(d, xb, yb, xo, uo, &it, &w, NULL, 0);
+                cnt[4] += 1;
+                cnt[7] += it;
+                cnt[6] += fi * it;
+            }
+            status[b] = st;
+            iters[b] = it;
+            cnt[0] += 1;
+            if (st) { cnt[5] += 1; nfail++; }
+        }
+        free(buf); free(g); free(z0); free(zf); free(wf); free(w0);
+    }
+    if (counters)
+        for (int i = 0; i < 8; i++) counters[i] += cnt[i];
     return nfail;
 }

@@ -129,6 +129,40 @@ class RiccatiIpmRef:
             raise ValueError("riccati_ipm_solve_batch rejected the problem dimensions")
         return X, U, st, it
 
+    def __del__(self):
+        if getattr(self, "_fast", None):
+            self.lib.riccati_fast_tables_free(ctypes.c_void_p(self._fast))
+            self._fast = None
+
+    def solve_fast(self, x0, yref, wsmax=16, nthreads=None):
+        """The engine's fp64 general solve, restated (riccati_ipm_solve_batch_fast): the unconstrained
+        solution on the shared factorisation, primal-dual active-set rounds on W from its violations, the
+        dual fallback, the full IPM + exact finish for what is left. Returns X, U, status, iters and the
+        counters {solves, unconstrained, set, set_steps, full, failed, flops, full_newton}."""
+        sp = self.spec
+        x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, sp.nx)
+        B = x0.shape[0]
+        yref = np.ascontiguousarray(yref, dtype=np.float64).reshape(B, -1)
+        assert yref.shape[1] == sp.N * sp.ny + sp.nx
+        X = np.zeros((B, sp.N + 1, sp.nx))
+        U = np.zeros((B, sp.N, sp.nu))
+        st = np.zeros(B, dtype=np.int32)
+        it = np.zeros(B, dtype=np.int32)
+        cnt = np.zeros(8)
+        p = lambda a: ctypes.c_void_p(a.ctypes.data)
+        if getattr(self, "_fast", None) is None:   # the factorisation and W, once per OCP (setup, untimed)
+            self.lib.riccati_fast_tables_create.restype = ctypes.c_void_p
+            self._fast = self.lib.riccati_fast_tables_create(ctypes.byref(self.desc))
+            if not self._fast:
+                raise ValueError("riccati_fast_tables_create rejected the problem dimensions")
+        rc = self.lib.riccati_ipm_solve_batch_fast(
+            ctypes.byref(self.desc), ctypes.c_void_p(self._fast), B, p(x0), p(yref), p(X), p(U), p(st), p(it), p(cnt), int(wsmax),
+            int(nthreads) if nthreads else self.max_threads())
+        if rc < 0:
+            raise ValueError("riccati_ipm_solve_batch_fast rejected the problem dimensions")
+        keys = ("solves", "unconstrained", "set", "set_steps", "full", "failed", "flops", "full_newton")
+        return X, U, st, it, dict(zip(keys, cnt.tolist()))
+
 
 class _ClDesc(ctypes.Structure):
     _fields_ = [

@@ -43,45 +43,72 @@ def rel_err(X, U, Xr, Ur):
     return err / scale
 
 
-def solve_batch(key, cases, precision="fp64", reps=1, ipw=None, kernel=None, structure=True):
+def solve_batch(key, cases, precision="fp64", reps=1, ipw=None, kernel=None, structure=True, fast=True, env=None):
     """kernel: None (default family: lane-per-component), "wave" (wavefront-per-instance,
-    with ipw instances per wavefront) or "lpc"; structure=False forces the dense
-    lane-per-component kernel instead of the model-structure-specialised one."""
+    with ipw instances per wavefront) or "lpc" — an explicit family also selects that family's full
+    IPM for the solve; structure=False forces the dense lane-per-component kernel instead of the
+    model-structure-specialised one. fast=False: the full IPM + exact finish instead of the fp64 fast
+    solve (sf_kernel + fin64_kernel, NMPC_SOLVE_FAST=0). env: extra environment for the handle's
+    lifetime (read at create and at each solve)."""
     name, N = split(key)
     x0 = np.tile(cases[key + "_x0"], (reps, 1))
     y = np.tile(cases[key + "_yref"], (reps, 1))
+    set_env = dict(env or {})
     if ipw:
-        os.environ["NMPC_IPW"] = str(ipw)
+        set_env["NMPC_IPW"] = str(ipw)
     if kernel:
-        os.environ["NMPC_KERNEL"] = kernel
+        set_env["NMPC_KERNEL"] = kernel
     if not structure:
-        os.environ["NMPC_STRUCT"] = "0"
+        set_env["NMPC_STRUCT"] = "0"
+    if not fast:
+        set_env["NMPC_SOLVE_FAST"] = "0"
+    os.environ.update(set_env)
     try:
         s = AcadosOcpSolver(OCPS[name](N), batch=x0.shape[0], precision=precision)
+        s.set_batch("x0", x0)
+        s.set_batch("yref", y)
+        st = s.solve()
     finally:
-        os.environ.pop("NMPC_IPW", None)
-        os.environ.pop("NMPC_KERNEL", None)
-        os.environ.pop("NMPC_STRUCT", None)
-    s.set_batch("x0", x0)
-    s.set_batch("yref", y)
-    st = s.solve()
+        for k_ in set_env:
+            os.environ.pop(k_, None)
     return s, st
+
 
 
 @pytest.mark.parametrize("key", KEYS)
 def test_batch_parity_fp64(key, cases):
-    s, st = solve_batch(key, cases)
-    assert st == 0
-    X, U = s.get_batch("x"), s.get_batch("u")
-    e = rel_err(X, U, cases[key + "_X"], cases[key + "_U"])
-    assert e.max() < TOL64, e.max()
-    # same algorithm as the C baseline: iteration counts agree (+-1 from rounding order)
+    """The fp64 solve (the fast path: unconstrained solution on the shared factorisation, sf_kernel, then the
+    active-set finish, fin64_kernel) against the certified oracle, with the same Newton-system counts as the C
+    restatement of that algorithm (riccati_ipm_solve_batch_fast) — and the full IPM + exact finish
+    (NMPC_SOLVE_FAST=0) with the counts of the C cold solve (+-1 from rounding order)."""
     name, N = split(key)
     o = OCPS[name](N).solver_options   # the OCP's IPM tolerances (quad13 sets its own) + exact finish
     R = cref.RiccatiIpmRef.for_options(models.MODELS[name](N), o)
-    _, _, stc, itc = R.solve(cases[key + "_x0"], cases[key + "_yref"])
-    it = s.get_batch_int("qp_iter")
-    assert np.abs(it - itc).max() <= 1, (it, itc)
+    for fast in (True, False):
+        s, st = solve_batch(key, cases, fast=fast)
+        assert st == 0
+        assert s.launch_info()["solve_kernel"] == ("sf_kernel" if fast else s.launch_info()["kernel"])
+        X, U = s.get_batch("x"), s.get_batch("u")
+        e = rel_err(X, U, cases[key + "_X"], cases[key + "_U"])
+        assert e.max() < TOL64, (fast, e.max())
+        if fast:
+            _, _, stc, itc, cnt = R.solve_fast(cases[key + "_x0"], cases[key + "_yref"], wsmax=cref.WSMAX[name])
+            assert cnt["full"] == 0
+        else:
+            _, _, stc, itc = R.solve(cases[key + "_x0"], cases[key + "_yref"])
+        it = s.get_batch_int("qp_iter")
+        assert np.abs(it - itc).max() <= (0 if fast else 1), (fast, it, itc)
+
+
+@pytest.mark.parametrize("key", ["force_N20", "jerk_N40", "quad13_N20"])
+def test_fast_solve_parks_take_the_full_solve(key, cases):
+    """The fast solve's last resort: with the dual fallback off (NMPC_CLF_NO_GI=1) every instance whose PDAS
+    rounds do not settle parks, and the full IPM (ipm_lpc_kernel in list mode, cold) solves it; the batch still
+    matches the certified oracle, and the parked instances carry the full solve's Newton-system counts."""
+    s, st = solve_batch(key, cases, env={"NMPC_CLF_NO_GI": "1"})
+    assert st == 0 and s.launch_info()["solve_kernel"] == "sf_kernel"
+    e = rel_err(s.get_batch("x"), s.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
+    assert e.max() < TOL64, e.max()
 
 
 @pytest.mark.parametrize("key", ["force_N20", "jerk_N40"])
@@ -385,7 +412,7 @@ def test_plant_simulator_matches_oracle():
             assert np.allclose(ss.simulate(x=x, u=u), ref(x, u, T), rtol=1e-13, atol=1e-15)
 
 
-@pytest.mark.parametrize("kernel", ["lpc", "wave"])
+@pytest.mark.parametrize("kernel", ["lpc", "wave", None])
 def test_factorisation_failure_keeps_last_iterate(kernel, cases, golden_dir):
     """A closed-loop jerk instance pushed past the position bound (tests/golden/qp_failure.npz,
     make_failure_case.py): x_1 cannot be feasible, F_uu loses positive definiteness at the C
@@ -395,7 +422,10 @@ def test_factorisation_failure_keeps_last_iterate(kernel, cases, golden_dir):
     key = "jerk_N40"
     x0 = np.vstack([f[key + "_x0"], cases[key + "_x0"][:3]])
     y = np.vstack([f[key + "_yref"], cases[key + "_yref"][:3]])
-    os.environ["NMPC_KERNEL"] = kernel
+    # kernel None: the fp64 fast solve, whose active-set finish cannot settle this QP (the dual fallback finds
+    # it infeasible, the certificate does not prove it), so it parks and takes the full IPM in list mode
+    if kernel:
+        os.environ["NMPC_KERNEL"] = kernel
     try:
         s = AcadosOcpSolver(OCPS["jerk"](40), batch=4)
     finally:
@@ -416,12 +446,14 @@ def test_factorisation_failure_keeps_last_iterate(kernel, cases, golden_dir):
     assert rel_err(X[1:], U[1:], cases[key + "_X"][:3], cases[key + "_U"][:3]).max() < TOL64
 
 
-@pytest.mark.parametrize("kernel", ["lpc", "wave"])
+@pytest.mark.parametrize("kernel", ["lpc", "wave", None])
 @pytest.mark.parametrize("name,N", [("jerk", 40), ("quad13", 20)])
 def test_infeasibility_certificate_on_gpu(kernel, name, N, golden_dir):
     """Closed-loop QPs past a position bound (tests/golden/qp_infeasible.npz): the kernels' interval
     certificate ends them before the first iteration — status 4, 0 iterations, the oracle's
-    initial point — next to feasible instances of the same launch that solve normally."""
+    initial point — next to feasible instances of the same launch that solve normally. kernel None: the
+    fp64 fast solve, whose finish (fin64_kernel) runs the same certificate and parks such an instance for
+    the full solve's list mode, which returns that status and initial point."""
     f = np.load(os.path.join(golden_dir, "qp_infeasible.npz"))
     d = np.load(os.path.join(golden_dir, "qp_cases.npz"))
     key = f"{name}_N{N}"
@@ -429,7 +461,8 @@ def test_infeasibility_certificate_on_gpu(kernel, name, N, golden_dir):
     n = f[key + "_x0"].shape[0]
     x0 = np.vstack([f[key + "_x0"], d[gkey + "_x0"][:3]]) if gkey == key else f[key + "_x0"]
     y = np.vstack([f[key + "_yref"], d[gkey + "_yref"][:3]]) if gkey == key else f[key + "_yref"]
-    os.environ["NMPC_KERNEL"] = kernel
+    if kernel:
+        os.environ["NMPC_KERNEL"] = kernel
     try:
         s = AcadosOcpSolver(OCPS[name](N), batch=x0.shape[0])
     finally:
