@@ -86,7 +86,9 @@ class ClosedLoop:
     """Device closed loop of `batch` instances of `model` on one GPU."""
 
     def __init__(self, model, batch, N=None, device=0, precision="fp64", table=None, offsets=None,
-                 x_init=None, instance_base=0, seed=42, noise_std=None, noise_table=None):
+                 x_init=None, instance_base=0, seed=42, noise_std=None, noise_table=None, cost_stage=None):
+        """cost_stage: the state the closed-loop cost is taken at (0: x_0 as force_model/controller.py:39,
+        1: x_1 as jerk_model/controller.py:39); default by model."""
         self.model = model
         self.N = N or DEFAULT_N[model]
         self.batch = batch
@@ -115,7 +117,7 @@ class ClosedLoop:
             keep["noise"] = np.ascontiguousarray(noise_table, dtype=np.float64).reshape(batch, -1)
             d.noise_table = _lib.dptr(keep["noise"])
             d.noise_len = keep["noise"].shape[1]
-        d.cost_stage = 1 if model == "jerk" else 0
+        d.cost_stage = (1 if model == "jerk" else 0) if cost_stage is None else int(cost_stage)
         if model == "quad13":
             w = np.array([1e2] * 3 + [1e0] * 3)
         else:

@@ -1041,12 +1041,14 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     h->off_lb = carve(3 * nz);
     h->off_ub = carve(3 * nz);
     // the unconstrained factorisation's tables (lqr_table, lqr_wmat) serve the exact finish's shortcuts of
-    // the stage-wise kernels (fp64 handles with the finish on: polish_mu > 0) and the lean closed loop
-    // (W and the explicit solution's tables, both precisions; fp32 handles' solves never read them)
+    // the stage-wise kernels and the fast solve (fp64 handles with the finish on: polish_mu > 0) and, from
+    // the host copy, the lean closed loop's tables in both precisions. fp32 handles keep only the host copy:
+    // their kernels never read the device tables (the lean loop and the fp32 finish use the fp64 W, d_clw)
     const bool lqr_on = !h->cond && (!f64 || h->polish_mu > 0);
-    h->off_lqr = carve(lqr_on ? (size_t)N * nz * lqr_words(nx, nu) : 0);
-    h->off_lqrf = carve(lqr_on ? (size_t)N * nz * lqrf_words(nx, nu) : 0);
-    h->off_lqrw = carve(lqr_on ? (size_t)(N + 1) * nz * (N + 1) * nz : 0);
+    const bool lqr_dev = lqr_on && f64;
+    h->off_lqr = carve(lqr_dev ? (size_t)N * nz * lqr_words(nx, nu) : 0);
+    h->off_lqrf = carve(lqr_dev ? (size_t)N * nz * lqrf_words(nx, nu) : 0);
+    h->off_lqrw = carve(lqr_dev ? (size_t)(N + 1) * nz * (N + 1) * nz : 0);
     const size_t model_bytes = off;
     if (h->cond) {
         if (!nmpc::cond_build(nx, nu, N, ny, ny_e, h->A, h->B, h->c, h->H, h->G, h->He, h->Ge, h->lbnd, h->ubnd, h->ch)) {
@@ -1129,11 +1131,13 @@ int nmpc_create(const nmpc_ocp_desc *d, int batch, int device, int precision, nm
     if (lqr_on) {
         std::vector<double> &lqr = h->lqr_host, lqrf;
         lqr_table(nx, nu, N, h->A, h->B, h->c, h->H, h->He, lqr, lqrf);
-        put(h->off_lqr, lqr);
-        put(h->off_lqrf, lqrf);
-        std::vector<double> wm;
-        lqr_wmat(nx, nu, N, h->A, h->B, lqr, wm);
-        put(h->off_lqrw, wm);
+        if (lqr_dev) {
+            put(h->off_lqr, lqr);
+            put(h->off_lqrf, lqrf);
+            std::vector<double> wm;
+            lqr_wmat(nx, nu, N, h->A, h->B, lqr, wm);
+            put(h->off_lqrw, wm);
+        }
     }
     if (h->cond) {
         const nmpc::CondHost &c = h->ch;
@@ -2047,7 +2051,9 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     // shape's lockstep variant is opt-in (NMPC_CLF_LOCK=1): its 20 tiles of z and v_t spill 130 VGPRs at 2 waves
     // per SIMD and it measured 200-202M against cl_fast_kernel's 253M steps/s (jerk B = 4096, tools/ab_check.sh lk4)
     const bool jerk = nx == 6 && nu == 2;
-    const bool lock = f64 && nmpc::cl_lock_shape(nx, nu) && d.cost_stage <= 1 &&
+    // (the cost on x_1, cost_stage 1, is gathered from the MFMA tiles by the jerk variant only: other shapes with
+    // cost_stage 1 run cl_fast_kernel)
+    const bool lock = f64 && nmpc::cl_lock_shape(nx, nu) && (d.cost_stage == 0 || (jerk && d.cost_stage == 1)) &&
                       (d.plant == NMPC_PLANT_MODEL || (jerk && d.plant == NMPC_PLANT_CRAZYFLIE_JERK)) &&
                       (jerk ? (lenv && lenv[0] == '1') : !(lenv && lenv[0] == '0'));
     // W over the slots in LDS for the shapes that have the variant, env NMPC_CLF_WLDS=1 (tuning; off by default:
@@ -2143,7 +2149,9 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     // one wavefront per workgroup starts in phase 2 (drains demoted instances while the others still run
     // lockstep): quad13 B = 8192 415M (0) -> 458-463M (1), 452-457M (2), 405-412M (3) steps/s (tools/lock_ab.sh, ab1/ab2)
     // (the jerk shape's lockstep variant, four wavefronts per workgroup and rarely a demotion: none)
-    p.lock_workers = lw ? std::max(0, std::min(4, std::atoi(lw))) : (h->nx == 6 && h->nu == 2 ? 0 : 1);
+    // (at most the variant's wavefronts per workgroup minus one, so some wavefront runs phase 1: quad13 8, jerk 4)
+    const int lock_wpb = (h->nx == 6 && h->nu == 2) ? 4 : 8;
+    p.lock_workers = lw ? std::max(0, std::min(lock_wpb - 1, std::atoi(lw))) : (h->nx == 6 && h->nu == 2 ? 0 : 1);
     const char *lp = std::getenv("NMPC_LOCK_PRIO");
     p.lock_prio = lp ? (lp[0] == '1') : 1;
     // the force shape claims its instances device-wide (env NMPC_CLF_GCLAIM=0 / 1 overrides)

@@ -201,7 +201,7 @@ class ClosedLoopRef:
 
     def __init__(self, spec, model, table, offsets, x_init, mode=0, noise_table=None, seed=42, instance_base=0,
                  noise_std=None, tol_comp=None, tol_res=None, polish_mu=DEFAULT_POLISH_MU,
-                 polish_steps=DEFAULT_POLISH_STEPS, period=None, instance_ids=None):
+                 polish_steps=DEFAULT_POLISH_STEPS, period=None, instance_ids=None, cost_stage=None):
         from . import params as P
         self.ipm = RiccatiIpmRef(spec, tol_comp=tol_comp or 1e-15, tol_res=tol_res or 1e-12, polish_mu=polish_mu,
                                  polish_steps=polish_steps)
@@ -226,7 +226,7 @@ class ClosedLoopRef:
         d.table = keep["table"].ctypes.data
         d.rows, d.cols = keep["table"].shape
         d.period = int(period or P.N_SIM)
-        d.cost_stage = 1 if model == "jerk" else 0
+        d.cost_stage = (1 if model == "jerk" else 0) if cost_stage is None else int(cost_stage)
         d.ncl = keep["wcl"].size
         d.aed_dims = 3 if model == "quad13" else 2
         d.noise_dims = 6 if model == "quad13" else nx

@@ -112,6 +112,35 @@ def test_jerk_lockstep_variant_matches_oracle():
 
 
 @pytest.mark.timeout(300)
+def test_quad13_cost_on_x1_runs_the_single_instance_loop():
+    """quad13 with the closed-loop cost on x_1 (cost_stage 1, the jerk loop's choice, jerk_model/controller.py:39):
+    the lockstep kernel gathers x_1 for the jerk shape only, so this configuration runs cl_fast_kernel, and its
+    per-instance cost sums (taken at x_1) match the C restatement (mode 1, cost_stage 1) over a ragged batch of
+    1030 and 23 steps (3 + 20); the cost differs from the x_0 loop's (the lockstep path once charged
+    it at x_0 silently)."""
+    from drone_attitude_control_amd.batched import ClosedLoop, workload
+    from oracle import cref, models
+    from drone_attitude_control_amd.models import OCPS
+    cl = ClosedLoop("quad13", 1030, N=20, seed=9, cost_stage=1)
+    assert cl.solver.launch_info()["closed_loop_kernel"] == "cl_fast_kernel"
+    cl.run(3)
+    cl.run(20)
+    x, acc = cl.state(), cl.instance_stats()
+    table, off, x0 = workload("quad13", 20, 1030, 9)
+    o = OCPS["quad13"](20).solver_options
+    ref = cref.ClosedLoopRef(models.quad13_model(20), "quad13", table, off, x0, mode=1, seed=9, cost_stage=1,
+                             tol_comp=o.qp_solver_tol_comp, tol_res=o.qp_solver_tol_stat)
+    ref.run(23)
+    assert _rel(x, ref.state).max() < 1e-6, _rel(x, ref.state).max()
+    assert np.array_equal(acc[:, 2:], ref.acc[:, 2:])
+    np.testing.assert_allclose(acc[:, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
+    ref0 = cref.ClosedLoopRef(models.quad13_model(20), "quad13", table, off, x0, mode=1, seed=9, cost_stage=0,
+                              tol_comp=o.qp_solver_tol_comp, tol_res=o.qp_solver_tol_stat)
+    ref0.run(23)
+    assert np.abs(ref0.acc[:, 0] - acc[:, 0]).max() > 1e-6
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("model,N,B", [("quad13", 20, 4096), ("jerk", 40, 2048)])
 def test_claim_order_changes_only_the_schedule(model, N, B):
     """The lean loop's claim order (NMPC_CLF_ORDER, read per run: the previous launch's warm-start and
