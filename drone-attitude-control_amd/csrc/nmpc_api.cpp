@@ -245,8 +245,15 @@ struct nmpc_solver {
     int *d_f64i = nullptr;                 // s_e, s_free
     size_t f64i[2] = {0, 0};
     int f64_nslot = 0, f64_nfree = 0, f64_resident = 0;
-    int *d_sfl = nullptr;                  // [0] listed count, [1] parked count, [2..2+B) list, [2+B..2+2B) parked
-    int *h_sfpark = nullptr;               // pinned: the parked count of the last fast solve
+    int *d_sfl = nullptr;                  // [0..4) two [listed, parked] counter pairs (solve i uses pair i & 1; its
+                                           // fin64_kernel zeroes the other), [4..4+B) list, [4+B..4+2B) parked
+    int sf_pair = 0;                       // the counter pair of the last fast solve
+    int sf_hint = 0;                       // listed instances of the last resolved fast solve (fin64's grid)
+    bool sf_fin_done = false;              // the last fast solve launched its finish (else sf_resolve does)
+    nmpc::ClFastParams<double> sf_fin{};   // ... and its parameters
+    int *h_sfpark = nullptr;               // pinned: the last resolved solve's [listed, parked] counts
+    unsigned long long *d_sfcyc = nullptr; // timing builds (env NMPC_SF_CYCLES): sf_kernel's phase clocks
+    size_t sfcyc_n = 0;
     int sf_kidx = -1;                      // lane-per-component kernel of the parked instances' full solves
     void *d_sf_scratch = nullptr;          // its scratch when the handle's own family is another
     hipEvent_t ev_fb = nullptr;            // start of the parked instances' full solve
@@ -524,7 +531,7 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
                     (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw,
                     (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0, (void *)h->d_sf, (void *)h->d_f64,
-                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch})
+                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch, (void *)h->d_sfcyc})
         if (p) hipFree(p);
     if (h->h_sfpark) hipHostFree(h->h_sfpark);
     if (h->ev_fb) hipEventDestroy(h->ev_fb);
@@ -1768,7 +1775,7 @@ int sf_setup(nmpc_solver *h)
     const int bpg = nx <= 4 ? 1 : (nx <= 8 ? 2 : 4), R = 4 * bpg;
     const int o_aclt = 0, o_kt = o_aclt + bpg * R * 4, o_fibt = o_kt + R * 4, o_nfi = o_fibt + bpg * 16, o_kk = o_nfi + 16,
               o_cp = o_kk + bpg * 16, o_cf = o_cp + R;
-    if (o_cf + 4 != ts) return h->fail(NMPC_EUNSUPPORTED, "sf_setup: table layout mismatch");
+    if (o_cf + 4 + 2 != ts) return h->fail(NMPC_EUNSUPPORTED, "sf_setup: table layout mismatch");   // + zero word, pad
     std::vector<double> tab((size_t)N * ts, 0.0), K((size_t)nu * nx), Fi((size_t)nu * nu), Pc(nx), Acl((size_t)nx * nx),
         FiBt((size_t)nu * nx);
     for (int k = 0; k < N; k++) {
@@ -1841,7 +1848,7 @@ int sf_setup(nmpc_solver *h)
     if (hipMalloc((void **)&h->d_sf, (h->sf_gd + gd.size()) * sizeof(double)) != hipSuccess ||
         hipMalloc((void **)&h->d_f64, ftot * sizeof(double)) != hipSuccess ||
         hipMalloc((void **)&h->d_f64i, itot * sizeof(int)) != hipSuccess ||
-        hipMalloc((void **)&h->d_sfl, (2 + 2 * (size_t)h->batch) * sizeof(int)) != hipSuccess ||
+        hipMalloc((void **)&h->d_sfl, (4 + 2 * (size_t)h->batch) * sizeof(int)) != hipSuccess ||
         (sc && hipMalloc(&h->d_sf_scratch, sc) != hipSuccess) ||
         hipHostMalloc((void **)&h->h_sfpark, 4 * sizeof(int), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&h->ev_fb) != hipSuccess)
@@ -1852,8 +1859,10 @@ int sf_setup(nmpc_solver *h)
         if (!fp[i]->empty()) e = hipMemcpy(h->d_f64 + h->f64o[i], fp[i]->data(), fp[i]->size() * sizeof(double), hipMemcpyHostToDevice);
     for (int i = 0; i < 2 && e == hipSuccess; i++)
         if (!ipp[i]->empty()) e = hipMemcpy(h->d_f64i + h->f64i[i], ipp[i]->data(), ipp[i]->size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(h->d_sfl, 0, 4 * sizeof(int));
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_create: fast-solve upload");
-    h->h_sfpark[0] = 0;
+    h->h_sfpark[0] = h->h_sfpark[1] = 0;
+    h->sf_hint = h->batch;   // the first solve's finish runs on every resident workgroup
     h->f64_nslot = (int)el.size();
     h->f64_nfree = (int)fr.size();
     h->f64_resident = res;
@@ -1885,8 +1894,10 @@ int sf_enqueue(nmpc_solver *h)
     sp.uout = (double *)h->d_u;
     sp.status = h->d_status;
     sp.iters = h->d_iters;
-    sp.list_count = h->d_sfl;
-    sp.list = h->d_sfl + 2;
+    h->sf_pair ^= 1;
+    int *cnt = h->d_sfl + 2 * h->sf_pair;
+    sp.list_count = cnt;
+    sp.list = h->d_sfl + 4;
     nmpc::ClFastParams<double> p{};
     p.B = h->batch;
     p.N = h->N;
@@ -1911,19 +1922,32 @@ int sf_enqueue(nmpc_solver *h)
     p.uout = sp.uout;
     p.status = h->d_status;
     p.iters = h->d_iters;
-    p.park_count = h->d_sfl + 1;
-    p.park_list = h->d_sfl + 2 + h->batch;
+    p.park_count = cnt + 1;
+    p.park_list = h->d_sfl + 4 + h->batch;
     p.x0in = sp.x0;
     p.work_list = sp.list;
-    p.work_count = sp.list_count;
+    p.work_count = cnt;
     p.z0_xu = 1;
+    sp.next_counts = h->d_sfl + 2 * (h->sf_pair ^ 1);
+    // env NMPC_SF_CYCLES=<file> with a timing build (-DNMPC_SF_TIMING): per-wavefront phase clocks of this launch,
+    // appended to <file> at the next sf_resolve ([waves][8] uint64, tools/sf_phases.py)
+    static const char *sf_cyc = std::getenv("NMPC_SF_CYCLES");
+    if (sf_cyc && !h->d_sfcyc) {
+        h->sfcyc_n = (size_t)(h->batch + 3) / 4 * 8 * 2;   // >= wavefronts x 8 for every shape (<= 4 instances per wave)
+        if (hipMalloc((void **)&h->d_sfcyc, h->sfcyc_n * sizeof(unsigned long long)) != hipSuccess) h->d_sfcyc = nullptr;
+    }
+    sp.cycles = h->d_sfcyc;
     hipEventRecord(h->ev0, h->stream);
-    hipError_t e = hipMemsetAsync(h->d_sfl, 0, 2 * sizeof(int), h->stream);
-    if (e == hipSuccess) e = nmpc::sf_launch(nx, nu, sp, h->stream);
-    if (e == hipSuccess) e = nmpc::fin64_launch(nx, nu, p, h->f64_resident, h->stream) ? hipGetLastError() : hipErrorInvalidValue;
+    hipError_t e = nmpc::sf_launch(nx, nu, sp, h->stream);
+    // the finish only when the last resolved solve listed instances: a launch whose every workgroup exits at once
+    // still costs ~4 us (rocprofv3, quad13 B = 8192, where no first-step QP is listed). A skipped finish with a
+    // non-empty list runs in sf_resolve, before anything reads the outputs
+    h->sf_fin_done = h->sf_hint > 0;
+    if (e == hipSuccess && h->sf_fin_done)
+        e = nmpc::fin64_launch(nx, nu, p, h->f64_resident, h->sf_hint, h->stream) ? hipGetLastError() : hipErrorInvalidValue;
     hipEventRecord(h->ev1, h->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(h->h_sfpark, h->d_sfl + 1, sizeof(int), hipMemcpyDeviceToHost, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "fast solve launch");
+    h->sf_fin = p;
     h->sf_pending = true;
     return 0;
 }
@@ -1935,11 +1959,32 @@ int sf_resolve(nmpc_solver *h)
 {
     if (!h->sf_pending) return 0;
     h->sf_pending = false;
-    hipError_t e = hipStreamSynchronize(h->stream);
+    // the last solve's counter pair (its finish zeroed only the other one), read once the stream has drained
+    hipError_t e = hipMemcpyAsync(h->h_sfpark, h->d_sfl + 2 * h->sf_pair, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "fast solve");
-    const int parked = h->h_sfpark[0];
+    h->sf_hint = h->h_sfpark[0];
+    if (!h->sf_fin_done && h->sf_hint > 0) {   // the finish this solve skipped: now, timed into its event pair
+        hipEventRecord(h->ev_fb, h->stream);
+        if (!nmpc::fin64_launch(h->nx, h->nu, h->sf_fin, h->f64_resident, h->sf_hint, h->stream))
+            return h->fail(NMPC_EDEVICE, "fast solve: finish launch");
+        hipEventRecord(h->ev1, h->stream);
+        e = hipMemcpyAsync(h->h_sfpark, h->d_sfl + 2 * h->sf_pair, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return hip_fail(h, e, "fast solve finish");
+    }
+    if (h->d_sfcyc) {
+        static const char *sf_cyc = std::getenv("NMPC_SF_CYCLES");
+        std::vector<unsigned long long> cy(h->sfcyc_n);
+        if (hipMemcpy(cy.data(), h->d_sfcyc, cy.size() * sizeof(cy[0]), hipMemcpyDeviceToHost) == hipSuccess)
+            if (FILE *f = std::fopen(sf_cyc, "ab")) {
+                std::fwrite(cy.data(), sizeof(cy[0]), cy.size(), f);
+                std::fclose(f);
+            }
+    }
+    const int parked = h->h_sfpark[1];
     if (parked <= 0) return 0;
-    const ListArgs la{parked, 0, 0, h->d_sfl + 2 + h->batch, h->sf_kidx, h->d_sf_scratch};
+    const ListArgs la{parked, 0, 0, h->d_sfl + 4 + h->batch, h->sf_kidx, h->d_sf_scratch};
     return launch<double>(h, h->ev_fb, h->ev1, 0, &la);
 }
 

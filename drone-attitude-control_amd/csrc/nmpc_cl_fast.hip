@@ -2204,11 +2204,12 @@ int fin64_resident(int nx, int nu, int nslot, int device)
     return res;
 }
 
-// grid: the resident workgroups (the list's length is known on the device only; idle workgroups exit at once)
-bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, hipStream_t s)
+// grid: enough workgroups for `hint` listed instances (the host's last observation: the list's length is known on
+// the device only), at most the resident ones; the persistent loop covers any longer list, idle workgroups exit
+bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, int hint, hipStream_t s)
 {
     return fin64_dispatch(nx, nu, p.nslot, [&](auto k, int wpb) {
-        const int blocks = std::max(1, std::min((p.B + wpb - 1) / wpb, resident));
+        const int blocks = std::max(1, std::min((std::min(hint, p.B) + wpb - 1) / wpb, resident));
         hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, s, p);
     });
 }

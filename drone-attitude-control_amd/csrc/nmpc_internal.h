@@ -176,13 +176,15 @@ struct SfParams {
     double *xout, *uout;
     int *status, *iters;
     int *list_count, *list;       // instances whose unconstrained solution violates a bound
+    int *next_counts;             // the next solve's [list, park] counters, zeroed by workgroup 0 (or null)
+    unsigned long long *cycles;   // diagnostic builds (NMPC_SF_TIMING): [waves][8] phase clocks, or null
 };
 // per-stage table words for (nx, nu) (0: no compiled sf_kernel), its dynamic LDS bytes at horizon N
 int sf_table_words(int nx, int nu);
 size_t sf_lds_bytes(int nx, int nu, int N);
 hipError_t sf_launch(int nx, int nu, const SfParams &p, hipStream_t s);
 // the active-set finish of the instances sf_kernel listed (fp64; shapes and slot counts as fin32)
-bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, hipStream_t s);
+bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, int hint, hipStream_t s);
 int fin64_resident(int nx, int nu, int nslot, int device);
 // compiled fast kernels: EPL slots per lane (0 if none for this shape)
 int cl_fast_epl(int nx, int nu);

@@ -69,12 +69,31 @@ void run(const char *name, F kern, int per_iter, int wpb)
     (void)hipFree(o);
     (void)hipFree(c);
 }
+// a dependent chain through a lane permute (the D -> B layout change of the sweeps): mfma, then the result
+// through ds_bpermute, as the next mfma's B operand
+__global__ void rchain(double *out, long long *cyc, int iters)
+{
+    double acc = threadIdx.x, x = 1.0;
+    const double a = threadIdx.x * 1e-3;
+    const int src = (threadIdx.x & 0x33) | (1 << 2);
+    const long long t0 = clock64();
+    for (int it = 0; it < iters; it++) {
+        acc = __builtin_amdgcn_mfma_f64_4x4x4f64(a, x, acc, 0, 0, 0);
+        x = __shfl(acc, src);
+    }
+    const long long t1 = clock64();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc + x;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
 int main()
 {
     for (int wpb : {4, 8}) {
         run("mfma_f64_4x4x4_4b x16", r44<16>, 16, wpb);
+        run("mfma_f64_4x4x4_4b dep", r44<1>, 1, wpb);
         run("mfma_f64_16x16x4 x8", r16<8>, 8, wpb);
+        run("mfma_f64_16x16x4 dep", r16<1>, 1, wpb);
         run("v_fma_f64 x16 indep", rfma<16>, 16, wpb);
+        run("mfma4x4 -> bpermute dep", rchain, 1, wpb);
     }
     return 0;
 }
