@@ -318,7 +318,10 @@ def main():
         fl_step = flops_cpu if flops_cpu is not None else 2.0 * nx * (ne_ - nx - nu) + 2.0 * nx * nz_
         fl_launch = fl_step * B
         achieved = fl_launch / (kernel_ms * 1e-3) / 1e12
-        peak = PEAK_TFLOPS[args.precision]
+        # the pipe the credited flops run on: an fp32 handle on the lean loop does its credited work (active-set
+        # solves, W combinations, acceptance) in fp64 — the PMC passes count ~20x more FP64 than FP32 flops there
+        arith = "fp64" if args.precision == "fp64" or lean else "fp32"
+        peak = PEAK_TFLOPS[arith]
         kernel = info["closed_loop_kernel"] if info["closed_loop_kernel"] != "fused" else info["kernel"]
         spl = min(args.steps, 64)   # steps per launch of the timed regions (clf_run / fused chunks)
         pmc = load_pmc(model, N, B, args.precision, kernel, spl)
@@ -354,8 +357,10 @@ def main():
                                                           "time is set by its slowest wavefront; region-to-region "
                                                           "differences below the IQR are not resolved"),
                            steps_per_region=args.steps),
-            "roofline": {"bound": "valu_fp64" if args.precision == "fp64" else "valu_fp32",
-                         "pipe": ("FP64 FMA on the VALU" if args.precision == "fp64" else "FP32 FMA on the VALU")
+            "roofline": {"bound": "valu_fp64" if arith == "fp64" else "valu_fp32",
+                         "pipe": ("FP64 FMA on the VALU" if arith == "fp64" else "FP32 FMA on the VALU")
+                         + (" (fp32 handle: the credited active-set arithmetic runs in fp64)"
+                            if arith != args.precision else "")
                          + " (MI355X: FP64 matrix peak = FP64 vector peak; FP32 matrix peak = FP32 vector peak)",
                          "kernel": kernel, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak,
@@ -375,12 +380,14 @@ def main():
                          "traffic": traffic,
                          "min_bytes_per_step": min_b,
                          "traffic_vs_min_bytes": traffic / min_b if traffic else None,
-                         "traffic_note": "FETCH_SIZE + WRITE_SIZE per closed-loop step (per launch / steps per launch) "
-                                         f"from the committed rocprofv3 PMC pass on launches of {spl} steps "
-                                         f"({pmc.get('source', 'none for this config and launch length')}); no x2 "
-                                         "FETCH_SIZE correction: the kernel's loads are 4/8-B per lane, the guide's x2 "
-                                         "is calibrated for 16-B streams; includes Infinity-Cache hits. min_bytes: x0 + "
-                                         "offset in, u0 + x1 out per instance (shared reference table)",
+                         "traffic_note": "2 x FETCH_SIZE + WRITE_SIZE per closed-loop step (per launch / steps per "
+                                         f"launch) from the committed rocprofv3 PMC pass on launches of {spl} steps "
+                                         f"({pmc.get('source', 'none for this config and launch length')}); FETCH_SIZE x 2 "
+                                         "is the gfx950 correction (MI355X_MICROARCH.md), calibrated for these 8-B "
+                                         "coalesced loads on sf_kernel's known byte count (tools/pmc_summary.py); "
+                                         "includes Infinity-Cache hits. min_bytes: x0 + offset in, u0 + x1 out per "
+                                         "instance-step; the shared tables (v_t, T_x, W), which every XCD's L2 pulls "
+                                         "once per launch, are not in it",
                          "gpu_mean_qp_iter": st["mean_qp_iter"]},
             "kernel_only": {"value": world * B / (kernel_ms * 1e-3), "unit": "NMPC steps/s",
                             "note": "closed-loop kernel time only (median of the regions' launch durations, HIP "
@@ -408,7 +415,8 @@ def main_solve(args, world, rank, dist, device):
     NMPC_SOLVE_FAST=0 (or fp32): the full IPM + exact finish for every QP. The QPs are the closed loop's
     first-step QPs of the bench workload (batched.first_step_qps). A step = one batched solve."""
     from drone_attitude_control_amd.acados import AcadosOcpSolver
-    from drone_attitude_control_amd.batched import DEFAULT_N, first_step_qps, flops_per_iter
+    from drone_attitude_control_amd.batched import (DEFAULT_N, NY, first_step_qps, flops_per_iter,
+                                                    unconstrained_solve_flops)
     from drone_attitude_control_amd.models import OCPS
     from drone_attitude_control_amd.sharding import rank_workload, reduce_run
 
@@ -499,6 +507,11 @@ def main_solve(args, world, rank, dist, device):
             credit = ("FP64 flops per QP of the CPU run of the same algorithm on the same QPs (riccati_ipm_solve_batch_"
                       "fast, counted per path: gradient G yref, the Riccati recursion on the shared factorisation, "
                       "active-set steps m^3/3 + 2 m^2 + 2 ne m, full solves F_iter per Newton system) x B / kernel time")
+        elif fast:   # no CPU run to count the paths taken: every QP credited with the unconstrained path only
+            fl_solve = unconstrained_solve_flops(nx, nu, N, *NY[model])
+            credit = ("FP64 flops per QP of the unconstrained path alone (gradient G yref + the Riccati recursion on "
+                      "the shared factorisation, as riccati_ipm_solve_batch_fast counts them; a lower bound: no CPU "
+                      "run counted the active-set steps) x B / kernel time")
         else:
             n_newton = cpu["mean_newton_systems"] if cpu else float(red[1] / max(1.0, red[2]))
             fl_solve = flops_per_iter(nx, nu, N) * n_newton
@@ -526,7 +539,8 @@ def main_solve(args, world, rank, dist, device):
                      "mfma_instructions_per_launch": pmc.get("mfma_insts_per_launch"),
                      "traffic": traffic, "min_bytes_per_step": min_b,
                      "traffic_vs_min_bytes": traffic / min_b if traffic else None,
-                     "traffic_note": "FETCH_SIZE + WRITE_SIZE per batched solve from the committed PMC pass "
+                     "traffic_note": "2 x FETCH_SIZE (the gfx950 correction) + WRITE_SIZE per batched solve from the "
+                                     "committed PMC pass "
                                      f"({pmc.get('source', 'none for this config')}); min bytes = x0 + yref window "
                                      "in, full x/u trajectories out (SURVEY 8d)",
                      "kernel_ms_note": "HIP events around the solve's launches (fast solve: sf_kernel + fin64_kernel "

@@ -93,6 +93,7 @@ SIGNATURES = {
     "nmpc_closed_loop_stats": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_int]),
     "nmpc_closed_loop_instance_stats": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_size_t]),
     "nmpc_closed_loop_get_state": (ctypes.c_int, [ctypes.c_void_p, _dp, ctypes.c_size_t]),
+    "nmpc_closed_loop_set_outputs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nmpc_closed_loop_iter_log": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t]),
     "nmpc_sim_plant": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                       ctypes.c_double, _dp, _dp, _dp]),

@@ -107,6 +107,7 @@ class ClosedLoop:
         d.ref_table = _lib.dptr(keep["table"])
         d.ref_rows, d.ref_cols = keep["table"].shape
         d.ref_period = p.N
+        self.period = p.N                                # start row of step s: (offset + s) % period
         d.offsets = keep["offsets"].ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
         d.x_init = _lib.dptr(keep["x"])
         d.instance_base = int(instance_base)
@@ -136,6 +137,14 @@ class ClosedLoop:
         rc = self.lib.nmpc_closed_loop_run(self.solver._h, int(steps), 1 if sync else 0)
         if rc != 0:
             raise NmpcError(f"nmpc_closed_loop_run: {self.lib.nmpc_last_error(self.solver._h).decode()}")
+
+    def set_outputs(self, on=True):
+        """Opt in to the lean loop's trajectory outputs (nmpc_closed_loop_set_outputs): after each later run the
+        solver's get / get_batch return every instance's last-step solution (x_0 = the state that step started
+        from), status and qp_iter. Off by default: the loop reads only u_0 / x_1 (controller.py:37-41)."""
+        rc = self.lib.nmpc_closed_loop_set_outputs(self.solver._h, 1 if on else 0)
+        if rc != 0:
+            raise NmpcError(f"nmpc_closed_loop_set_outputs: {self.lib.nmpc_last_error(self.solver._h).decode()}")
 
     def stats(self):
         out = np.zeros(10)
@@ -183,6 +192,15 @@ def flops_per_iter(nx, nu, N):
     per_stage = (2 * nx * nx * nz + 2 * nx * nz * nz + nu ** 3 / 3 + 2 * nu * nu * nx + 2 * nu * nx * nx
                  + 2 * (2 * nx * nz + 2 * nu * nx + 2 * nx * nx) + 40 * nz)
     return N * per_stage
+
+
+def unconstrained_solve_flops(nx, nu, N, ny, ny_e):
+    """FP64 flops of the fast solve's unconstrained path per QP, as oracle/c/riccati_ipm.c
+    riccati_ipm_solve_batch_fast counts them: the gradient G yref (2 n m per stage, n = nx + nu rows for
+    k < N, nx for the terminal stage) and the Riccati recursion on the shared factorisation."""
+    nz = nx + nu
+    grad = N * 2 * nz * ny + 2 * nx * ny_e
+    return grad + N * (2 * nx * nx + 2 * nx * nz + 2 * nu * nu + 4 * nu * nx + 2 * nx * nz)
 
 
 def bytes_per_step(nx, nu, N, ny, ny_e, itemsize=8):

@@ -222,6 +222,7 @@ struct nmpc_solver {
     int clf_nslot = 0, clf_epl = 0, clf_x1slot = 0, clf_sid = 0;
     int clf_kidx = -1;                     // list-mode fallback kernel (lane per component)
     void *d_clf_scratch = nullptr;         // its scratch when the handle's own family is another
+    unsigned *d_clf_check = nullptr;       // env NMPC_CLF_CHECK with a checked build: the failed index checks
     void *d_fsT = nullptr;                 // typed: s_lb, s_ub, s_tx, vb, uinit
     double *d_clw = nullptr;               // fp32 handles: the lean loop's W in fp64 (fp64 handles: the model's)
     // fp32 handles: the solve's exact finish (fin32_z0_kernel + fin32_kernel, nmpc_cl_fast.hip)
@@ -266,6 +267,7 @@ struct nmpc_solver {
     std::vector<float> tmp_x0f, tmp_yf;
     // closed loop
     bool cl_ready = false;
+    bool cl_traj_out = false, out_from_loop = false;   // the lean loop writes the last step's x / u trajectories (nmpc_closed_loop_set_outputs)
     nmpc_closed_loop_desc cl{};
     void *d_table = nullptr, *d_state = nullptr, *d_plant = nullptr, *d_wcl = nullptr;
     int *d_offsets = nullptr;
@@ -531,7 +533,7 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
                     (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw,
                     (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0, (void *)h->d_sf, (void *)h->d_f64,
-                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch, (void *)h->d_sfcyc})
+                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch, (void *)h->d_sfcyc, (void *)h->d_clf_check})
         if (p) hipFree(p);
     if (h->h_sfpark) hipHostFree(h->h_sfpark);
     if (h->ev_fb) hipEventDestroy(h->ev_fb);
@@ -621,14 +623,17 @@ struct ListArgs {
     void *scratch;
 };
 
-// cl_steps > 0: fused closed loop of that many steps (lane-per-component / wavefront kernels)
+// cl_steps > 0: fused closed loop of that many steps (lane-per-component / wavefront kernels). fast: a plain
+// solve of an fp64 handle may take the fast solve (sf_enqueue; its parked instances run at sf_resolve) — the
+// per-step closed loop passes false: its advance kernel follows the solve on the stream with no host step between
 int sf_enqueue(nmpc_solver *h);
 
 template <typename T>
-int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0, const ListArgs *la = nullptr)
+int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0, const ListArgs *la = nullptr,
+           bool fast = true)
 {
     if (h->cond) return launch_cond<T>(h, e0, e1);
-    if (std::is_same<T, double>::value && h->sfast && cl_steps == 0 && !la) return sf_enqueue(h);
+    if (std::is_same<T, double>::value && fast && h->sfast && cl_steps == 0 && !la) return sf_enqueue(h);
     nmpc::IpmParams<T> p{};
     int kidx = h->kidx;
     void *scratch = h->d_scratch;
@@ -1342,6 +1347,34 @@ int nmpc_synchronize(nmpc_solver *h)
     return 0;
 }
 
+// the device trajectories, status and qp_iter of the last solve (or the lean closed loop's last step) to the
+// host copies nmpc_get / nmpc_get_batch read; waits for the handle's stream
+static int download_outputs(nmpc_solver *h)
+{
+    hipError_t e;
+    const size_t nxo = h->h_x.size(), nuo = h->h_u.size();
+    if (h->precision == NMPC_FP64) {
+        hipMemcpyAsync(h->h_x.data(), h->d_x, nxo * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+        hipMemcpyAsync(h->h_u.data(), h->d_u, nuo * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+    }
+    std::vector<float> fx, fu;
+    if (h->precision == NMPC_FP32) {
+        fx.resize(nxo);
+        fu.resize(nuo);
+        hipMemcpyAsync(fx.data(), h->d_x, nxo * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+        hipMemcpyAsync(fu.data(), h->d_u, nuo * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+    }
+    hipMemcpyAsync(h->h_status.data(), h->d_status, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    hipMemcpyAsync(h->h_iters.data(), h->d_iters, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "solve");
+    if (h->precision == NMPC_FP32) {
+        for (size_t i = 0; i < nxo; i++) h->h_x[i] = fx[i];
+        for (size_t i = 0; i < nuo; i++) h->h_u[i] = fu[i];
+    }
+    h->out_valid = true;
+    return 0;
+}
+
 int nmpc_solve(nmpc_solver *h)
 {
     if (!h) return NMPC_EINVAL;
@@ -1367,27 +1400,9 @@ int nmpc_solve(nmpc_solver *h)
     int r = h->precision == NMPC_FP64 ? launch<double>(h) : launch<float>(h);
     if (r < 0) return r;
     if ((r = sf_resolve(h)) < 0) return r;   // fast solve: full solves of the parked instances, if any
-    const size_t nxo = h->h_x.size(), nuo = h->h_u.size();
-    if (h->precision == NMPC_FP64) {
-        hipMemcpyAsync(h->h_x.data(), h->d_x, nxo * sizeof(double), hipMemcpyDeviceToHost, h->stream);
-        hipMemcpyAsync(h->h_u.data(), h->d_u, nuo * sizeof(double), hipMemcpyDeviceToHost, h->stream);
-    }
-    std::vector<float> fx, fu;
-    if (h->precision == NMPC_FP32) {
-        fx.resize(nxo);
-        fu.resize(nuo);
-        hipMemcpyAsync(fx.data(), h->d_x, nxo * sizeof(float), hipMemcpyDeviceToHost, h->stream);
-        hipMemcpyAsync(fu.data(), h->d_u, nuo * sizeof(float), hipMemcpyDeviceToHost, h->stream);
-    }
-    hipMemcpyAsync(h->h_status.data(), h->d_status, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
-    hipMemcpyAsync(h->h_iters.data(), h->d_iters, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
-    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "solve");
-    if (h->precision == NMPC_FP32) {
-        for (size_t i = 0; i < nxo; i++) h->h_x[i] = fx[i];
-        for (size_t i = 0; i < nuo; i++) h->h_u[i] = fu[i];
-    }
+    if ((r = download_outputs(h)) < 0) return r;
+    h->out_from_loop = false;
     hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1);
-    h->out_valid = true;
     int st = 0;
     for (int b = 0; b < h->batch; b++) st = std::max(st, (int)h->h_status[b]);
     return st;
@@ -1398,6 +1413,8 @@ int nmpc_get_cost(nmpc_solver *h, int inst, double *cost)
     if (!h || !cost) return NMPC_EINVAL;
     if (inst < 0 || inst >= h->batch) return h->fail(NMPC_EINVAL, "nmpc_get_cost: instance out of range");
     if (!h->out_valid) return h->fail(NMPC_ESTATE, "nmpc_get_cost: no solution available");
+    if (h->out_from_loop)   // the loop's windows come from its reference table, not from the host-staged yref
+        return h->fail(NMPC_ESTATE, "nmpc_get_cost: the outputs are a closed-loop step's (nmpc_closed_loop_stats has its cost)");
     const int nx = h->nx, nu = h->nu, N = h->N, ny = h->ny, ny_e = h->ny_e;
     const double sc = h->cost_s;
     const double *X = &h->h_x[(size_t)inst * (N + 1) * nx];
@@ -1566,7 +1583,7 @@ int cl_step_enqueue(nmpc_solver *h, int launch_idx)
     nmpc::ClParams<T> p = cl_params<T>(h);
     hipError_t e = nmpc::cl_prepare_launch<T>(p, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "closed-loop prepare");
-    const int r = launch<T>(h, h->cl_events[2 * launch_idx], h->cl_events[2 * launch_idx + 1]);
+    const int r = launch<T>(h, h->cl_events[2 * launch_idx], h->cl_events[2 * launch_idx + 1], 0, nullptr, false);
     if (r < 0) return r;
     e = nmpc::cl_advance_launch<T>(p, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "closed-loop advance");
@@ -2150,6 +2167,7 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     p.dt = d.dt;
     p.dt_conv = d.dt_conv;
     p.target = target;
+    p.traj_out = h->cl_traj_out ? 1 : 0;
     p.step0 = step0;
     p.noise_ld = noise_ld;
     p.polish_steps = h->polish_steps;
@@ -2258,6 +2276,14 @@ int clf_run(nmpc_solver *h, int steps)
         h->h_park = nullptr;
         return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: pinned park word");
     }
+    // env NMPC_CLF_CHECK with a checked build (-DNMPC_CLF_CHECK): the kernels' index checks report into a
+    // device word, read after every round; a failed check fails the run
+    static const bool check = std::getenv("NMPC_CLF_CHECK") != nullptr;
+    if (check && !h->d_clf_check) {
+        if (hipMalloc((void **)&h->d_clf_check, sizeof(unsigned)) != hipSuccess ||
+            hipMemset(h->d_clf_check, 0, sizeof(unsigned)) != hipSuccess)
+            return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: check word");
+    }
     int launches = 0;
     h->clf_parked = h->clf_rounds = 0;
     // env NMPC_CLF_CYCLES=<file> with a timing build (-DNMPC_CLF_TIMING): per-instance phase cycles of the
@@ -2274,6 +2300,7 @@ int clf_run(nmpc_solver *h, int steps)
         if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
         nmpc::ClFastParams<T> fp = clf_params<T>(h, target, h->cl_step, n);
         fp.cycles = d_cyc;
+        fp.check = h->d_clf_check;
         if (iter_log && h->d_iter_log) {
             const size_t rows = (size_t)(n + 2) * h->batch;
             if ((e = hipMemsetAsync(h->d_iter_log, 0xff, rows * sizeof(int), h->stream)) != hipSuccess)
@@ -2294,6 +2321,14 @@ int clf_run(nmpc_solver *h, int steps)
             if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
             if (e != hipSuccess) return hip_fail(h, e, "lean closed loop (fast kernel)");
             const int parked = h->h_park[0];
+            if (h->d_clf_check) {
+                unsigned bad = 0;
+                if ((e = hipMemcpy(&bad, h->d_clf_check, sizeof(bad), hipMemcpyDeviceToHost)) != hipSuccess)
+                    return hip_fail(h, e, "lean closed loop check word");
+                if (bad)
+                    return h->fail(NMPC_EDEVICE, "lean closed loop: index check failed, codes mask " + std::to_string(bad) +
+                                                     " (nmpc_cl_fast.hip CLF_CHECK)");
+            }
             if (dbg) std::fprintf(stderr, "[nmpc clf] steps %d..%d round %d: %d parked\n", h->cl_step, target, round, parked);
             if (parked <= 0) break;
             h->clf_parked += parked;
@@ -2495,6 +2530,11 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
     }
     h->cl_last_launches = launches;
     h->cl_last_steps = steps;
+    if (lean && h->cl_traj_out && steps > 0) {   // the last step's solutions, readable through nmpc_get*
+        const int r = download_outputs(h);
+        if (r < 0) return r;
+        h->out_from_loop = true;
+    }
     // the loop rewrote the device x0 / yref: the next nmpc_solve re-uploads the host-staged inputs
     h->x0_dirty = h->yref_dirty = true;
     if (sync) {
@@ -2560,6 +2600,13 @@ int nmpc_closed_loop_instance_stats(nmpc_solver *h, double *out, size_t count)
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e == hipSuccess) e = hipMemcpy(out, h->d_acc, count * sizeof(double), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_instance_stats");
+    return 0;
+}
+
+int nmpc_closed_loop_set_outputs(nmpc_solver *h, int on)
+{
+    if (!h) return NMPC_EINVAL;
+    h->cl_traj_out = on != 0;
     return 0;
 }
 

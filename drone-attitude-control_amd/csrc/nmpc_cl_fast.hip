@@ -77,6 +77,28 @@ constexpr int CLF_NT = 20;
     } while (0)
 #endif
 
+// Checked builds (-DNMPC_CLF_CHECK, build.build_experiment("clfcheck", ["NMPC_CLF_CHECK"])): every index the
+// lean loops form from run-time data is tested before its access; a failed test sets bit `code` of p.check
+// (a global vector atomic), prints its first occurrence, and the host fails the run (nmpc_api.cpp clf_run).
+// Codes: 1 claim-order position, 2 claimed instance, 3 v_t row, 4 phase-2 queue position, 5 noise column,
+// 6 reference row, 7 run_instance's instance, 8 run_instance's step below the launch's first, 9 phase-2
+// instance, 10 output element
+#ifdef NMPC_CLF_CHECK
+template <typename P>
+__device__ __noinline__ void clf_violation(const P &p, int code, long long v, int line)
+{
+    if (p.check && atomicOr(p.check, 1u << code) == 0u) printf("[clf check] code %d value %lld (line %d)\n", code, v, line);
+}
+#define CLF_CHECK(ok, code, v)                                                 \
+    do {                                                                       \
+        if (!(ok)) clf_violation(p, (code), (long long)(v), __LINE__);         \
+    } while (0)
+#else
+#define CLF_CHECK(ok, code, v) \
+    do {                       \
+    } while (0)
+#endif
+
 // decision thresholds by storage precision, relative to 1 + |b|: viol — a bound counts as violated beyond
 // it (fast-path acceptance, PDAS additions, the dual fallback's entering bound); onb — the solution's
 // warm-start flags (z within it of a bound). fp32 handles hold z_0 = v_t + T_x x to a few fp32 ulps of the
@@ -957,6 +979,7 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<
     constexpr int NZ = NX + NU;
     const int N = p.N, ne = p.ne;
     auto put = [&](int e, T z) {
+        CLF_CHECK(e >= 0 && e < ne, 10, e);
         const int k = e / NZ, r = e % NZ;
         if (r < NX) p.xout[((size_t)inst * (N + 1) + k) * NX + r] = z;
         else p.uout[((size_t)inst * N + k) * NU + (r - NX)] = z;
@@ -1073,6 +1096,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
     for (int i = 0; i < NU; i++) uin[i] = (double)p.uinit[i];
     CLF_T(tr0);
     const long long inst_t0 = p.iter_log ? wall_clock64() : 0;
+    CLF_CHECK(inst >= 0 && inst < p.B, 7, inst);
     // the instance's record, issued together: step, state (lane i < NX holds x_i), active flags of the
     // last solution by slot (bit 2j lower, 2j+1 upper; meaningful after step 0), offset, status
     int step = p.istep[inst];
@@ -1086,6 +1110,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
     const unsigned off = (unsigned)p.offset[inst];
     const int st_prev = p.status[inst];
     if (step >= p.target) return;
+    CLF_CHECK(step >= p.step0, 8, step - p.step0);
     unsigned fl = 0;
     if (step > 0) {
 #pragma unroll
@@ -1102,6 +1127,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
     // noise draw are issued at the top of the step and consumed after the solve
     T vtn[EPL];
     auto fetch_v = [&](int tt) {
+        CLF_CHECK(tt >= 0 && tt < p.period, 3, tt);
         const T *vp = p.vb + (size_t)tt * NSLOT;
 #pragma unroll
         for (int j = 0; j < EPL; j++) vtn[j] = vp[j * 64 + lane];
@@ -1116,6 +1142,8 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
         for (int j = 0; j < EPL; j++) vt[j] = vtn[j];
         const int tn = t + 1 == p.period ? 0 : t + 1;
         if (step + 1 < p.target) fetch_v(tn);
+        CLF_CHECK(t >= 0 && t < p.period, 6, t);
+        CLF_CHECK(step - p.step0 >= 0 && step - p.step0 < p.noise_ld, 5, step - p.step0);
         const double xr = lane < nref ? (double)p.table[(size_t)t * p.table_cols + lane] : 0.0;
         const double w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
         if (lane < NX) L.xs[lane] = xl;
@@ -1193,7 +1221,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
         last_iters = iters;
         // ---- the trajectory outputs of the instance's last step of the run
         CLF_T(to0);
-        if (step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, t, status, m_acc, z);
+        if (p.traj_out && step + 1 == p.target) write_outputs<T, NX, NU, EPL>(p, L, sv, lane, inst, t, status, m_acc, z);
         CLF_TADD(L, 7, to0);
         CLF_T(tl0);
         // ---- plant step + noise
@@ -1684,6 +1712,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 #pragma unroll
         for (int q = 0; q < NT; q++) vt[q] = T(0);
         auto fetch_v = [&](int tt) {
+            CLF_CHECK(tt >= 0 && tt < p.period, 3, tt);
             const T *vp = p.vb + (size_t)tt * NSLOT;
 #pragma unroll
             for (int q = 0; q < NT; q++) vt[q] = vp[slot_of(q)];
@@ -1695,7 +1724,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             if (lane < 4 && want) nx_ = atomicAdd(&wg_next, 1);
             nx_ = __shfl(nx_, n);
             if (!want) return;
+            CLF_CHECK(nx_ >= wg_hi - wg_lo || nx_ < LOCK_QCAP, 1, nx_);
             inst = nx_ < wg_hi - wg_lo ? wg_lo + (int)ord[nx_] : -1;
+            CLF_CHECK(inst < p.B, 2, inst);
             flany = false;
             cost = aed = 0.0;
             nfail = nst = 0;
@@ -1759,6 +1790,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == n) {
                     const int pos = atomicAdd(&dq_tail, 1);
+                    CLF_CHECK(pos < LOCK_QCAP, 4, pos);
                     __hip_atomic_store(&dq[pos], inst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
@@ -1821,7 +1853,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             CLF_T(tk_out);
             // the trajectory outputs of a fast instance's last step (write_outputs' success branch with an
             // empty set): x_0 the state, the bounded elements z clamped, the unbounded ones from the full tables
-            if (__any(adv && step + 1 == p.target)) {
+            if (p.traj_out && __any(adv && step + 1 == p.target)) {
                 double xa[NX];   // the instance's whole state on each of its lanes
 #pragma unroll
                 for (int c = 0; c < NX; c++) xa[c] = __shfl(xr[c / 4], 16 * (c % 4) + n);
@@ -1835,6 +1867,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
                     for (int q = 0; q < NT; q++) {
                         const int s_ = slot_of(q), e = sse[s_];
                         if (e < 0) continue;
+                        CLF_CHECK(e < p.ne, 10, e);
                         const T zc = fmin(fmax(z[q], (T)slb[s_]), (T)sub[s_]);
                         const int k = e / NZ, r = e % NZ;
                         if (r < NX) p.xout[((size_t)inst * (p.N + 1) + k) * NX + r] = zc;
@@ -1856,7 +1889,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             CLF_T(tk_ld);
             // ---- the next step's v (one step ahead), this step's reference row and noise draw
             double w = 0.0;
-            if (adv) w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
+            if (adv) {
+                CLF_CHECK(step - p.step0 >= 0 && step - p.step0 < p.noise_ld, 5, step - p.step0);
+                CLF_CHECK(t >= 0 && t < p.period, 6, t);
+                w = p.noise[(size_t)inst * p.noise_ld + (step - p.step0)];
+            }
             double xrf[KC];
 #pragma unroll
             for (int kc = 0; kc < KC; kc++) {
@@ -2010,6 +2047,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         fin = __builtin_amdgcn_readfirstlane(fin);
         if (fin) break;
         const int inst = __builtin_amdgcn_readfirstlane(got);
+        CLF_CHECK(inst >= 0 && inst < p.B, 9, inst);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         // explicit form of one instance on the same MFMA tiles: all four B columns the instance's x (L.xs),
         // the n = 0 lanes' results staged to slot order

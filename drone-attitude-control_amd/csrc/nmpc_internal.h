@@ -135,11 +135,14 @@ struct ClFastParams {
     const T *AB, *c;              // [nx][nz], [nx]: the controller model (plant 0, certificate)
     const T *wcl;                 // [ncl]
     const T *uinit;               // [nu] inputs of the solver's initial point (failure output)
-    T *xout, *uout;               // trajectories of the last solve (written at the last step)
+    T *xout, *uout;               // trajectories of the last solve (written at the last step when traj_out)
+    int traj_out;                 // closed loop: 1 writes the last step's x / u trajectories (opt-in,
+                                  // nmpc_closed_loop_set_outputs); the loop itself reads only u_0 / x_1
     int *status, *iters;
     int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
     int *iter_log;                // optional [steps][B]: active-set steps (<= 255) | status << 8 | wall-clock ticks (<= 32767) << 16
     unsigned long long *cycles;   // diagnostic builds (NMPC_CLF_TIMING): [B][14] phase cycles / counts per instance
+    unsigned *check;              // checked builds (NMPC_CLF_CHECK): bit mask of the failed index checks
     // the fp32 solve finish (fin32_kernel): z_0 of every element per instance ([B][z0_ld], fin32_z0_kernel),
     // the pinned states x0 [B][nx]; the lean loop leaves them null (z_0 from T_x x + v_t)
     const T *z0all;

@@ -171,7 +171,12 @@ int nmpc_device_ptr(nmpc_solver *h, const char *field, void **out);
 /* solve all instances. nmpc_solve: upload host-staged inputs, launch, wait, download; returns
  * the max status over instances (0 when every instance succeeded) or < 0 on API error.
  * nmpc_solve_async: launch on the handle's stream using the device buffers as they are;
- * returns immediately (no host staging). */
+ * returns immediately (no host staging). With the fast solve (nmpc_get_launch_info out[8]) the instances
+ * the first two launches leave parked get their full solve when the host next waits: inside nmpc_solve,
+ * or at nmpc_synchronize after nmpc_solve_async — read the device buffers only after nmpc_synchronize.
+ * Back-to-back nmpc_solve_async calls write the same device outputs; the last one's are final after
+ * nmpc_synchronize (stream-ordered kernels of the caller that read the outputs before it may see a parked
+ * instance's unconstrained point). */
 int nmpc_solve(nmpc_solver *h);
 int nmpc_solve_async(nmpc_solver *h);
 int nmpc_synchronize(nmpc_solver *h);
@@ -192,7 +197,11 @@ int nmpc_get_stats(nmpc_solver *h, double *stats, int n);
  * kernel is specialised for (0: dense; 1 force, 2 jerk, 3 quad13; env NMPC_STRUCT=0 forces dense),
  * out[6] = the closed loop's kernel after nmpc_closed_loop_init (1: the lean loop, cl_fast_kernel; 2: the
  * lean loop's lockstep kernel cl_lock_kernel, four instances per wavefront on MFMA; 0: the fused / per-step
- * launches of the family above), out[7] = the lean loop's largest active set */
+ * launches of the family above), out[7] = the lean loop's largest active set, out[8] = 1 when this handle's
+ * plain solves (nmpc_solve / nmpc_solve_async) take the fast solve (fp64 handles of the compiled shapes:
+ * sf_kernel's unconstrained solution + bound test, fin64_kernel's active-set steps for the instances with a
+ * violated bound, the full IPM in list mode for what they leave; env NMPC_SOLVE_FAST=0 or an explicit
+ * NMPC_KERNEL family: 0, every QP on the full IPM + exact finish) */
 int nmpc_get_launch_info(const nmpc_solver *h, int *out, int n);
 
 /* ------------------------------------------------------------------ batched closed loop
@@ -257,6 +266,14 @@ int nmpc_closed_loop_instance_stats(nmpc_solver *h, double *out, size_t count);
  *     fallback solved keeps the marker -1. The last two rows: each instance's start and end in that
  *     launch (wall-clock ticks, low 31 bits). */
 int nmpc_closed_loop_iter_log(nmpc_solver *h, int32_t *out, size_t count);
+/* the lean loop's trajectory outputs (opt-in; default off). The loop reads only u_0 and x_1 of each step's
+ * solution (controller.py:37-41), so by default no trajectory is written to HBM. With on != 0, every later
+ * nmpc_closed_loop_run on the lean loop writes each instance's last-step solution (x_0 = the state the
+ * step started from) and downloads it with that step's status and qp_iter when the run ends: nmpc_get /
+ * nmpc_get_batch / nmpc_get_batch_int then read them (nmpc_get_cost refuses: the loop's windows come
+ * from its reference table). The fused and per-step paths (NMPC_CL_FAST=0 / NMPC_CL_FUSED=0) do not
+ * expose their outputs either way. */
+int nmpc_closed_loop_set_outputs(nmpc_solver *h, int on);
 /* current closed-loop states, batch*nx */
 int nmpc_closed_loop_get_state(nmpc_solver *h, double *out, size_t count);
 

@@ -251,3 +251,41 @@ def test_shared_factorisation_paths_match_full_factorisation(model, N, B):
         err = np.abs(x1 - ref.state).max(1) / np.maximum(1.0, np.abs(ref.state).max(1))
         assert err.max() < 1e-6, (env, err.max())
         np.testing.assert_allclose(s1[:, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12, err_msg=str(env))
+
+
+@pytest.mark.parametrize("model,N,B", [("quad13", 20, 2048), ("force", 20, 1024), ("jerk", 40, 1024)])
+def test_lean_loop_trajectory_outputs_are_opt_in(model, N, B):
+    """The lean loop writes no trajectory by default (the loop reads only u_0 / x_1, controller.py:37-41);
+    nmpc_closed_loop_set_outputs(1) turns the last step's write-back on. Results are the same either way
+    (states and per-instance sums bit for bit), the default leaves nothing to read, and the opted-in outputs
+    are each instance's last-step solution: x_0 the state that step started from, the trajectory the oracle's
+    QP solution from that state and window (1e-6 relative), the status the oracle's."""
+    from drone_attitude_control_amd.batched import ClosedLoop, first_step_qps, workload
+    from drone_attitude_control_amd._lib import NmpcError
+    from oracle import cref, models
+    table, off, x = workload(model, N, B, 42)
+    a = ClosedLoop(model, B, N=N, table=table, offsets=off, x_init=x, seed=42)
+    b = ClosedLoop(model, B, N=N, table=table, offsets=off, x_init=x, seed=42)
+    b.set_outputs(True)
+    k = 7
+    a.run(k - 1)       # the same launch split for both (a launch boundary flushes the sums and may move an
+    a.run(1)           # instance between the lockstep and the single-instance code: last-bit differences)
+    b.run(k - 1)
+    xs = b.state()
+    b.run(1)
+    assert np.array_equal(a.state(), b.state())
+    assert np.array_equal(a.instance_stats(), b.instance_stats())
+    with pytest.raises(NmpcError):
+        a.solver.get_batch("x")
+    X, U = b.solver.get_batch("x"), b.solver.get_batch("u")
+    st = b.solver.get_batch_int("status")
+    assert np.array_equal(X[:, 0], xs)
+    idx = np.arange(0, B, max(1, B // 97))
+    x0s, Y = first_step_qps(model, N, table, (np.asarray(off)[idx] + k - 1) % b.period, xs[idx])
+    Xr, Ur, str_, _ = cref.RiccatiIpmRef(models.MODELS[model](N)).solve(x0s, Y)
+    assert np.array_equal(st[idx], str_)
+    ok = str_ == 0
+    assert ok.sum() >= len(idx) - 2
+    scale = np.maximum(1.0, np.maximum(np.abs(Xr).max(axis=(-2, -1)), np.abs(Ur).max(axis=(-2, -1))))
+    err = np.maximum(np.abs(X[idx] - Xr).max(axis=(-2, -1)), np.abs(U[idx] - Ur).max(axis=(-2, -1))) / scale
+    assert err[ok].max() < 1e-6, err.max()
