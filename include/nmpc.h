@@ -241,7 +241,10 @@ int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d);
  *   - the lean loop (nmpc_cl_fast.hip; quad13 / jerk / force shapes, fp64 and fp32 — fp32: fp32 tables
  *     and explicit form, fp64 W, set solves and acceptance — the default): launches of at
  *     most 64 steps; after each launch the host reads the count of parked instances (a step the fast
- *     path could not solve) and runs their full solve in list mode. That read waits for the launch, so
+ *     path could not solve) and runs their full solve in list mode. fp32 handles: that full solve is the
+ *     fp32 IPM without the exact finish (1e-3..1e-2 from the exact step solution, which the plant then
+ *     carries); on the bench workloads no fp32 step parks (tests/test_gpu_bench_parity.py forces parks with
+ *     NMPC_CLF_NO_GI=1 to measure it). That read waits for the launch, so
  *     the lean loop returns only when its last launch is done, whatever `sync` says;
  *   - fused (lane-per-component and wavefront kernel families, NMPC_CL_FAST=0): each solve launch
  *     carries up to 64 steps of every instance (prepare + solve + advance per instance, no step barrier

@@ -171,6 +171,37 @@ TOL_CL32 = 1e-5        # fp32 lean loop, force (BASELINE config 3), DESIGN.md §
 TOL_CL32_LOOP = 1e-3   # fp32 lean loop, quad13 / jerk: a few loop-sensitive instances (measured 2.6e-4 / 5.2e-4)
 
 
+TOL_CL32_PARKED = 5e-2   # fp32 lean loop whose parked steps take the fp32 IPM (no exact finish), include/nmpc.h
+
+
+@pytest.mark.timeout(300)
+def test_fp32_parked_steps_take_the_fp32_ipm(golden, monkeypatch):
+    """The fp32 lean loop's fallback, forced: NMPC_CLF_NO_GI=1 parks every step the PDAS rounds do not settle
+    (no dual fallback), so those steps run the fp32 list-mode IPM, which has no exact finish (include/nmpc.h).
+    Force N=20 B=8192 fp32 (BASELINE config 3's workload) against the exact fp64 oracle loop: parks happen, step
+    counts stay exact, and the states stay within the fp32 IPM's accuracy carried through the loop
+    (TOL_CL32_PARKED) — the measured size of the difference the default path (0 parks) does not have."""
+    from drone_attitude_control_amd.batched import ClosedLoop
+    monkeypatch.setenv("NMPC_CLF_NO_GI", "1")
+    key = "force_N20_B8192"
+    sel = golden[f"{key}_sel"]
+    loop = ClosedLoop("force", 8192, N=20, seed=42, precision="fp32")
+    states, sums, parked = [], [], 0
+    for n in REGIONS[:4]:
+        loop.run(n)
+        parked += loop.stats()["parked"]
+        states.append(loop.state())
+        sums.append(loop.instance_stats())
+    S, A = np.array(states), np.array(sums)
+    err = _rel(S[:, sel], golden[f"{key}_states"][:4])
+    print(f"fp32 {key} closed loop with parks: parked {parked}, max state err {err.max():.3e}, "
+          f"median {np.median(err):.3e}, instances above 1e-5: {(err.max(0) > 1e-5).sum()} of {len(sel)}")
+    assert parked > 0
+    assert np.array_equal(A[:, sel, 3], golden[f"{key}_sums"][:4, :, 3])
+    assert np.median(err) < 1e-5
+    assert err.max() < TOL_CL32_PARKED
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("model,N,B", [("force", 20, 8192), ("quad13", 20, 8192), ("jerk", 40, 4096)])
 def test_fp32_closed_loop_matches_oracle(golden, model, N, B):
