@@ -261,7 +261,7 @@ struct nmpc_solver {
     int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
     int clf_resident = 0;                  // workgroups of cl_fast_kernel the handle's device holds at once
-    int clf_kind = 0;                      // nmpc::CLF_FAST / CLF_LOCK (cl_lock_kernel) / CLF_WLDS (W in LDS)
+    int clf_kind = 0;                      // nmpc::CLF_FAST / CLF_LOCK (cl_lock_kernel) / CLF_WLDS (W in LDS) / CLF_ONE
     int clf_parked = 0, clf_rounds = 0;    // the last run: parked solves (list-mode full solves), fast launches
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
     std::vector<float> tmp_x0f, tmp_yf;
@@ -2123,7 +2123,13 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     // path's steps are bound by their instruction chains, not by W's L2 latency; tools/ab_check.sh, wl1)
     const char *wenv = std::getenv("NMPC_CLF_WLDS");
     const bool wlds = nmpc::cl_wlds_shape(nx, nu) && wenv && wenv[0] == '1';
-    h->clf_kind = lock ? nmpc::CLF_LOCK : (wlds ? nmpc::CLF_WLDS : nmpc::CLF_FAST);
+    // a batch no larger than the device's SIMD count runs one wavefront per SIMD anyway: the variant compiled
+    // for that (its rare path unrolled further) where the shape has one (env NMPC_CLF_ONE=0: off)
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+    const char *oenv = std::getenv("NMPC_CLF_ONE");
+    const bool one = nmpc::cl_one_shape(nx, nu) && cus > 0 && h->batch <= 4 * cus && !(oenv && oenv[0] == '0');
+    h->clf_kind = lock ? nmpc::CLF_LOCK : (wlds ? nmpc::CLF_WLDS : (one ? nmpc::CLF_ONE : nmpc::CLF_FAST));
     // resident workgroups on this handle's device (nmpc_closed_loop_init runs on it: hipSetDevice above)
     h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, h->clf_kind, f64, h->device);
     // the lockstep kernel's per-workgroup queue holds at most 512 demoted instances

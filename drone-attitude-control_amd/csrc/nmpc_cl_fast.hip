@@ -168,8 +168,11 @@ struct HGeom {
     static constexpr int CPL = WSM * WSM / 64;   // H columns per lane: lane = row i + WSM * column group g
     static constexpr int HP = WSM + 2;           // row pitch (even: 16-byte aligned column groups)
 };
-template <int NSLOT, int NZ, int WSM>
+// SW2: the symmetric sweep with its pivots unrolled per column group (the one-wavefront-per-SIMD variant, which
+// has the register room; sweep_inverse)
+template <int NSLOT, int NZ, int WSM, bool SW2 = false>
 struct Lds {
+    static constexpr bool sweep2 = SW2;
     alignas(16) double xs[32];   // x (lane i writes x_i; x_nx.. stay 0): explicit form, plant rows, rare paths
     signed char fl[NSLOT];       // the warm-start shift buffer
     alignas(16) double hm[WSM][HGeom<WSM>::HP];
@@ -276,20 +279,21 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView
         if (j == lane) wii = row[j];
     if (lane < m) L.wdg[lane] = wii;
     pd = true;
-#pragma unroll
+    // every pivot unrolled: row[c] / row[j] and the readlane source are compile-time (a runtime pivot loop
+    // indexes the register row dynamically: s_set_gpr_idx moves on every access). Columns j >= m are zero in
+    // every row, so their updates leave them zero and need no guard
+#pragma clang loop unroll(full)
     for (int c = 0; c < WSM; c++) {
-        if (c >= m) break;
-        const double d0 = bcast(row[c], c), wcc = bcast(wii, c), tc = bcast(t, c);
-        pd = pd && wcc > 0.0;
-        const double d = d0 > 1e-9 * wcc ? d0 : fmax(d0, 0.0) + 1e-6 * wcc;
-        const double f = lane != c ? row[c] * rcp_nr(d) : 0.0;
-#pragma unroll
-        for (int j = c + 1; j < WSM; j++) {
-            if (j >= m) break;
-            row[j] = fma(-f, bcast(row[j], c), row[j]);
+        if (c < m) {
+            const double d0 = bcast(row[c], c), wcc = bcast(wii, c), tc = bcast(t, c);
+            pd = pd && wcc > 0.0;
+            const double d = d0 > 1e-9 * wcc ? d0 : fmax(d0, 0.0) + 1e-6 * wcc;
+            const double f = lane != c ? row[c] * rcp_nr(d) : 0.0;
+#pragma clang loop unroll(full)
+            for (int j = c + 1; j < WSM; j++) row[j] = fma(-f, bcast(row[j], c), row[j]);
+            t = fma(-f, tc, t);
+            if (lane == c) row[c] = d;
         }
-        t = fma(-f, tc, t);
-        if (lane == c) row[c] = d;
     }
     double dd = 1.0;
 #pragma unroll
@@ -324,20 +328,46 @@ __device__ bool sweep_inverse(const ClFastParams<T> &p, LdsT &L, const SlotView<
         if (g * CPL + q == i && i < m) L.wdg[i] = a[q];
     CLF_SYNC();
     bool pd = true;
+    if constexpr (LdsT::sweep2) {
+        // pivots k = k0 + kk with kk unrolled, so a[kk] is a compile-time register; the runtime loop below
+        // indexes the register row dynamically and copies it per pivot. Same arithmetic, same order. Measured
+        // (force B = 1024, one wavefront per SIMD) +3 % over the runtime loop; its register use costs the
+        // second wavefront per SIMD at B = 8192 (-22 %), hence only in the CLF_ONE variant
+        for (int k0 = 0; k0 < m; k0 += CPL) {
+            const bool own = g == k0 / CPL;   // this lane's registers hold the group's columns
+#pragma clang loop unroll(full)
+            for (int kk = 0; kk < CPL; kk++) {
+                const int k = k0 + kk;
+                if (k < m) {
+                    if (own) L.vb1[i] = a[kk];
+                    CLF_SYNC();
+                    const double ci = L.vb1[i], d0 = L.vb1[k], wkk = L.wdg[k];
+                    pd = pd && wkk > 0.0;
+                    const double d = d0 > 1e-9 * wkk ? d0 : fmax(d0, 0.0) + 1e-6 * wkk;
+                    const double f = rcp_nr(d);
+                    const double cif = i == k ? 1.0 - f : ci * f;
 #pragma unroll
-    for (int k = 0; k < WSM; k++) {
-        if (k >= m) break;
-        if (g == k / CPL) L.vb1[i] = a[k % CPL];
-        CLF_SYNC();
-        const double ci = L.vb1[i], d0 = L.vb1[k], wkk = L.wdg[k];
-        pd = pd && wkk > 0.0;
-        const double d = d0 > 1e-9 * wkk ? d0 : fmax(d0, 0.0) + 1e-6 * wkk;
-        const double f = rcp_nr(d);
-        // rows i != k: a_ij - c_i f c_j; row k (a_kj = c_j by symmetry): a_kj - (1 - f) c_j = c_j f
-        const double cif = i == k ? 1.0 - f : ci * f;
+                    for (int q = 0; q < CPL; q++) a[q] = fma(-cif, L.vb1[g * CPL + q], a[q]);
+                    if (own) a[kk] = i == k ? -f : ci * f;
+                }
+            }
+        }
+    } else {
 #pragma unroll
-        for (int q = 0; q < CPL; q++) a[q] = fma(-cif, L.vb1[g * CPL + q], a[q]);
-        if (g == k / CPL) a[k % CPL] = i == k ? -f : ci * f;
+        for (int k = 0; k < WSM; k++) {
+            if (k >= m) break;
+            if (g == k / CPL) L.vb1[i] = a[k % CPL];
+            CLF_SYNC();
+            const double ci = L.vb1[i], d0 = L.vb1[k], wkk = L.wdg[k];
+            pd = pd && wkk > 0.0;
+            const double d = d0 > 1e-9 * wkk ? d0 : fmax(d0, 0.0) + 1e-6 * wkk;
+            const double f = rcp_nr(d);
+            // rows i != k: a_ij - c_i f c_j; row k (a_kj = c_j by symmetry): a_kj - (1 - f) c_j = c_j f
+            const double cif = i == k ? 1.0 - f : ci * f;
+#pragma unroll
+            for (int q = 0; q < CPL; q++) a[q] = fma(-cif, L.vb1[g * CPL + q], a[q]);
+            if (g == k / CPL) a[k % CPL] = i == k ? -f : ci * f;
+        }
     }
 #pragma unroll
     for (int q = 0; q < CPL; q++) L.hm[i][g * CPL + q] = -a[q];
@@ -1303,12 +1333,12 @@ __device__ inline void claim_order(unsigned short *ord, const unsigned char *har
 
 // WPB wavefronts per workgroup (the slot tables in LDS are shared by them), MW the occupancy target
 // (waves per SIMD; 0: none)
-template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP, bool WL = false>
+template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP, bool WL = false, bool SW2 = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0 ? MW : 1, 8))) void cl_fast_kernel(ClFastParams<T> p)
 {
     constexpr int NZ = NX + NU, NSLOT = EPL * 64;
     static_assert(NX < 32 && NZ <= 64, "lane-distributed state");
-    __shared__ Lds<NSLOT, NZ, WSM> lds_all[WPB];
+    __shared__ Lds<NSLOT, NZ, WSM, SW2> lds_all[WPB];
     // workgroup constants: [A B], c (plant), the slots' bounds, thresholds, elements and warm-start sources
     __shared__ double abl[NX * NZ], cl[NX], slb[NSLOT], sub[NSLOT], slo[NSLOT], shi[NSLOT], sol[NSLOT], sou[NSLOT];
     __shared__ int sse[NSLOT], ssrc[NSLOT];
@@ -1359,7 +1389,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     __shared__ int wg_next;   // the workgroup's next instance (offset into its range)
     __shared__ unsigned short ord[LOCK_QCAP];   // claim order (offsets into the workgroup's range)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
+    Lds<NSLOT, NZ, WSM, SW2> &L = lds_all[wave];
     if (lane < 32) L.xs[lane] = 0.0;
 #ifdef NMPC_CLF_TIMING
     if (lane < CLF_NT) L.tacc[lane] = 0;
@@ -2094,10 +2124,10 @@ int cl_fast_wsmax(int nx, int nu)
 }
 
 // one compiled variant per shape, as a tag type
-template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, int MW_, class SP_, bool WL_ = false>
+template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, int MW_, class SP_, bool WL_ = false, bool SW2_ = false>
 struct Variant {
     static constexpr int WPB = WPB_;
-    static constexpr auto kernel() { return clf::cl_fast_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_, WL_>; }
+    static constexpr auto kernel() { return clf::cl_fast_kernel<T_, NX_, NU_, EPL_, WSM_, WPB_, MW_, SP_, WL_, SW2_>; }
 };
 // the lockstep kernel (four instances per wavefront, MFMA explicit form and plant)
 template <typename T_, int NX_, int NU_, int EPL_, int WSM_, int WPB_, int MW_, class SP_>
@@ -2110,6 +2140,7 @@ struct LockVariant {
 // sit on x_1: the host checks plant and cost stage)
 bool cl_lock_shape(int nx, int nu) { return (nx == 13 && nu == 4) || (nx == 6 && nu == 2); }
 bool cl_wlds_shape(int nx, int nu) { return nx == 4 && nu == 2; }
+bool cl_one_shape(int nx, int nu) { return nx == 4 && nu == 2; }
 
 // calls f(Variant<...>{}) for the shape's compiled variant; false: none. NMPC_CLF_VARIANT=1 (tuning):
 // an occupancy target (quad13 4 waves per SIMD: spills, measured 10 % slower than the default)
@@ -2138,6 +2169,7 @@ static bool clf_dispatch(int nx, int nu, int sid, int kind, F &&f)
         f(Variant<T, 6, 2, 5, 16, 8, 0, lpc::DenseStructure<6, 2>>{});
     } else if (nx == 4 && nu == 2) {
         if (kind == CLF_WLDS) f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>, true>{});
+        else if (kind == CLF_ONE) f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>, false, true>{});
         else if (var == 1) f(Variant<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>{});
         else f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>{});
     } else {

@@ -198,8 +198,11 @@ int cl_fast_wsmax(int nx, int nu);
 bool cl_lock_shape(int nx, int nu);
 // whether the shape has a cl_fast_kernel variant with W over the slots in LDS (the force shape)
 bool cl_wlds_shape(int nx, int nu);
+bool cl_one_shape(int nx, int nu);
 // lean-loop kernel kinds: one instance per wavefront (W from L2 / from LDS), the lockstep kernel
-constexpr int CLF_FAST = 0, CLF_LOCK = 1, CLF_WLDS = 2;
+// CLF_ONE: cl_fast_kernel compiled for one wavefront per SIMD (the whole register file; batches no larger than
+// the device's SIMD count)
+constexpr int CLF_FAST = 0, CLF_LOCK = 1, CLF_WLDS = 2, CLF_ONE = 3;
 // workgroups of the shape's cl_fast_kernel (lock: cl_lock_kernel, fp64 only) in the handle's precision
 // that `device` holds at once (the persistent grid), or 0
 int cl_fast_resident(int nx, int nu, int sid, int kind, bool f64, int device);
