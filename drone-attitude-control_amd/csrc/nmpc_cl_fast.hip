@@ -222,6 +222,14 @@ struct SlotView {
     __device__ int src(int j) const { return src_[j * 64 + lane]; }
 };
 
+// The rare path's W gathers as unconditional loads (a clamped index outside the set, the value masked after the
+// load; a load under a branch makes the join wait for every load in flight) and the dual fallback's W[p, :] row
+// issued with its a = W[S, p]: for the force shape (two slots per lane). Same-box A/B (profiles/
+// r6r_gather_ab.jsonl, r6s_mix_ab.jsonl): force B = 1024 and 8192 +7..10 %; quad13 and jerk -6 %, so they keep the
+// branches
+template <int EPL>
+constexpr bool UNCOND_GATHER = EPL <= 2;
+
 // 2-bit flags of a per-lane mask (bit 2j lower, 2j+1 upper) <-> -1 / 0 / 1
 __device__ __forceinline__ signed char flag_of(unsigned m, int j)
 {
@@ -272,7 +280,15 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView
     double row[WSM];
     const int ei = lane < m ? L.se_e[lane] : 0, si = lane < m ? L.gi_slot[lane] : 0;
 #pragma unroll
-    for (int j = 0; j < WSM; j++) row[j] = (j < m && lane < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
+    for (int j = 0; j < WSM; j++) {
+        if constexpr (UNCOND_GATHER<EPL>) {   // clamped index, value masked after the load (no branch per load)
+            const int jj = j < m ? j : 0;
+            const double w = sv.w(p, L.se_e[jj], L.gi_slot[jj], ei, si);
+            row[j] = (j < m && lane < m) ? w : 0.0;
+        } else {
+            row[j] = (j < m && lane < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
+        }
+    }
     double wii = 1.0;
 #pragma unroll
     for (int j = 0; j < WSM; j++)
@@ -311,9 +327,75 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView
 // fast_finish's regularisation: below 1e-9 W_kk it becomes max(d, 0) + 1e-6 W_kk, so the result is the
 // inverse of the same regularised system the Cholesky / Gauss-Jordan paths solve. H = W_SS^-1 goes to
 // L.hm (zero outside the m x m block), W_ii to L.wdg. false: a non-positive W_ii.
+// The sweep's gather and result (the lane's register row a[CPL]: lane = row i + WSM * column group g)
+template <typename T, int WSM, int EPL, class LdsT>
+__device__ __forceinline__ void sweep_gather(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> &sv, int m, int i, int g,
+                                             double (&a)[HGeom<WSM>::CPL])
+{
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int ei = i < m ? L.se_e[i] : 0, si = i < m ? L.gi_slot[i] : 0;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) {
+        const int j = g * CPL + q;
+        if constexpr (UNCOND_GATHER<EPL>) {
+            const int jj = j < m ? j : 0;
+            const double w = sv.w(p, L.se_e[jj], L.gi_slot[jj], ei, si);
+            a[q] = (i < m && j < m) ? w : 0.0;
+        } else {
+            a[q] = (i < m && j < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < CPL; q++)
+        if (g * CPL + q == i && i < m) L.wdg[i] = a[q];
+    CLF_SYNC();
+}
+template <int WSM, class LdsT>
+__device__ __forceinline__ void sweep_store(LdsT &L, int i, int g, const double (&a)[HGeom<WSM>::CPL])
+{
+    constexpr int CPL = HGeom<WSM>::CPL;
+#pragma unroll
+    for (int q = 0; q < CPL; q++) L.hm[i][g * CPL + q] = -a[q];
+    CLF_SYNC();
+}
+
+// The symmetric sweep for sets of up to 16, inlined into its caller: a run-time pivot loop over the lane's CPL
+// register entries (the index a register move).
+template <typename T, int WSM, int EPL, class LdsT>
+__device__ __forceinline__ bool sweep_inverse_rt(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> &sv, int m, int lane)
+{
+    constexpr int CPL = HGeom<WSM>::CPL;
+    const int i = lane % WSM, g = lane / WSM;
+    double a[CPL];
+    sweep_gather<T, WSM>(p, L, sv, m, i, g, a);
+    bool pd = true;
+#pragma unroll
+    for (int k = 0; k < WSM; k++) {
+        if (k >= m) break;
+        if (g == k / CPL) L.vb1[i] = a[k % CPL];
+        CLF_SYNC();
+        const double ci = L.vb1[i], d0 = L.vb1[k], wkk = L.wdg[k];
+        pd = pd && wkk > 0.0;
+        const double d = d0 > 1e-9 * wkk ? d0 : fmax(d0, 0.0) + 1e-6 * wkk;
+        const double f = rcp_nr(d);
+        // rows i != k: a_ij - c_i f c_j; row k (a_kj = c_j by symmetry): a_kj - (1 - f) c_j = c_j f
+        const double cif = i == k ? 1.0 - f : ci * f;
+#pragma unroll
+        for (int q = 0; q < CPL; q++) a[q] = fma(-cif, L.vb1[g * CPL + q], a[q]);
+        if (g == k / CPL) a[k % CPL] = i == k ? -f : ci * f;
+    }
+    sweep_store<WSM>(L, i, g, a);
+    return pd;
+}
+
+// Sets of 17..32 (the force shape, WSM 32) keep the form the compiler outlines: its run-time pivot loop keeps a[]
+// in scratch memory, and measured faster there than the inlined form, which costs the force kernels registers
+// (-10 % at B = 1024 and 8192, profiles/r6n_sweep_inline_ab.jsonl). Sets of up to 16 (GI's H for quad13 / jerk)
+// take sweep_inverse_rt, inlined (quad13 +6.8 %, same A/B).
 template <typename T, int WSM, int EPL, class LdsT>
 __device__ bool sweep_inverse(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> &sv, int m, int lane)
 {
+    if constexpr (WSM <= 16) return sweep_inverse_rt<T, WSM>(p, L, sv, m, lane);   // sets of up to 16: inlined
     constexpr int CPL = HGeom<WSM>::CPL;
     const int i = lane % WSM, g = lane / WSM;
     double a[CPL];
@@ -321,7 +403,13 @@ __device__ bool sweep_inverse(const ClFastParams<T> &p, LdsT &L, const SlotView<
 #pragma unroll
     for (int q = 0; q < CPL; q++) {
         const int j = g * CPL + q;
-        a[q] = (i < m && j < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
+        if constexpr (UNCOND_GATHER<EPL>) {
+            const int jj = j < m ? j : 0;
+            const double w = sv.w(p, L.se_e[jj], L.gi_slot[jj], ei, si);
+            a[q] = (i < m && j < m) ? w : 0.0;
+        } else {
+            a[q] = (i < m && j < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
+        }
     }
 #pragma unroll
     for (int q = 0; q < CPL; q++)
@@ -478,7 +566,14 @@ __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const int
         for (int q = 0; q < QB; q++) {
             const int row = i0 + q < m ? el[i0 + q] : 0, rs = i0 + q < m ? sl[i0 + q] : 0;
 #pragma unroll
-            for (int j = 0; j < EPL; j++) w[q][j] = (i0 + q < m && e[j] >= 0) ? sv.w(p, row, rs, e[j], j * 64 + sv.lane) : 0.0;
+            for (int j = 0; j < EPL; j++) {
+                if constexpr (UNCOND_GATHER<EPL>) {
+                    const double wl = sv.w(p, row, rs, e[j] >= 0 ? e[j] : 0, e[j] >= 0 ? j * 64 + sv.lane : 0);
+                    w[q][j] = (i0 + q < m && e[j] >= 0) ? wl : 0.0;
+                } else {
+                    w[q][j] = (i0 + q < m && e[j] >= 0) ? sv.w(p, row, rs, e[j], j * 64 + sv.lane) : 0.0;
+                }
+            }
         }
 #pragma unroll
         for (int q = 0; q < QB; q++)
@@ -794,7 +889,19 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         CLF_T(tg_sol);
         // a = W[S, p] (occupied positions) and W_pp, loads issued together
         const bool occ = pl && ((am >> lane) & 1u);
-        const double ai = occ ? sv.w(p, L.se_e[lane], L.gi_slot[lane], ep, ps) : 0.0;
+        double ai;
+        double wpj[EPL];   // (UNCOND_GATHER) W[p, slots] of the step direction, issued with a
+        if constexpr (UNCOND_GATHER<EPL>) {
+            const double aw = sv.w(p, occ ? L.se_e[lane] : ep, occ ? L.gi_slot[lane] : ps, ep, ps);
+            ai = occ ? aw : 0.0;
+#pragma unroll
+            for (int j = 0; j < EPL; j++) {
+                const int e = sv.e(j);
+                wpj[j] = sv.w(p, ep, ps, e >= 0 ? e : 0, e >= 0 ? j * 64 + lane : 0);
+            }
+        } else {
+            ai = occ ? sv.w(p, L.se_e[lane], L.gi_slot[lane], ep, ps) : 0.0;
+        }
         const double wpp = sv.w(p, ep, ps, ep, ps);
         double zc = 0.0;
 #pragma unroll
@@ -827,7 +934,12 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
                 const int e = sv.e(j);
-                if (e >= 0) z[j] = fma(t, (double)sp * (sv.w(p, ep, ps, e, j * 64 + lane) - comb[j]), z[j]);
+                if (e >= 0) {
+                    double wj;
+                    if constexpr (UNCOND_GATHER<EPL>) wj = wpj[j];
+                    else wj = sv.w(p, ep, ps, e, j * 64 + lane);
+                    z[j] = fma(t, (double)sp * (wj - comb[j]), z[j]);
+                }
             }
             CLF_SYNC();
         }
@@ -2148,6 +2260,15 @@ template <typename T, class F>
 static bool clf_dispatch(int nx, int nu, int sid, int kind, F &&f)
 {
     static const int var = std::getenv("NMPC_CLF_VARIANT") ? std::atoi(std::getenv("NMPC_CLF_VARIANT")) : 0;
+    // (the force variants come first: the code object emits the kernels in this order, so the force kernels'
+    // placement does not move with the other shapes' code sizes)
+    if (nx == 4 && nu == 2 && kind != CLF_LOCK) {
+        if (kind == CLF_WLDS) f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>, true>{});
+        else if (kind == CLF_ONE) f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>, false, true>{});
+        else if (var == 1) f(Variant<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>{});
+        else f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>{});
+        return true;
+    }
     if (kind == CLF_LOCK) {   // fp64 only (the f64 MFMA tiles)
         if constexpr (std::is_same<T, double>::value) {
             if (nx == 13 && nu == 4 && sid == lpc::Quad13Structure::id) f(LockVariant<T, 13, 4, 4, 16, 8, 0, lpc::Quad13Structure>{});
@@ -2167,11 +2288,6 @@ static bool clf_dispatch(int nx, int nu, int sid, int kind, F &&f)
         f(Variant<T, 13, 4, 4, 16, 8, 0, lpc::DenseStructure<13, 4>>{});
     } else if (nx == 6 && nu == 2) {
         f(Variant<T, 6, 2, 5, 16, 8, 0, lpc::DenseStructure<6, 2>>{});
-    } else if (nx == 4 && nu == 2) {
-        if (kind == CLF_WLDS) f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>, true>{});
-        else if (kind == CLF_ONE) f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>, false, true>{});
-        else if (var == 1) f(Variant<T, 4, 2, 2, 32, 4, 2, lpc::DenseStructure<4, 2>>{});
-        else f(Variant<T, 4, 2, 2, 32, 4, 0, lpc::DenseStructure<4, 2>>{});
     } else {
         return false;
     }
