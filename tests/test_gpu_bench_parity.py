@@ -84,6 +84,38 @@ def test_bench_closed_loop_matches_oracle(golden, model, N, B):
 
 
 @pytest.mark.timeout(300)
+def test_force_config2_one_wave_variant_matches_oracle(monkeypatch):
+    """BASELINE config 2 (force N=20 B=1024 fp64) runs the one-wavefront-per-SIMD variant (CLF_ONE: batch <= the
+    device's SIMD count; its sweep pivots unrolled). Its states, sums and failures equal the default variant's
+    (NMPC_CLF_ONE=0) bit for bit — the arithmetic is the same — and every instance matches the C restatement of
+    the algorithm (oracle mode 1) over 43 steps."""
+    from drone_attitude_control_amd.batched import ClosedLoop, workload
+    from drone_attitude_control_amd.models import OCPS
+    from oracle import cref, models
+    B, N, steps = 1024, 20, (3, 20, 20)
+
+    def run(one):
+        monkeypatch.setenv("NMPC_CLF_ONE", one)
+        loop = ClosedLoop("force", B, N=N, seed=42)
+        for n in steps:
+            loop.run(n)
+        return loop.state(), loop.instance_stats()
+
+    S1, A1 = run("1")
+    S0, A0 = run("0")
+    assert np.array_equal(S1, S0) and np.array_equal(A1, A0)
+    table, off, x = workload("force", N, B, 42)
+    o = OCPS["force"](N).solver_options
+    ref = cref.ClosedLoopRef(models.force_model(N), "force", table, off, x, mode=1, seed=42,
+                             tol_comp=o.qp_solver_tol_comp, tol_res=o.qp_solver_tol_stat)
+    ref.run(sum(steps))
+    err = _rel(S1, ref.state)
+    assert err.max() < 1e-6, (err.max(), int(err.argmax()))
+    assert np.array_equal(A1[:, 2:], ref.acc[:, 2:])
+    np.testing.assert_allclose(A1[:, :2], ref.acc[:, :2], rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.timeout(300)
 def test_jerk_lockstep_variant_matches_oracle():
     """The jerk shape's lockstep kernel (opt-in, NMPC_CLF_LOCK=1: cl_lock_kernel with the jerk converter plant
     evaluated per instance in the four-instance layout and the cost on x_1 gathered from the MFMA tiles;
