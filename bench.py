@@ -249,8 +249,26 @@ def workload_label(model, tols, paths, kernel):
             f"full-solve options tol_comp {tols[0]:g}, tol_res {tols[1]:g}) + plant/noise advance + cost/AED")
 
 
+_JSON_FD = None
+
+
+def claim_stdout():
+    """Keep stdout for the one JSON line: everything else written to fd 1 from here on — RCCL's version banner at
+    the first collective, library prints — goes to stderr (the driver parses stdout)."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(line):
+    os.write(_JSON_FD if _JSON_FD is not None else 1, (json.dumps(line) + "\n").encode())
+
+
 def main():
     args = parse()
+    claim_stdout()
     world, rank, dist, device = init_dist(args)
     if args.mode == "solve":
         return main_solve(args, world, rank, dist, device)
@@ -399,7 +417,7 @@ def main():
                             "aed": red[1] / max(1.0, red[3]) / (2 if model != "quad13" else 3),
                             "failed_solves": int(red[2]), "instance_steps": int(red[3])},
         }
-        print(json.dumps(line))
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -571,7 +589,7 @@ def main_solve(args, world, rank, dist, device):
             "failed_solves": int(red[0]),
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
 
