@@ -193,10 +193,50 @@ def python_loop_rate(N, steps):
             "sample": f"{steps} steps of controllers.force_follow_trajectory (force, N={N}, B=1, fp64) in {el:.2f} s"}
 
 
+def fail(msg, code=2):
+    sys.stderr.write(f"bench.py: {msg}\n")
+    sys.exit(code)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` with N > 1 and no launcher around it (no WORLD_SIZE in the environment): start
+    the N ranks ourselves — torch.distributed.run as a child process, one rank per GPU, rendezvous on
+    127.0.0.1 — and relay rank 0's one JSON line. Runs before anything in this process imports torch or
+    touches the GPU (the parent only waits; it never execs). Exits non-zero when a rank fails or when the
+    line's n_gpus is not N."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", NMPC_BENCH_SELF_LAUNCH=str(args.gpus))
+    sys.stderr.write("bench.py: starting %d ranks: %s\n" % (args.gpus, " ".join(cmd)))
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)
+    out = p.stdout.decode(errors="replace")
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        sys.stderr.write(out)
+        fail(f"the {args.gpus}-rank run failed (exit {p.returncode})", p.returncode or 1)
+    line = json.loads(lines[-1])
+    if line.get("n_gpus") != args.gpus:
+        fail(f"the run reported n_gpus {line.get('n_gpus')}, asked for --gpus {args.gpus}", 3)
+    os.write(1, (lines[-1] + "\n").encode())
+    sys.exit(0)
+
+
 def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        fail(f"world size {world} (WORLD_SIZE) differs from --gpus {args.gpus}")
     dist = None
     device = local_rank
     # a process group whenever torch.distributed.run launched us (RANK in the environment), also at
@@ -206,6 +246,10 @@ def init_dist(args):
         import torch
         import torch.distributed as dist
         if args.dist_backend == "nccl":
+            # one GPU per rank (device_count() does not initialise the GPU on this image)
+            if torch.cuda.device_count() < world:
+                fail(f"backend nccl (RCCL) needs one GPU per rank: {world} ranks, "
+                     f"{torch.cuda.device_count()} visible GPUs (use --dist-backend gloo to rehearse)")
             torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
@@ -220,7 +264,9 @@ def parallelism_label(dist, world):
     if dist is None:
         return f"instance-sharded x{world}, single process (no collective)"
     be = dist.get_backend()
-    return f"instance-sharded x{world}, {'RCCL' if be == 'nccl' else be} stats reduce ({be} process group)"
+    how = (f", {world} ranks started by bench.py --gpus {world} (torch.distributed.run child)"
+           if os.environ.get("NMPC_BENCH_SELF_LAUNCH") else "")
+    return f"instance-sharded x{world}, {'RCCL' if be == 'nccl' else be} stats reduce ({be} process group){how}"
 
 
 def timing_block(regions, elapsed, note):
@@ -268,6 +314,10 @@ def emit(line):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        fail(f"--gpus {args.gpus}")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(args)
     claim_stdout()
     world, rank, dist, device = init_dist(args)
     if args.mode == "solve":
@@ -504,6 +554,10 @@ def main_solve(args, world, rank, dist, device):
         regions.append(t1 - t0)
         kms.append(s.get_stats("time_tot") * 1e3)   # the region's last launch (HIP events)
     s.solve()                                   # one synchronous solve: outputs, status and qp_iter to the host
+    counts = ({"listed": s.get_stats("fast_listed"), "parked": s.get_stats("fast_parked"),
+               "note": "the final solve's instances listed for fin64_kernel / parked for the list-mode IPM; every timed "
+                       "solve is complete in stream order (the three launches read their list lengths on the device)"}
+              if fast else None)
     status = s.get_batch_int("status")
     iters = s.get_batch_int("qp_iter")
     red, regions, kms = reduce_run(dist, np.array([float((status != 0).sum()), float(iters.sum()), float(B)]),
@@ -561,8 +615,9 @@ def main_solve(args, world, rank, dist, device):
                                      "committed PMC pass "
                                      f"({pmc.get('source', 'none for this config')}); min bytes = x0 + yref window "
                                      "in, full x/u trajectories out (SURVEY 8d)",
-                     "kernel_ms_note": "HIP events around the solve's launches (fast solve: sf_kernel + fin64_kernel "
-                                       "and, when any instance parks, the full solve of the parked ones)",
+                     "kernel_ms_note": "HIP events around the solve's launches (fast solve: sf_kernel, fin64_kernel "
+                                       "and the list-mode full IPM of the parked instances, the last two always "
+                                       "enqueued and empty when nothing is listed / parked)",
                      "gpu_mean_qp_iter": float(red[1] / max(1.0, red[2]))})
         what = (f"fp64 fast solve (sf_kernel: unconstrained solution by the Riccati recursion on the shared "
                 f"factorisation on the f64 matrix cores + bound test; fin64_kernel: active-set steps on W and the dual "
@@ -587,6 +642,7 @@ def main_solve(args, world, rank, dist, device):
                            steps_per_region=args.steps),
             "roofline": roof,
             "failed_solves": int(red[0]),
+            "fast_counts": counts,
             "cpu_baseline": cpu,
         }
         emit(line)

@@ -370,6 +370,10 @@ class AcadosOcpSolver:
             return float(s[3]) * 1e-3
         if field_ == "status":
             return self.get_status()
+        if field_ in ("fast_listed", "fast_parked"):   # the last fast solve waited for (batched extension)
+            s7 = np.zeros(7)
+            self._check(self.lib.nmpc_get_stats(self._h, _lib.dptr(s7), 7), "get_stats")
+            return int(s7[5 if field_ == "fast_listed" else 6])
         raise NmpcError(f"get_stats: unknown field '{field_}'")
 
     def print_statistics(self):

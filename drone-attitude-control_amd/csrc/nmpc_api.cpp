@@ -249,10 +249,9 @@ struct nmpc_solver {
     int *d_sfl = nullptr;                  // [0..4) two [listed, parked] counter pairs (solve i uses pair i & 1; its
                                            // fin64_kernel zeroes the other), [4..4+B) list, [4+B..4+2B) parked
     int sf_pair = 0;                       // the counter pair of the last fast solve
-    int sf_hint = 0;                       // listed instances of the last resolved fast solve (fin64's grid)
-    bool sf_fin_done = false;              // the last fast solve launched its finish (else sf_resolve does)
-    nmpc::ClFastParams<double> sf_fin{};   // ... and its parameters
-    int *h_sfpark = nullptr;               // pinned: the last resolved solve's [listed, parked] counts
+    int *h_sfpark = nullptr;               // pinned: the last fast solve's [listed, parked] counts (copied in
+                                           // stream order behind its kernels; valid once the stream has drained)
+    int sf_listed = 0, sf_parked = 0;      // ... as read at the last wait (nmpc_get_stats out[5], out[6])
     unsigned long long *d_sfcyc = nullptr; // timing builds (env NMPC_SF_CYCLES): sf_kernel's phase clocks
     size_t sfcyc_n = 0;
     int sf_kidx = -1;                      // lane-per-component kernel of the parked instances' full solves
@@ -278,6 +277,9 @@ struct nmpc_solver {
     int iter_log_steps = 0;       // steps in the log (the last fused launch; the lean loop: the last run)
     size_t iter_log_cap = 0;      // capacity of d_iter_log (ints)
     int *h_park = nullptr;        // pinned host word: the lean loop's parked count per round
+    int *h_parkr = nullptr;       // pinned: an asynchronous lean run's per-round counter pairs, CLF_ROUND_WORDS per chunk
+    size_t parkr_cap = 0;         // ... capacity (ints)
+    int clf_async_chunks = 0;     // chunks of the last asynchronous run whose counts h_parkr holds (0: none pending)
     std::vector<hipEvent_t> cl_events;
     double cl_last_ms = 0.0;
     double cost_s = 1.0;  // stage cost factor (time step or 1)
@@ -539,6 +541,7 @@ void free_all(nmpc_solver *h)
     if (h->ev_fb) hipEventDestroy(h->ev_fb);
     for (hipEvent_t e : h->cl_events) hipEventDestroy(e);
     if (h->h_park) hipHostFree(h->h_park);
+    if (h->h_parkr) hipHostFree(h->h_parkr);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
@@ -608,6 +611,10 @@ template <typename T>
 nmpc::ClParams<T> cl_params(nmpc_solver *h);
 
 constexpr int CL_FUSED_CHUNK = 64;   // closed-loop steps per fused solve launch
+constexpr int CLF_CHUNK = 64;        // closed-loop steps per lean-loop launch (bounded noise / log buffers)
+// the lean loop's asynchronous runs (sync = 0): per round of a chunk its own [park count, claim counter] pair,
+// after the park list in d_park
+constexpr int CLF_ROUND_WORDS = 2 * (CLF_CHUNK + 1);
 
 int fin32_setup(nmpc_solver *h);
 hipError_t fin32_enqueue(nmpc_solver *h);
@@ -621,19 +628,20 @@ struct ListArgs {
     const int *list;
     int kidx;
     void *scratch;
+    const int *count_dev = nullptr;   // the list's length on the device (count: the grid's capacity), or null
 };
 
 // cl_steps > 0: fused closed loop of that many steps (lane-per-component / wavefront kernels). fast: a plain
-// solve of an fp64 handle may take the fast solve (sf_enqueue; its parked instances run at sf_resolve) — the
-// per-step closed loop passes false: its advance kernel follows the solve on the stream with no host step between
-int sf_enqueue(nmpc_solver *h);
+// solve of an fp64 handle may take the fast solve (sf_enqueue: complete in stream order, so the per-step closed
+// loop's advance kernel can follow it on the stream with no host step between)
+int sf_enqueue(nmpc_solver *h, hipEvent_t e0, hipEvent_t e1);
 
 template <typename T>
 int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int cl_steps = 0, const ListArgs *la = nullptr,
            bool fast = true)
 {
     if (h->cond) return launch_cond<T>(h, e0, e1);
-    if (std::is_same<T, double>::value && fast && h->sfast && cl_steps == 0 && !la) return sf_enqueue(h);
+    if (std::is_same<T, double>::value && fast && h->sfast && cl_steps == 0 && !la) return sf_enqueue(h, e0, e1);
     nmpc::IpmParams<T> p{};
     int kidx = h->kidx;
     void *scratch = h->d_scratch;
@@ -643,6 +651,7 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
         if (la->scratch) scratch = la->scratch;
         p.cl_list = la->list;
         p.cl_count = la->count;
+        p.cl_count_dev = la->count_dev;
         p.cl_istep = h->d_istep;
         p.cl_noise_ld = la->noise_ld;
         p.cl_noise_step0 = la->step0;
@@ -727,11 +736,11 @@ int launch(nmpc_solver *h, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int
             h->d_cycles = nullptr;
         p.cycles = h->d_cycles;
     }
-    hipEventRecord(e0 ? e0 : h->ev0, h->stream);
-    hipError_t e = nmpc::ipm_launch<T>(kidx, p, h->stream);
+    hipError_t e = hipEventRecord(e0 ? e0 : h->ev0, h->stream);
+    if (e == hipSuccess) e = nmpc::ipm_launch<T>(kidx, p, h->stream);
     // fp32 solves: the exact finish (inside the timed pair: it is part of the solve)
     if (e == hipSuccess && cl_steps == 0 && !la && h->fin32) e = fin32_enqueue(h);
-    hipEventRecord(e1 ? e1 : h->ev1, h->stream);
+    if (e == hipSuccess) e = hipEventRecord(e1 ? e1 : h->ev1, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "ipm kernel launch");
     if (sweep_cycles && h->d_cycles) {
         // tuning aid (experiment builds with NMPC_SWEEP_TIMING): mean clock cycles per instance
@@ -1340,10 +1349,9 @@ int nmpc_synchronize(nmpc_solver *h)
     if (!h) return NMPC_EINVAL;
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize");
-    const int r = sf_resolve(h);   // the last fast solve's parked instances (full solves), if any
+    const int r = sf_resolve(h);   // the last fast solve's listed / parked counts (its kernels are done)
     if (r < 0) return r;
-    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize");
-    hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1);
+    if ((e = hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1)) != hipSuccess) return hip_fail(h, e, "solve timing events");
     return 0;
 }
 
@@ -1399,10 +1407,10 @@ int nmpc_solve(nmpc_solver *h)
     }
     int r = h->precision == NMPC_FP64 ? launch<double>(h) : launch<float>(h);
     if (r < 0) return r;
-    if ((r = sf_resolve(h)) < 0) return r;   // fast solve: full solves of the parked instances, if any
-    if ((r = download_outputs(h)) < 0) return r;
+    if ((r = download_outputs(h)) < 0) return r;   // waits for the stream
+    if ((r = sf_resolve(h)) < 0) return r;         // fast solve: its listed / parked counts
     h->out_from_loop = false;
-    hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1);
+    if ((e = hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1)) != hipSuccess) return hip_fail(h, e, "solve timing events");
     int st = 0;
     for (int b = 0; b < h->batch; b++) st = std::max(st, (int)h->h_status[b]);
     return st;
@@ -1458,8 +1466,8 @@ int nmpc_get_stats(nmpc_solver *h, double *st, int n)
         mean += h->h_iters[b];
         nf += h->h_status[b] != 0;
     }
-    const double v[5] = {mx, mean / h->batch, nf, (double)h->last_ms, 1.0};
-    for (int i = 0; i < n && i < 5; i++) st[i] = v[i];
+    const double v[7] = {mx, mean / h->batch, nf, (double)h->last_ms, 1.0, (double)h->sf_listed, (double)h->sf_parked};
+    for (int i = 0; i < n && i < 7; i++) st[i] = v[i];
     return 0;
 }
 
@@ -1583,7 +1591,7 @@ int cl_step_enqueue(nmpc_solver *h, int launch_idx)
     nmpc::ClParams<T> p = cl_params<T>(h);
     hipError_t e = nmpc::cl_prepare_launch<T>(p, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "closed-loop prepare");
-    const int r = launch<T>(h, h->cl_events[2 * launch_idx], h->cl_events[2 * launch_idx + 1], 0, nullptr, false);
+    const int r = launch<T>(h, h->cl_events[2 * launch_idx], h->cl_events[2 * launch_idx + 1]);
     if (r < 0) return r;
     e = nmpc::cl_advance_launch<T>(p, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "closed-loop advance");
@@ -1879,7 +1887,6 @@ int sf_setup(nmpc_solver *h)
     if (e == hipSuccess) e = hipMemset(h->d_sfl, 0, 4 * sizeof(int));
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_create: fast-solve upload");
     h->h_sfpark[0] = h->h_sfpark[1] = 0;
-    h->sf_hint = h->batch;   // the first solve's finish runs on every resident workgroup
     h->f64_nslot = (int)el.size();
     h->f64_nfree = (int)fr.size();
     h->f64_resident = res;
@@ -1888,9 +1895,11 @@ int sf_setup(nmpc_solver *h)
     return 0;
 }
 
-// one fast solve on the handle's stream: list / park counters reset, sf_kernel, fin64_kernel, the parked count
-// to the pinned host word (sf_resolve reads it once the stream has drained)
-int sf_enqueue(nmpc_solver *h)
+// one fast solve on the handle's stream, complete in stream order: sf_kernel (every instance's unconstrained
+// solution; the violated ones listed), fin64_kernel (active-set steps for the listed), the full IPM in list mode
+// for what the finish parked — no host step between them, so kernels the caller enqueues behind the solve read
+// final outputs. Timed from e0 (or ev0) to e1 (or ev1); the listed / parked counts follow to the pinned host words
+int sf_enqueue(nmpc_solver *h, hipEvent_t e0, hipEvent_t e1)
 {
     const int nx = h->nx, nu = h->nu, nz = nx + nu;
     const char *m = (const char *)h->d_model;
@@ -1911,8 +1920,8 @@ int sf_enqueue(nmpc_solver *h)
     sp.uout = (double *)h->d_u;
     sp.status = h->d_status;
     sp.iters = h->d_iters;
-    h->sf_pair ^= 1;
-    int *cnt = h->d_sfl + 2 * h->sf_pair;
+    const int pair = h->sf_pair ^ 1;   // this solve's counter pair (zeroed by the last solve's sf_kernel)
+    int *cnt = h->d_sfl + 2 * pair;
     sp.list_count = cnt;
     sp.list = h->d_sfl + 4;
     nmpc::ClFastParams<double> p{};
@@ -1945,7 +1954,7 @@ int sf_enqueue(nmpc_solver *h)
     p.work_list = sp.list;
     p.work_count = cnt;
     p.z0_xu = 1;
-    sp.next_counts = h->d_sfl + 2 * (h->sf_pair ^ 1);
+    sp.next_counts = h->d_sfl + 2 * (pair ^ 1);
     // env NMPC_SF_CYCLES=<file> with a timing build (-DNMPC_SF_TIMING): per-wavefront phase clocks of this launch,
     // appended to <file> at the next sf_resolve ([waves][8] uint64, tools/sf_phases.py)
     static const char *sf_cyc = std::getenv("NMPC_SF_CYCLES");
@@ -1954,55 +1963,46 @@ int sf_enqueue(nmpc_solver *h)
         if (hipMalloc((void **)&h->d_sfcyc, h->sfcyc_n * sizeof(unsigned long long)) != hipSuccess) h->d_sfcyc = nullptr;
     }
     sp.cycles = h->d_sfcyc;
-    hipEventRecord(h->ev0, h->stream);
-    hipError_t e = nmpc::sf_launch(nx, nu, sp, h->stream);
-    // the finish only when the last resolved solve listed instances: a launch whose every workgroup exits at once
-    // still costs ~4 us (rocprofv3, quad13 B = 8192, where no first-step QP is listed). A skipped finish with a
-    // non-empty list runs in sf_resolve, before anything reads the outputs
-    h->sf_fin_done = h->sf_hint > 0;
-    if (e == hipSuccess && h->sf_fin_done)
-        e = nmpc::fin64_launch(nx, nu, p, h->f64_resident, h->sf_hint, h->stream) ? hipGetLastError() : hipErrorInvalidValue;
-    hipEventRecord(h->ev1, h->stream);
-    if (e != hipSuccess) return hip_fail(h, e, "fast solve launch");
-    h->sf_fin = p;
+    hipError_t e = hipEventRecord(e0 ? e0 : h->ev0, h->stream);
+    if (e == hipSuccess) e = nmpc::sf_launch(nx, nu, sp, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "fast solve launch (sf_kernel)");
+    // sf_kernel ran: it zeroed the other pair for the next solve, whatever happens below
+    h->sf_pair = pair;
+    // the finish of the listed instances, always enqueued: the list's length is read on the device, so the solve
+    // is complete in stream order (an empty list: every workgroup returns at once)
+    if ((e = nmpc::fin64_launch(nx, nu, p, h->f64_resident, h->stream)) != hipSuccess)
+        return hip_fail(h, e, "fast solve launch (fin64_kernel)");
+    // the instances the finish parked: the cold full IPM + exact finish in list mode, the park count read on the
+    // device (grid sized for the whole batch; workgroups past the count return before any setup), timed from ev_fb
+    ListArgs la{h->batch, 0, 0, h->d_sfl + 4 + h->batch, h->sf_kidx, h->d_sf_scratch};
+    la.count_dev = cnt + 1;
+    const int r = launch<double>(h, h->ev_fb, e1 ? e1 : h->ev1, 0, &la);
+    if (r < 0) return r;
+    // the counts behind the kernels, for nmpc_get_stats (read at the next wait)
+    if ((e = hipMemcpyAsync(h->h_sfpark, cnt, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+        return hip_fail(h, e, "fast solve counts");
     h->sf_pending = true;
     return 0;
 }
 
-// after a fast solve: waits for it; the instances fin64_kernel parked (certified-infeasible QPs, sets the
-// active-set finish did not settle) get the full IPM + exact finish (ipm_lpc_kernel in list mode, cold), timed
-// into the solve's event pair
+// after the stream has drained: the last fast solve's listed / parked counts; timing builds dump sf_kernel's clocks
 int sf_resolve(nmpc_solver *h)
 {
     if (!h->sf_pending) return 0;
     h->sf_pending = false;
-    // the last solve's counter pair (its finish zeroed only the other one), read once the stream has drained
-    hipError_t e = hipMemcpyAsync(h->h_sfpark, h->d_sfl + 2 * h->sf_pair, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    if (e != hipSuccess) return hip_fail(h, e, "fast solve");
-    h->sf_hint = h->h_sfpark[0];
-    if (!h->sf_fin_done && h->sf_hint > 0) {   // the finish this solve skipped: now, timed into its event pair
-        hipEventRecord(h->ev_fb, h->stream);
-        if (!nmpc::fin64_launch(h->nx, h->nu, h->sf_fin, h->f64_resident, h->sf_hint, h->stream))
-            return h->fail(NMPC_EDEVICE, "fast solve: finish launch");
-        hipEventRecord(h->ev1, h->stream);
-        e = hipMemcpyAsync(h->h_sfpark, h->d_sfl + 2 * h->sf_pair, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-        if (e != hipSuccess) return hip_fail(h, e, "fast solve finish");
-    }
+    h->sf_listed = h->h_sfpark[0];
+    h->sf_parked = h->h_sfpark[1];
     if (h->d_sfcyc) {
         static const char *sf_cyc = std::getenv("NMPC_SF_CYCLES");
         std::vector<unsigned long long> cy(h->sfcyc_n);
-        if (hipMemcpy(cy.data(), h->d_sfcyc, cy.size() * sizeof(cy[0]), hipMemcpyDeviceToHost) == hipSuccess)
-            if (FILE *f = std::fopen(sf_cyc, "ab")) {
-                std::fwrite(cy.data(), sizeof(cy[0]), cy.size(), f);
-                std::fclose(f);
-            }
+        const hipError_t e = hipMemcpy(cy.data(), h->d_sfcyc, cy.size() * sizeof(cy[0]), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_fail(h, e, "sf_kernel clocks");
+        if (FILE *f = std::fopen(sf_cyc, "ab")) {
+            std::fwrite(cy.data(), sizeof(cy[0]), cy.size(), f);
+            std::fclose(f);
+        }
     }
-    const int parked = h->h_sfpark[1];
-    if (parked <= 0) return 0;
-    const ListArgs la{parked, 0, 0, h->d_sfl + 4 + h->batch, h->sf_kidx, h->d_sf_scratch};
-    return launch<double>(h, h->ev_fb, h->ev1, 0, &la);
+    return 0;
 }
 
 // The lean closed loop (nmpc_cl_fast.hip) for this handle: fp64 with the exact finish, or fp32 (the tables
@@ -2087,7 +2087,7 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     bool ok = hipMalloc(&h->d_fsT, tot * es) == hipSuccess &&
               hipMalloc((void **)&h->d_fsI, itot * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_istep, (size_t)h->batch * sizeof(int)) == hipSuccess &&
-              hipMalloc((void **)&h->d_park, (size_t)(h->batch + 2) * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_park, (size_t)(h->batch + 2 + CLF_ROUND_WORDS) * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_flags, (size_t)h->batch * (nslot + 1)) == hipSuccess;   // + the order bytes
     if (ok && fk != h->kidx)
         ok = hipMalloc(&h->d_clf_scratch, (f64 ? nmpc::ipm_scratch_elems<double>(fk, h->batch, N)
@@ -2244,16 +2244,18 @@ hipEvent_t cl_event(nmpc_solver *h, size_t i)
     return h->cl_events[i];
 }
 
-constexpr int CLF_CHUNK = 64;   // closed-loop steps per lean-loop launch (bounded noise / log buffers)
-
 // `steps` closed-loop steps on the lean loop, in chunks of at most CLF_CHUNK steps: per chunk the noise
 // draws, then rounds of (fast kernel over every instance up to the chunk's target step; the count of
 // parked instances back to the host — the one host wait per round; one full solve + plant step per
 // parked instance, ipm_lpc_kernel in list mode) until none is parked. Returns the number of kernel
 // launches (each bracketed by an event pair), or < 0. h->clf_parked / clf_rounds: the run's parked
 // solves and fast launches.
+// async (nmpc_closed_loop_run with sync = 0): no host wait at all — every chunk enqueues all its possible rounds
+// (chunk length + 1), round r > 0's fast kernel guarded by round r - 1's park count on the device (0: every
+// workgroup returns at entry) and each round's list-mode full solve sized by its own count on the device; the
+// per-round counts follow to pinned host memory and nmpc_closed_loop_stats sums them.
 template <typename T>
-int clf_run(nmpc_solver *h, int steps)
+int clf_run(nmpc_solver *h, int steps, bool async)
 {
     const size_t need = (size_t)h->batch * std::min(steps, CLF_CHUNK);
     if (h->fnoise_cap < need) {
@@ -2292,6 +2294,23 @@ int clf_run(nmpc_solver *h, int steps)
     }
     int launches = 0;
     h->clf_parked = h->clf_rounds = 0;
+    h->clf_async_chunks = 0;
+    // (the diagnostic modes read the device after every round: host-driven rounds)
+    if (iter_log || dbg || check || std::getenv("NMPC_CLF_CYCLES")) async = false;
+    if (async) {
+        const size_t need_r = (size_t)((steps + CLF_CHUNK - 1) / CLF_CHUNK) * CLF_ROUND_WORDS;
+        if (h->parkr_cap < need_r) {
+            hipError_t e = hipStreamSynchronize(h->stream);   // no copy into the old buffer is pending
+            if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_run");
+            if (h->h_parkr) hipHostFree(h->h_parkr);
+            h->h_parkr = nullptr;
+            h->parkr_cap = 0;
+            if ((e = hipHostMalloc((void **)&h->h_parkr, need_r * sizeof(int), hipHostMallocDefault)) != hipSuccess)
+                return hip_fail(h, e, "nmpc_closed_loop_run: pinned round counters");
+            h->parkr_cap = need_r;
+        }
+    }
+    int *d_rc = h->d_park + 2 + h->batch;   // asynchronous runs: the rounds' [park count, claim counter] pairs
     // env NMPC_CLF_CYCLES=<file> with a timing build (-DNMPC_CLF_TIMING): per-instance phase cycles of the
     // run, [B][20] uint64, appended to <file> (tools/clf_phases.py)
     static const char *cyc_path = std::getenv("NMPC_CLF_CYCLES");
@@ -2314,15 +2333,30 @@ int clf_run(nmpc_solver *h, int steps)
             fp.iter_log = h->d_iter_log;
             h->iter_log_steps = n + 2;   // + the instance start / end rows
         }
+        if (async && (e = hipMemsetAsync(d_rc, 0, (size_t)2 * (n + 1) * sizeof(int), h->stream)) != hipSuccess)
+            return hip_fail(h, e, "round counters reset");
         for (int round = 0; round <= n; round++) {
-            if (round > 0 && (e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess)
+            if (!async && round > 0 && (e = hipMemsetAsync(h->d_park, 0, 2 * sizeof(int), h->stream)) != hipSuccess)
                 return hip_fail(h, e, "park reset");
-            hipEventRecord(cl_event(h, 2 * launches), h->stream);
-            e = nmpc::cl_fast_launch<T>(h->nx, h->nu, h->clf_sid, h->clf_kind, fp, h->batch, h->clf_resident, h->stream);
-            hipEventRecord(cl_event(h, 2 * launches + 1), h->stream);
+            fp.park_count = async ? d_rc + 2 * round : h->d_park;
+            fp.run_if = async && round > 0 ? d_rc + 2 * (round - 1) : nullptr;
+            hipEvent_t ea = cl_event(h, 2 * launches), eb = cl_event(h, 2 * launches + 1);
+            if (!ea || !eb) return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: hipEventCreate");
+            e = hipEventRecord(ea, h->stream);
+            if (e == hipSuccess)
+                e = nmpc::cl_fast_launch<T>(h->nx, h->nu, h->clf_sid, h->clf_kind, fp, h->batch, h->clf_resident, h->stream);
+            if (e == hipSuccess) e = hipEventRecord(eb, h->stream);
             launches++;
             h->clf_rounds++;
             if (e != hipSuccess) return hip_fail(h, e, "lean closed-loop kernel launch");
+            if (async) {   // this round's parked instances, their count read on the device
+                ListArgs la{h->batch, h->cl_step, n, h->d_park + 2, h->clf_kidx, h->d_clf_scratch};
+                la.count_dev = fp.park_count;
+                const int r = launch<T>(h, cl_event(h, 2 * launches), cl_event(h, 2 * launches + 1), 1, &la);
+                launches++;
+                if (r < 0) return r;
+                continue;
+            }
             e = hipMemcpyAsync(h->h_park, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
             if (e != hipSuccess) return hip_fail(h, e, "lean closed loop (fast kernel)");
@@ -2344,6 +2378,15 @@ int clf_run(nmpc_solver *h, int steps)
             launches++;
             if (r < 0) return r;
             if (dbg && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "lean closed loop (list-mode fallback)");
+        }
+        if (async) {   // the rounds' counts, summed by nmpc_closed_loop_stats
+            e = hipMemcpyAsync(h->h_parkr + (size_t)h->clf_async_chunks * CLF_ROUND_WORDS, d_rc,
+                               (size_t)2 * (n + 1) * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+            if (e != hipSuccess) return hip_fail(h, e, "round counters");
+            if (n + 1 < CLF_CHUNK + 1)   // the rest of the chunk's slot: no rounds
+                std::fill(h->h_parkr + (size_t)h->clf_async_chunks * CLF_ROUND_WORDS + 2 * (n + 1),
+                          h->h_parkr + (size_t)(h->clf_async_chunks + 1) * CLF_ROUND_WORDS, 0);
+            h->clf_async_chunks++;
         }
         h->cl_step = target;
         done += n;
@@ -2508,7 +2551,7 @@ int nmpc_closed_loop_run(nmpc_solver *h, int steps, int sync)
     const bool lean = h->clf && !(fused_env && fused_env[0] == '0');
     h->clf_parked = h->clf_rounds = 0;
     if (lean) {
-        launches = steps <= 0 ? 0 : (h->precision == NMPC_FP64 ? clf_run<double>(h, steps) : clf_run<float>(h, steps));
+        launches = steps <= 0 ? 0 : (h->precision == NMPC_FP64 ? clf_run<double>(h, steps, !sync) : clf_run<float>(h, steps, !sync));
         if (launches < 0) return launches;
     } else if (cl_fused(h)) {
         if (h->fnoise_cap < (size_t)h->batch * CL_FUSED_CHUNK) {
@@ -2558,19 +2601,31 @@ int nmpc_closed_loop_stats(nmpc_solver *h, double *out, int n)
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "nmpc_closed_loop_stats");
     std::vector<double> acc((size_t)h->batch * 4);
-    hipMemcpy(acc.data(), h->d_acc, acc.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if ((e = hipMemcpy(acc.data(), h->d_acc, acc.size() * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(h, e, "nmpc_closed_loop_stats (accumulators)");
     double v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = 0; b < h->batch; b++)
         for (int j = 0; j < 4; j++) v[j] += acc[(size_t)b * 4 + j];
     double ms = 0.0;
     for (int s = 0; s < h->cl_last_launches; s++) {
+        // every launch of the run recorded its pair (launch / sf_enqueue / clf_run); a failed read is an error,
+        // not a launch to leave out of the kernel time
         float t = 0.f;
-        if (hipEventElapsedTime(&t, h->cl_events[2 * s], h->cl_events[2 * s + 1]) == hipSuccess) ms += t;
+        if ((e = hipEventElapsedTime(&t, h->cl_events[2 * s], h->cl_events[2 * s + 1])) != hipSuccess)
+            return hip_fail(h, e, ("nmpc_closed_loop_stats: timing events of launch " + std::to_string(s)).c_str());
+        ms += t;
     }
     v[4] = ms;
     v[5] = h->cl_last_launches;
+    if (h->clf_async_chunks > 0) {   // an asynchronous lean run: its rounds' park counts (pinned, the stream has drained)
+        h->clf_parked = 0;
+        for (int c = 0; c < h->clf_async_chunks; c++)
+            for (int r = 0; r <= CLF_CHUNK; r++) h->clf_parked += h->h_parkr[(size_t)c * CLF_ROUND_WORDS + 2 * r];
+        h->clf_async_chunks = 0;
+    }
     std::vector<int32_t> it(h->batch);
-    hipMemcpy(it.data(), h->d_iters, h->batch * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if ((e = hipMemcpy(it.data(), h->d_iters, h->batch * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(h, e, "nmpc_closed_loop_stats (qp_iter)");
     double mean = 0.0;
     for (int b = 0; b < h->batch; b++) mean += it[b];
     v[6] = mean / h->batch;

@@ -1448,6 +1448,7 @@ __device__ inline void claim_order(unsigned short *ord, const unsigned char *har
 template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP, bool WL = false, bool SW2 = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0 ? MW : 1, 8))) void cl_fast_kernel(ClFastParams<T> p)
 {
+    if (p.run_if && __builtin_amdgcn_readfirstlane(*p.run_if) == 0) return;   // an empty asynchronous round
     constexpr int NZ = NX + NU, NSLOT = EPL * 64;
     static_assert(NX < 32 && NZ <= 64, "lane-distributed state");
     __shared__ Lds<NSLOT, NZ, WSM, SW2> lds_all[WPB];
@@ -1779,6 +1780,7 @@ __global__ __launch_bounds__(64 * WPB) void fin64_kernel(ClFastParams<double> p)
 template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0 ? MW : 1, MW > 0 ? MW : 8))) void cl_lock_kernel(ClFastParams<T> p)
 {
+    if (p.run_if && __builtin_amdgcn_readfirstlane(*p.run_if) == 0) return;   // an empty asynchronous round
     constexpr int NZ = NX + NU, NSLOT = EPL * 64, NT = NSLOT / 16, KC = (NX + 3) / 4, KU = (NU + 3) / 4;
     static_assert(NX <= 16 && NU <= 4 && NZ <= 64 && NT <= 32, "lockstep layout: states in 4 chunks, inputs in one");
     __shared__ Lds<NSLOT, NZ, WSM> lds_all[WPB];
@@ -2321,7 +2323,7 @@ hipError_t cl_fast_launch(int nx, int nu, int sid, int kind, const ClFastParams<
         // the lockstep kernel: four instances per wavefront
         const int wv = kind == CLF_LOCK ? (waves + 3) / 4 : waves;
         const int blocks = std::max(1, std::min((wv + V::WPB - 1) / V::WPB, resident));
-        hipLaunchKernelGGL(V::kernel(), dim3(blocks), dim3(64 * V::WPB), 0, s, p);
+        NMPC_LAUNCH(V::kernel(), dim3(blocks), dim3(64 * V::WPB), 0, s, p);
     });
     return ok ? hipGetLastError() : hipErrorInvalidValue;
 }
@@ -2331,7 +2333,7 @@ template hipError_t cl_fast_launch<double>(int, int, int, int, const ClFastParam
 hipError_t fin32_z0_launch(const Fin32Z0Params &p, hipStream_t s)
 {
     if (p.m16 % 16 || p.kp % 4 || p.B < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(clf::fin32_z0_kernel<4>, dim3((p.B + 15) / 16), dim3(256), 0, s, p);
+    NMPC_LAUNCH(clf::fin32_z0_kernel<4>, dim3((p.B + 15) / 16), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -2390,21 +2392,25 @@ int fin64_resident(int nx, int nu, int nslot, int device)
     return res;
 }
 
-// grid: enough workgroups for `hint` listed instances (the host's last observation: the list's length is known on
-// the device only), at most the resident ones; the persistent loop covers any longer list, idle workgroups exit
-bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, int hint, hipStream_t s)
+// grid: the resident workgroups, at most one per wpb instances of the batch. The list's length is known on the device
+// only (sf_kernel fills it on the same stream), so the grid covers the longest list the persistent loop may meet;
+// workgroups past the list's end return before any setup. hipErrorInvalidValue: no compiled finish for the shape
+hipError_t fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, hipStream_t s)
 {
-    return fin64_dispatch(nx, nu, p.nslot, [&](auto k, int wpb) {
-        const int blocks = std::max(1, std::min((std::min(hint, p.B) + wpb - 1) / wpb, resident));
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, s, p);
+    hipError_t e = hipErrorInvalidValue;
+    fin64_dispatch(nx, nu, p.nslot, [&](auto k, int wpb) {
+        const int blocks = std::max(1, std::min((p.B + wpb - 1) / wpb, resident));
+        NMPC_LAUNCH(k, dim3(blocks), dim3(64 * wpb), 0, s, p);
+        e = hipGetLastError();
     });
+    return e;
 }
 
 bool fin32_launch(int nx, int nu, int, const ClFastParams<float> &p, int resident, hipStream_t s)
 {
     return fin32_dispatch(nx, nu, p.nslot, [&](auto k, int wpb) {
         const int blocks = std::max(1, std::min((p.B + wpb - 1) / wpb, resident));
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, s, p);
+        NMPC_LAUNCH(k, dim3(blocks), dim3(64 * wpb), 0, s, p);
     });
 }
 template hipError_t cl_fast_launch<float>(int, int, int, int, const ClFastParams<float> &, int, int, hipStream_t);

@@ -86,7 +86,7 @@ hipError_t cl_noise_launch(const ClParams<T> &p, int step0, int nsteps, double *
 {
     const size_t total = (size_t)p.B * nsteps;
     const int blocks = (int)std::max<size_t>(1, std::min<size_t>((total + 255) / 256, 4096));
-    hipLaunchKernelGGL(cl_noise_kernel<T>, dim3(blocks), dim3(256), 0, s, p, step0, nsteps, out, zero2);
+    NMPC_LAUNCH(cl_noise_kernel<T>, dim3(blocks), dim3(256), 0, s, p, step0, nsteps, out, zero2);
     return hipGetLastError();
 }
 
@@ -95,7 +95,7 @@ hipError_t cl_prepare_launch(const ClParams<T> &p, hipStream_t s)
 {
     const size_t total = (size_t)p.B * (p.N * p.ny + p.ny_e);
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(cl_prepare_kernel<T>, dim3(blocks), dim3(256), 0, s, p);
+    NMPC_LAUNCH(cl_prepare_kernel<T>, dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -103,10 +103,10 @@ template <typename T>
 hipError_t cl_advance_launch(const ClParams<T> &p, hipStream_t s)
 {
     if (p.plant == 0 && p.nx == 13 && p.nu == 4) {   // quad13 (the headline model)
-        hipLaunchKernelGGL((cl_model_advance_kernel<T, 13, 4>), dim3((p.B + 255) / 256), dim3(256), 0, s, p);
+        NMPC_LAUNCH((cl_model_advance_kernel<T, 13, 4>), dim3((p.B + 255) / 256), dim3(256), 0, s, p);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(cl_advance_kernel<T>, dim3((p.B + 255) / 256), dim3(256), 0, s, p);
+    NMPC_LAUNCH(cl_advance_kernel<T>, dim3((p.B + 255) / 256), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -704,7 +704,7 @@ static hipError_t launch_cond_rcuc(const CondParams<T> &p, int wpb, size_t lds, 
                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (set != hipSuccess) return set;
     }
-    hipLaunchKernelGGL((cond::cond_ipm_kernel<T, RC, UC>), dim3(blocks), dim3(64 * wpb), lds, s, p);
+    NMPC_LAUNCH((cond::cond_ipm_kernel<T, RC, UC>), dim3(blocks), dim3(64 * wpb), lds, s, p);
     return hipGetLastError();
 }
 

@@ -6,6 +6,15 @@
 
 #include <vector>
 
+// A kernel launch whose error check sees that launch alone: hipLaunchKernelGGL reports through the thread's
+// sticky last-error word, so a failure of an earlier, unrelated call (already reported at its own call site —
+// every HIP return in nmpc_api.cpp is checked) is cleared first instead of being blamed on this launch.
+#define NMPC_LAUNCH(...)        \
+    do {                        \
+        (void)hipGetLastError(); \
+        hipLaunchKernelGGL(__VA_ARGS__); \
+    } while (0)
+
 namespace nmpc {
 
 // closed-loop step kernels (nmpc_closed_loop.hip)
@@ -89,7 +98,9 @@ struct IpmParams {
     // noise cl_noise[inst * cl_noise_ld + step - cl_noise_step0]; the solution's active flags to
     // cl_flags[inst][cl_eslot[k nz + r]] (bounded elements)
     const int *cl_list;
-    int cl_count;
+    int cl_count;                 // list length; with cl_count_dev: the grid's capacity (an upper bound)
+    const int *cl_count_dev;      // or null: the list length on the device (read by the kernel), so the list can be
+                                  // filled by an earlier kernel of the same stream with no host round trip
     int *cl_istep;
     int cl_noise_ld, cl_noise_step0;
     signed char *cl_flags;
@@ -140,6 +151,8 @@ struct ClFastParams {
                                   // nmpc_closed_loop_set_outputs); the loop itself reads only u_0 / x_1
     int *status, *iters;
     int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
+    const int *run_if;            // or null: the launch runs only if *run_if != 0 (the lean loop's asynchronous rounds:
+                                  // the previous round's park count), else every workgroup returns at entry
     int *iter_log;                // optional [steps][B]: active-set steps (<= 255) | status << 8 | wall-clock ticks (<= 32767) << 16
     unsigned long long *cycles;   // diagnostic builds (NMPC_CLF_TIMING): [B][14] phase cycles / counts per instance
     unsigned *check;              // checked builds (NMPC_CLF_CHECK): bit mask of the failed index checks
@@ -186,8 +199,9 @@ struct SfParams {
 int sf_table_words(int nx, int nu);
 size_t sf_lds_bytes(int nx, int nu, int N);
 hipError_t sf_launch(int nx, int nu, const SfParams &p, hipStream_t s);
-// the active-set finish of the instances sf_kernel listed (fp64; shapes and slot counts as fin32)
-bool fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, int hint, hipStream_t s);
+// the active-set finish of the instances sf_kernel listed (fp64; shapes and slot counts as fin32); the list's
+// length is read on the device
+hipError_t fin64_launch(int nx, int nu, const ClFastParams<double> &p, int resident, hipStream_t s);
 int fin64_resident(int nx, int nu, int nslot, int device);
 // compiled fast kernels: EPL slots per lane (0 if none for this shape)
 int cl_fast_epl(int nx, int nu);

@@ -1184,7 +1184,7 @@ static hipError_t launch_ipm(const IpmParams<T> &p, hipStream_t s)
 {
     const int waves = (p.B + IPW - 1) / IPW;
     const int blocks = (waves + WPB - 1) / WPB;
-    hipLaunchKernelGGL((ipm_kernel<T, NX, NU, IPW, WPB, MW>), dim3(blocks), dim3(64 * WPB), 0, s, p);
+    NMPC_LAUNCH((ipm_kernel<T, NX, NU, IPW, WPB, MW>), dim3(blocks), dim3(64 * WPB), 0, s, p);
     return hipGetLastError();
 }
 

@@ -289,7 +289,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW, 8)
     const long long inst_raw = (long long)wg * IPW + grp;
     // list mode (the lean closed loop's fallback): lane group g solves instance cl_list[g]
     const bool lmode = p.cl_list != nullptr;
-    const bool inst_ok = grp < IPW && inst_raw < (lmode ? (long long)p.cl_count : (long long)p.B);
+    // a list whose length is on the device (written by an earlier kernel of the stream): workgroups past it
+    // leave before any setup (the grid is sized for the longest possible list)
+    const long long lcount = lmode ? (p.cl_count_dev ? (long long)__builtin_amdgcn_readfirstlane(*p.cl_count_dev)
+                                                     : (long long)p.cl_count)
+                                   : 0;
+    if (lmode && (long long)blockIdx.x * WPB * IPW >= lcount) return;
+    const bool inst_ok = grp < IPW && inst_raw < (lmode ? lcount : (long long)p.B);
     const int inst = inst_ok ? (lmode ? p.cl_list[inst_raw] : (int)inst_raw) : 0;   // idle lanes read instance 0, never write outputs
 
     // ---- model constants -> LDS (once per workgroup)
@@ -2348,7 +2354,7 @@ hipError_t launch_ipm_lpc(const IpmParams<T> &p, hipStream_t s)
     const int waves = ((p.cl_list ? p.cl_count : p.B) + Gm::IPW - 1) / Gm::IPW;
     const int blocks = (waves + WPB - 1) / WPB;
     if (blocks < 1) return hipSuccess;
-    hipLaunchKernelGGL((lpc::ipm_lpc_kernel<T, NX, NU, WPB, MW, SP>), dim3(blocks), dim3(64 * WPB), 0, s, p);
+    NMPC_LAUNCH((lpc::ipm_lpc_kernel<T, NX, NU, WPB, MW, SP>), dim3(blocks), dim3(64 * WPB), 0, s, p);
     return hipGetLastError();
 }
 

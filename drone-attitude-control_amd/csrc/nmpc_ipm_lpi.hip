@@ -716,7 +716,7 @@ hipError_t launch_ipm_lpi(const IpmParams<T> &p, hipStream_t s)
     const long long waves = ((long long)p.B + W - 1) / W;
     const int wpb = 4;
     const int blocks = (int)((waves + wpb - 1) / wpb);
-    hipLaunchKernelGGL((lpi::ipm_lpi_kernel<T, NX, NU, SP>), dim3(blocks), dim3(64 * wpb), 0, s, p);
+    NMPC_LAUNCH((lpi::ipm_lpi_kernel<T, NX, NU, SP>), dim3(blocks), dim3(64 * wpb), 0, s, p);
     return hipGetLastError();
 }
 

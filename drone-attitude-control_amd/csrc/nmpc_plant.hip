@@ -60,7 +60,7 @@ hipError_t plant_step_launch(int batch, int num_stages, double T, double mass, d
                              const double *u, double *x_out, hipStream_t s)
 {
     const int blocks = (batch + 255) / 256;
-    hipLaunchKernelGGL(plant_step_kernel, dim3(blocks), dim3(256), 0, s, batch, num_stages, T, mass, g, x_in, u,
+    NMPC_LAUNCH(plant_step_kernel, dim3(blocks), dim3(256), 0, s, batch, num_stages, T, mass, g, x_in, u,
                        x_out);
     return hipGetLastError();
 }

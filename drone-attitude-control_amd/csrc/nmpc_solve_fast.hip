@@ -380,7 +380,7 @@ hipError_t sf_launch(int nx, int nu, const SfParams &p, hipStream_t s)
         const size_t lds = sf_lds(p.N, wpb, ts, kw, sch);
         if (lds > 160 * 1024 || p.B < 1) return;
         const int per_wg = wpb * ipw;
-        hipLaunchKernelGGL(k, dim3((p.B + per_wg - 1) / per_wg), dim3(64 * wpb), lds, s, p);
+        NMPC_LAUNCH(k, dim3((p.B + per_wg - 1) / per_wg), dim3(64 * wpb), lds, s, p);
         e = hipGetLastError();
     });
     return e;

@@ -171,12 +171,12 @@ int nmpc_device_ptr(nmpc_solver *h, const char *field, void **out);
 /* solve all instances. nmpc_solve: upload host-staged inputs, launch, wait, download; returns
  * the max status over instances (0 when every instance succeeded) or < 0 on API error.
  * nmpc_solve_async: launch on the handle's stream using the device buffers as they are;
- * returns immediately (no host staging). With the fast solve (nmpc_get_launch_info out[8]) the instances
- * the first two launches leave parked get their full solve when the host next waits: inside nmpc_solve,
- * or at nmpc_synchronize after nmpc_solve_async — read the device buffers only after nmpc_synchronize.
- * Back-to-back nmpc_solve_async calls write the same device outputs; the last one's are final after
- * nmpc_synchronize (stream-ordered kernels of the caller that read the outputs before it may see a parked
- * instance's unconstrained point). */
+ * returns immediately (no host staging). The solve is complete in stream order: with the fast solve
+ * (nmpc_get_launch_info out[8]) its three launches (sf_kernel, fin64_kernel for the instances with a violated
+ * bound, the full IPM in list mode for what the finish parks) read their list lengths on the device, so a
+ * kernel or copy the caller enqueues behind nmpc_solve_async on the handle's stream (nmpc_set_stream) reads
+ * the final x / u / status / qp_iter of every instance. Back-to-back nmpc_solve_async calls write the same
+ * device outputs, each complete before the next starts. nmpc_synchronize waits for the stream. */
 int nmpc_solve(nmpc_solver *h);
 int nmpc_solve_async(nmpc_solver *h);
 int nmpc_synchronize(nmpc_solver *h);
@@ -187,7 +187,10 @@ int nmpc_get_cost(nmpc_solver *h, int instance, double *cost);
 
 /* statistics of the last solve: stats[0] = max qp_iter, stats[1] = mean qp_iter,
  * stats[2] = number of instances with status != 0, stats[3] = device time of the last
- * solve in ms (HIP events), stats[4] = sqp_iter (always 1: one QP solves an LQ-OCP) */
+ * solve in ms (HIP events), stats[4] = sqp_iter (always 1: one QP solves an LQ-OCP),
+ * stats[5] / stats[6] = the last fast solve's instances listed for the active-set finish / parked for the
+ * full IPM (0 without the fast solve); n <= 7 values are written. stats[0..2] describe the outputs last
+ * downloaded (nmpc_solve / nmpc_get_batch*), stats[3], [5], [6] the last solve waited for */
 int nmpc_get_stats(nmpc_solver *h, double *stats, int n);
 
 /* kernel geometry chosen for this handle: out[0] = instances per wavefront,
@@ -240,12 +243,16 @@ int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d);
  * Paths (the same results on every one; the choice may change from run to run on one handle):
  *   - the lean loop (nmpc_cl_fast.hip; quad13 / jerk / force shapes, fp64 and fp32 — fp32: fp32 tables
  *     and explicit form, fp64 W, set solves and acceptance — the default): launches of at
- *     most 64 steps; after each launch the host reads the count of parked instances (a step the fast
- *     path could not solve) and runs their full solve in list mode. fp32 handles: that full solve is the
- *     fp32 IPM without the exact finish (1e-3..1e-2 from the exact step solution, which the plant then
- *     carries); on the bench workloads no fp32 step parks (tests/test_gpu_bench_parity.py forces parks with
- *     NMPC_CLF_NO_GI=1 to measure it). That read waits for the launch, so
- *     the lean loop returns only when its last launch is done, whatever `sync` says;
+ *     most 64 steps; a step the fast path cannot solve parks, and the parked instances get their full solve
+ *     in list mode, after which the fast kernel continues them. sync != 0: after each launch the host reads the
+ *     park count and enqueues only the rounds needed. sync = 0: nothing waits — each chunk enqueues all its
+ *     possible rounds (chunk length + 1 fast launches and list-mode solves), each guarded by the count of the
+ *     round before on the device (an empty round returns at entry), so the run is asynchronous and complete
+ *     in stream order, at the cost of the empty rounds' launches. fp32 handles: the list-mode full solve is
+ *     the fp32 IPM without the exact finish (1e-3..1e-2 from the exact step solution, which the plant then
+ *     carries);
+ *     on the bench workloads no step parks (tests/test_gpu_bench_parity.py forces parks with
+ *     NMPC_CLF_NO_GI=1 to measure it);
  *   - fused (lane-per-component and wavefront kernel families, NMPC_CL_FAST=0): each solve launch
  *     carries up to 64 steps of every instance (prepare + solve + advance per instance, no step barrier
  *     between instances); asynchronous with sync = 0;

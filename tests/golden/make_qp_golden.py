@@ -10,7 +10,7 @@ These fixtures pin the HIP engine to the oracle; the oracle itself is pinned to 
 reference through the fixtures of make_golden.py and to acados's own recorded run through
 tests/golden/reference_plots.npz (extract_reference_plots.py).
 
-    python tests/golden/make_qp_golden.py [qp] [closed_loop]
+    python tests/golden/make_qp_golden.py [qp] [qp_rt] [closed_loop]
 """
 import os
 import sys
@@ -25,11 +25,19 @@ from oracle import models, qp  # noqa: E402
 
 CASES = [("force", 20), ("force", 30), ("jerk", 40), ("jerk", 30), ("quad13", 20)]
 PER_CASE = 48
+# horizons the fast solve has no compiled (fully unrolled) kernel for: its runtime-horizon sf_kernel variants
+# (N = 3: a single LDS slot, N below the chunk of 4 stages) — qp_cases_rt.npz
+CASES_RT = [("force", 10), ("force", 3), ("jerk", 20), ("quad13", 30)]
+PER_CASE_RT = 32
 
 
 def reference_table(name, N):
     refs = np.load(os.path.join(HERE, "circle_ref.npz"))
-    base = refs[f"nh{N}_nx6"] if f"nh{N}_nx6" in refs else None
+    if f"nh{N}_nx6" in refs:
+        base = refs[f"nh{N}_nx6"]
+    else:   # a horizon the reference fixture does not hold: the same table (generate_trajectory.py:7-28)
+        from oracle.trajectory import gen_circle_traj
+        base = gen_circle_traj(500, N, 6, 2)
     if name == "force":
         return base[:, :4], base[:, 4:6]
     if name == "jerk":
@@ -58,14 +66,14 @@ def perturbed_x0(name, xr, t, rng):
     return x0
 
 
-def qp_cases():
+def qp_cases(cases=CASES, per_case=PER_CASE, seed=20251121, fname="qp_cases.npz"):
     out = {}
-    rng = np.random.default_rng(20251121)
-    for name, N in CASES:
+    rng = np.random.default_rng(seed)
+    for name, N in cases:
         spec = models.MODELS[name](N)
         xr, ur = reference_table(name, N)
         X0, Y, XS, US, COST = [], [], [], [], []
-        while len(X0) < PER_CASE:
+        while len(X0) < per_case:
             t = int(rng.integers(0, 500))
             x0 = perturbed_x0(name, xr, t, rng)
             yref, yref_e = qp.yref_window(xr, ur, t, N)
@@ -84,8 +92,8 @@ def qp_cases():
         out[key + "_U"] = np.array(US)
         out[key + "_cost"] = np.array(COST)
         print(key, "done")
-    np.savez_compressed(os.path.join(HERE, "qp_cases.npz"), **out)
-    print("wrote qp_cases.npz")
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print("wrote", fname)
 
 
 def closed_loops():
@@ -115,9 +123,11 @@ def closed_loops():
 
 
 def main():
-    what = sys.argv[1:] or ["qp", "closed_loop"]
+    what = sys.argv[1:] or ["qp", "qp_rt", "closed_loop"]
     if "qp" in what:
         qp_cases()
+    if "qp_rt" in what:
+        qp_cases(CASES_RT, PER_CASE_RT, 20261018, "qp_cases_rt.npz")
     if "closed_loop" in what:
         closed_loops()
 

@@ -49,3 +49,16 @@ def test_cpu_baseline(line):
     c = line["cpu_baseline"]
     assert c["kind"] in ("port", "reference")
     assert c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A launcher's WORLD_SIZE that differs from --gpus is refused before any GPU work (exit 2, nothing
+    on stdout), so a driver run can never report the wrong number of GPUs."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4"], env=env,
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 2 and out.stdout == ""
+    assert "differs from --gpus 4" in out.stderr

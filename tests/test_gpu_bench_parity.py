@@ -324,14 +324,16 @@ def test_force_fused_loop_families_agree():
 
 
 @pytest.mark.timeout(300)
-def test_lean_loop_list_mode_fallback_with_forced_parks():
+@pytest.mark.parametrize("sync", [True, False])
+def test_lean_loop_list_mode_fallback_with_forced_parks(sync):
     """The lean loop's list-mode fallback (nmpc_api.cpp clf_run -> ipm_lpc_kernel in list mode, the path
     whose idle lanes once read an unset noise column, nmpc_ipm_lpc.hip list mode) forced by the test knob
     NMPC_CLF_NO_GI=1: without the dual active-set fallback every force step whose PDAS run does not
     settle parks and gets the full solve. Force (saturating inputs, src/force_model/ocp.py:64-68), a
     ragged batch of 2049 over 40 steps in three runs (3 + 20 + 17, reference loop
     src/force_model/controller.py:25-54): parks happen, and states / sums match the exact oracle loop
-    (mode 0) at 1e-6 with the failure counts exact."""
+    (mode 0) at 1e-6 with the failure counts exact. sync=False: nmpc_closed_loop_run(.., sync = 0) enqueues
+    every round with its park count read on the device (no host wait inside the run); the same results."""
     from drone_attitude_control_amd.batched import ClosedLoop, workload
     from oracle import cref, models
     os.environ["NMPC_CLF_NO_GI"] = "1"
@@ -340,8 +342,11 @@ def test_lean_loop_list_mode_fallback_with_forced_parks():
         assert cl.solver.launch_info()["closed_loop_kernel"] == "cl_fast_kernel"
         parked = 0
         for n in (3, 20, 17):
-            cl.run(n)
-            parked += cl.stats()["parked"]
+            cl.run(n, sync=sync)
+            st = cl.stats()
+            parked += st["parked"]
+            if not sync:   # every possible round was enqueued: n + 1 fast launches
+                assert st["fast_launches"] == n + 1, st
         x, acc = cl.state(), cl.instance_stats()
     finally:
         os.environ.pop("NMPC_CLF_NO_GI", None)

@@ -30,7 +30,9 @@ def _bench(args, world, backend="gloo", launcher=None, **env_extra):
     """bench.py as one process (world 1, no launcher) or under torch.distributed.run with `world`
     ranks and the given process-group backend."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
-    if world > 1 or launcher == "torchrun":
+    if launcher == "self":   # bench.py --gpus N starts its N ranks itself
+        cmd += ["--dist-backend", backend]
+    elif world > 1 or launcher == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
                *args, "--dist-backend", backend]
@@ -62,6 +64,38 @@ def test_force_two_ranks_reduce_equals_one_process():
         assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=rel)
         assert a["aed"] == pytest.approx(b["aed"], rel=rel)
         assert two["value"] > 0 and len(two["timing"]["region_ms"]) == 2
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_two_starts_two_ranks_itself():
+    """`python bench.py --gpus 2` with no launcher (the driver's form) starts its two ranks itself
+    (a torch.distributed.run child, before any GPU call in the parent) and relays rank 0's line:
+    n_gpus 2, global batch 8192, statistics equal to one process over the same 8192 instances.
+    gloo, both ranks on the box's one GPU (RCCL needs a GPU per rank)."""
+    common = ["--model", "force", "--steps", "4", "--warmup", "2", "--repeats", "2", "--no-cpu-baseline"]
+    two = _bench(common + ["--gpus", "2", "--batch", "4096"], 2, launcher="self")
+    one = _bench(common + ["--gpus", "1", "--batch", "8192"], 1)
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == one["config"]["global_batch"] == 8192
+    assert "started by bench.py --gpus 2" in two["config"]["parallelism"]
+    a, b = two["closed_loop"], one["closed_loop"]
+    assert a["instance_steps"] == b["instance_steps"] == 8192 * (2 + 2 * 4)
+    assert a["failed_solves"] == b["failed_solves"]
+    assert a["mean_cost_per_step"] == pytest.approx(b["mean_cost_per_step"], rel=1e-10)
+    assert a["aed"] == pytest.approx(b["aed"], rel=1e-10)
+
+
+@pytest.mark.timeout(120)
+def test_bench_nccl_refuses_more_ranks_than_gpus():
+    """backend nccl with more ranks than visible GPUs exits non-zero with the reason, instead of putting
+    two RCCL ranks on one device."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--model", "force", "--batch", "64",
+           "--steps", "1", "--warmup", "1", "--repeats", "1", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"),
+                         capture_output=True, text=True, timeout=100)
+    assert out.returncode != 0 and out.stdout.strip() == ""
+    assert "needs one GPU per rank" in out.stderr
 
 
 @pytest.mark.timeout(600)

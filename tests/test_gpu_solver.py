@@ -111,6 +111,89 @@ def test_fast_solve_parks_take_the_full_solve(key, cases):
     assert e.max() < TOL64, e.max()
 
 
+RT_KEYS = ["force_N10", "force_N3", "jerk_N20", "quad13_N30"]
+
+
+@pytest.mark.parametrize("key", RT_KEYS)
+@pytest.mark.parametrize("no_gi", [False, True])
+def test_fast_solve_runtime_horizons(key, no_gi, golden_dir):
+    """The fast solve at horizons without a compiled (fully unrolled) sf_kernel: the runtime-horizon variants
+    (four-stage two-slot LDS ring, the register ring indexed at run time; N = 3 is a single slot, shorter than a
+    chunk). Against the certified oracle on tests/golden/qp_cases_rt.npz (make_qp_golden.py qp_rt), with the
+    C restatement's Newton-system counts; no_gi: the dual fallback off, so unsettled instances park and take
+    the list-mode full IPM."""
+    cases = np.load(os.path.join(golden_dir, "qp_cases_rt.npz"))
+    name, N = split(key)
+    env = {"NMPC_CLF_NO_GI": "1"} if no_gi else None
+    s, st = solve_batch(key, cases, env=env)
+    assert s.launch_info()["solve_kernel"] == "sf_kernel"
+    assert st == 0
+    e = rel_err(s.get_batch("x"), s.get_batch("u"), cases[key + "_X"], cases[key + "_U"])
+    assert e.max() < TOL64, e.max()
+    if not no_gi:
+        R = cref.RiccatiIpmRef.for_options(models.MODELS[name](N), OCPS[name](N).solver_options)
+        _, _, stc, itc, cnt = R.solve_fast(cases[key + "_x0"], cases[key + "_yref"], wsmax=cref.WSMAX[name])
+        assert cnt["full"] == 0
+        assert np.array_equal(s.get_batch_int("qp_iter"), itc)
+
+
+def _hip():
+    """The HIP runtime libnmpc_hip.so already loaded (same soname: the same runtime and device context)."""
+    import ctypes
+    from drone_attitude_control_amd import _lib
+    _lib.load()
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+@pytest.mark.parametrize("key", ["force_N20", "jerk_N40", "quad13_N20"])
+def test_solve_async_is_complete_in_stream_order(key, cases):
+    """nmpc_solve_async on a caller's stream (nmpc_set_stream), then hipMemcpyAsync of the device x / u on that
+    stream and a plain hipStreamSynchronize — no nmpc_synchronize, no host step of the engine in between. With
+    the dual fallback off (NMPC_CLF_NO_GI=1) instances park, so the copy is correct only if the parked
+    instances' full IPM ran in stream order before it (src/force_model/controller.py:32-39: solve() returns a
+    finished solution). Twice back to back: the second solve's copies are final too."""
+    import ctypes
+    name, N = split(key)
+    x0, y = cases[key + "_x0"], cases[key + "_yref"]
+    B = x0.shape[0]
+    os.environ["NMPC_CLF_NO_GI"] = "1"
+    hip = _hip()
+    stream = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(stream)) == 0
+    try:
+        s = AcadosOcpSolver(OCPS[name](N), batch=B)
+        assert s.launch_info()["solve_kernel"] == "sf_kernel"
+        s.set_stream(stream.value)
+        s.set_batch("x0", x0)
+        s.set_batch("yref", y)
+        s.solve()                       # stages the inputs in HBM (and one complete solve)
+        for rep in range(2):
+            X = np.zeros((B, N + 1, s.nx))
+            U = np.zeros((B, N, s.nu))
+            st = np.zeros(B, dtype=np.int32)
+            s.solve_async()
+            for host, field in ((X, "x"), (U, "u"), (st, "status")):
+                assert hip.hipMemcpyAsync(host.ctypes.data, s.device_ptr(field), host.nbytes, 2, stream) == 0
+            assert hip.hipStreamSynchronize(stream) == 0
+            assert (st == 0).all(), st
+            e = rel_err(X, U, cases[key + "_X"], cases[key + "_U"])
+            assert e.max() < TOL64, (rep, e.max())
+        s.synchronize()
+        parked, listed = s.get_stats("fast_parked"), s.get_stats("fast_listed")
+        print(f"{key}: listed {listed}, parked {parked} of {B}")
+        if name == "force":
+            assert parked > 0, "the test needs parked instances"
+        s.set_stream(0)
+    finally:
+        os.environ.pop("NMPC_CLF_NO_GI", None)
+        hip.hipStreamDestroy(stream)
+
+
 @pytest.mark.parametrize("key", ["force_N20", "jerk_N40"])
 @pytest.mark.parametrize("ipw", [1, 2, 4])
 def test_instance_packing_variants(key, ipw, cases):

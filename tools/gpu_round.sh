@@ -24,4 +24,14 @@ import json
 for l in open('$OUT/configs_$TAG.jsonl'):
     b = json.loads(l); print(b['config']['model'], b['dtype'], b['config']['batch_per_gpu'], '%.3fM' % (b['value'] / 1e6), 'kernel %.4f ms' % b['roofline']['kernel_ms'], 'failed', b['closed_loop']['failed_solves'])"
 fi
+if [ "${SOLVES:-0}" = "1" ]; then
+  : > $OUT/solves_$TAG.jsonl
+  for a in "--model quad13" "--model force" "--model jerk --horizon 40 --batch 4096"; do
+    timeout -k 10 300 python bench.py --mode solve $a ${CFG_ARGS:-} >> $OUT/solves_$TAG.jsonl 2>> $OUT/solves_$TAG.err || { echo "solve line failed: $a"; exit 1; }
+  done
+  python -c "
+import json
+for l in open('$OUT/solves_$TAG.jsonl'):
+    b = json.loads(l); print('solve', b['config']['model'], b['config']['batch_per_gpu'], '%.1fM QP/s' % (b['value'] / 1e6), 'kernel %.4f ms' % b['roofline']['kernel_ms'], b.get('fast_counts'))"
+fi
 echo "round pass done"
