@@ -615,6 +615,7 @@ constexpr int CLF_CHUNK = 64;        // closed-loop steps per lean-loop launch (
 // the lean loop's asynchronous runs (sync = 0): per round of a chunk its own [park count, claim counter] pair,
 // after the park list in d_park
 constexpr int CLF_ROUND_WORDS = 2 * (CLF_CHUNK + 1);
+constexpr int CLF_NT_HOST = 24;      // timing builds: phase counters per instance (nmpc_cl_fast.hip CLF_NT)
 
 int fin32_setup(nmpc_solver *h);
 hipError_t fin32_enqueue(nmpc_solver *h);
@@ -2053,13 +2054,22 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         for (int i = 0; i < d.ncl; i++)
             if (x1slot < 0 || eslot[nz + i] != x1slot + i || x1slot + i >= 64) return 0;
     }
-    std::vector<int> src(nslot, -1);
+    // warm-start source code per slot (nmpc_cl_fast.hip run_instance): (source slot + 1) | (end partner + 1) << 12 |
+    // kind << 24. Source: the slot of the same component one stage later (the shift). Kind 1 / 2: a state slot of
+    // stage N - 1 / N - 2 and its partner the same component's slot of stage N - 2 / N - 1 — a bound active at
+    // N - 1 but not at N - 2 stays at N - 1 (oracle/c/riccati_ipm.c, closed loop mode 1)
+    std::vector<int> src(nslot, 0);
     for (int s = 0; s < nslot; s++) {
         const int k = el[s] / nz, r = el[s] % nz;
         int ks = k < N ? k + 1 : k;
         if (k == N - 1 && r >= nx) ks = k;   // inputs of stage N mirror N - 1
-        src[s] = eslot[ks * nz + r];
+        src[s] = eslot[ks * nz + r] + 1;
+        if (r < nx && N >= 3 && (k == N - 1 || k == N - 2)) {
+            const int ps = eslot[(k == N - 1 ? N - 2 : N - 1) * nz + r];
+            if (ps >= 0) src[s] |= (ps + 1) << 12 | (k == N - 1 ? 1 : 2) << 24;
+        }
     }
+    if (NS > 4095) return 0;   // (the code's slot fields)
     std::vector<double> stx((size_t)nslot * nx), vb((size_t)P_ * NS, 0.0);
     for (int s = 0; s < nslot; s++)
         for (int c = 0; c < nx; c++) stx[(size_t)s * nx + c] = tx[(size_t)el[s] * nx + c];
@@ -2312,11 +2322,11 @@ int clf_run(nmpc_solver *h, int steps, bool async)
     }
     int *d_rc = h->d_park + 2 + h->batch;   // asynchronous runs: the rounds' [park count, claim counter] pairs
     // env NMPC_CLF_CYCLES=<file> with a timing build (-DNMPC_CLF_TIMING): per-instance phase cycles of the
-    // run, [B][20] uint64, appended to <file> (tools/clf_phases.py)
+    // run, [B][CLF_NT_HOST] uint64, appended to <file> (tools/clf_phases.py)
     static const char *cyc_path = std::getenv("NMPC_CLF_CYCLES");
     unsigned long long *d_cyc = nullptr;
-    if (cyc_path && hipMalloc((void **)&d_cyc, (size_t)h->batch * 20 * sizeof(unsigned long long)) == hipSuccess)
-        (void)hipMemsetAsync(d_cyc, 0, (size_t)h->batch * 20 * sizeof(unsigned long long), h->stream);
+    if (cyc_path && hipMalloc((void **)&d_cyc, (size_t)h->batch * CLF_NT_HOST * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemsetAsync(d_cyc, 0, (size_t)h->batch * CLF_NT_HOST * sizeof(unsigned long long), h->stream);
     for (int done = 0; done < steps;) {
         const int n = std::min(CLF_CHUNK, steps - done), target = h->cl_step + n;
         nmpc::ClParams<T> cp = cl_params<T>(h);
@@ -2392,7 +2402,7 @@ int clf_run(nmpc_solver *h, int steps, bool async)
         done += n;
     }
     if (d_cyc) {
-        std::vector<unsigned long long> cy((size_t)h->batch * 20);
+        std::vector<unsigned long long> cy((size_t)h->batch * CLF_NT_HOST);
         if (hipStreamSynchronize(h->stream) == hipSuccess &&
             hipMemcpy(cy.data(), d_cyc, cy.size() * sizeof(cy[0]), hipMemcpyDeviceToHost) == hipSuccess) {
             if (FILE *f = std::fopen(cyc_path, "ab")) {

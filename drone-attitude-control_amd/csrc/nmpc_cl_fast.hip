@@ -53,8 +53,9 @@ constexpr int PDAS_ROUNDS = 6;   // rounds of the first PDAS run before the fall
 // fallback (gi_set), 6 certificate, 7 outputs, 8 plant + cost, 9 instance record load / write-back;
 // counts: 10 PDAS rounds, 11 GI iterations, 12 slow steps, 13 steps; GI parts: 14 entering-bound choice,
 // 15 a = W[S, p] loads + r = H a + theta + ratio test, 16 dz combination, 17 H update; PDAS parts: 18 set
-// load, 19 bound tests / additions after the combination
-constexpr int CLF_NT = 20;
+// load, 19 bound tests / additions after the combination, of which 20 the state additions (add_states);
+// 21 the multiplier signs after the set solve, 22 the round's set count at its top, 23 the z checks alone
+constexpr int CLF_NT = 24;   // (nmpc_api.cpp CLF_NT_HOST)
 #ifdef NMPC_CLF_TIMING
 #define CLF_T(v) const long long v = clock64()
 #define CLF_TADD(L, i, v)                              \
@@ -196,7 +197,7 @@ struct Lds {
 template <int EPL>
 struct SlotView {
     const double *lb_, *ub_, *lo_, *hi_, *onl_, *onu_;
-    const int *e_, *src_;
+    const int *e_, *src_;   // src_: the warm-start source codes (nmpc_api.cpp clf_setup; 0: none)
     int lane;
     // wl_: W over the slots in the workgroup's LDS (lower triangle, row s: wt_[s (s + 1) / 2 + s'], s' <= s);
     // else W from the global table by element. W is symmetric. (A flag, not a null test: the compiler cannot
@@ -684,9 +685,11 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         CLF_SYNC();
     };
     for (int ws = 0, first = 1; ws < rounds; first = 0) {
+        CLF_T(tm0);
         int m = 0;
 #pragma unroll
         for (int j = 0; j < EPL; j++) m += __popcll(__ballot(((wf >> (2 * j)) & 3u) != 0));
+        CLF_TADD(L, 22, tm0);
         if (m == 0) {
             // no bound held: the iterate is z_0 — accepted if feasible, else the set from its violations
             if (!first) ws++;
@@ -734,6 +737,7 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         CLF_TADD(L, 3, ts0);
         CLF_TCNT(L, 10, 1);
         if (!pd) break;
+        CLF_T(tmu0);
         // multiplier signs as displacements nu_i W_ii (lower: >= 0, upper: <= 0) to 1e-10 (1 + |b - z_0|)
         bool rmv = false;
         if (lane < m) {
@@ -744,6 +748,7 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         }
         const unsigned long long remm = __ballot(rmv);
         CLF_SYNC();
+        CLF_TADD(L, 21, tmu0);
         const int round = ws++;
         wsteps++;
         const int nrem = __popcll(remm);
@@ -783,11 +788,14 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
             }
             z[j] = (T)zz;
         }
+        CLF_TADD(L, 23, tk0);
         if (!__any(bad)) {
             CLF_TADD(L, 19, tk0);
             return done(m);
         }
+        CLF_T(tad0);
         if (addok) add_states(v, sgn, nwf);
+        CLF_TADD(L, 20, tad0);
         wf = nwf;
         CLF_SYNC();
         CLF_TADD(L, 19, tk0);
@@ -1297,8 +1305,17 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
             CLF_SYNC();
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
-                const int sr_ = sv.src(j);
-                wf |= bits_of(sr_ >= 0 ? L.fl[sr_] : (signed char)0) << (2 * j);
+                // the slot's source code (nmpc_api.cpp clf_setup): the flag of the same component one stage later;
+                // kinds 1 / 2 (state slots of stages N - 1 / N - 2): a bound held at N - 1 but not at N - 2 stays at
+                // N - 1 (the horizon's end holds it; oracle closed loop mode 1)
+                const int code = sv.src(j), sr_ = (code & 0xfff) - 1, ps = ((code >> 12) & 0xfff) - 1, kind = code >> 24;
+                signed char f = sr_ >= 0 ? L.fl[sr_] : (signed char)0;
+                if (kind != 0) {
+                    const signed char own = L.fl[j * 64 + lane], par = L.fl[ps];
+                    if (kind == 1 && own != 0 && par == 0) f = own;
+                    if (kind == 2 && par != 0 && own == 0) f = 0;
+                }
+                wf |= bits_of(f) << (2 * j);
             }
         }
         CLF_SYNC();
@@ -1484,7 +1501,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         sol[s] = hl ? l + ClfTol<T>::onb * (1.0 + fabs(l)) : -DBL_MAX;
         sou[s] = hu ? u - ClfTol<T>::onb * (1.0 + fabs(u)) : DBL_MAX;
         sse[s] = v ? p.s_e[s] : -1;
-        ssrc[s] = v ? p.s_src[s] : -1;
+        ssrc[s] = v ? p.s_src[s] : 0;
     }
     // WL: W over the slots in LDS (lower triangle; the rare path's gathers and W[:, S] nu combinations
     // then wait on LDS instead of L2 — the force shape, whose steps are mostly active-set steps)
@@ -1632,7 +1649,7 @@ __global__ __launch_bounds__(64 * WPB) void fin32_kernel(ClFastParams<float> p)
         sol[s] = hl ? l + 1e-3 * (1.0 + fabs(l)) : -DBL_MAX;   // the IPM solution's active bounds
         sou[s] = hu ? u - 1e-3 * (1.0 + fabs(u)) : DBL_MAX;
         sse[s] = v ? p.s_e[s] : -1;
-        ssrc[s] = -1;
+        ssrc[s] = 0;
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
@@ -1712,7 +1729,7 @@ __global__ __launch_bounds__(64 * WPB) void fin64_kernel(ClFastParams<double> p)
         sol[s] = hl ? l + ClfTol<T>::onb * (1.0 + fabs(l)) : -DBL_MAX;
         sou[s] = hu ? u - ClfTol<T>::onb * (1.0 + fabs(u)) : DBL_MAX;
         sse[s] = v ? p.s_e[s] : -1;
-        ssrc[s] = -1;
+        ssrc[s] = 0;
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ, WSM> &L = lds_all[wave];
@@ -1816,7 +1833,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         lohi[s] = make_double2(slo[s], shi[s]);
         onb[s] = make_double2(sol[s], sou[s]);
         sse[s] = v ? p.s_e[s] : -1;
-        ssrc[s] = v ? p.s_src[s] : -1;
+        ssrc[s] = v ? p.s_src[s] : 0;
     }
     for (int e = threadIdx.x; e < LOCK_QCAP; e += 64 * WPB) dq[e] = -1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

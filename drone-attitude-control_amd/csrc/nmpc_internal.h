@@ -133,7 +133,7 @@ struct ClFastParams {
     int *istep;                   // [B] closed-loop step each instance has reached
     signed char *flags;           // [B][nslot] the last solution's active flags (-1 lower, 1 upper)
     const double *noise;          // [B][noise_ld]
-    const int *s_e, *s_src;       // [nslot] element index k nz + r; warm-start source slot (or -1)
+    const int *s_e, *s_src;       // [nslot] element index k nz + r; warm-start source code (nmpc_api.cpp clf_setup)
     const int *s_free;            // [nfree] the decision elements without a bound (outputs only)
     int nfree;
     const T *s_lb, *s_ub;         // [nslot]

@@ -1566,6 +1566,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
         double *z0 = (double *)malloc(sizeof(double) * ne), *zf = (double *)malloc(sizeof(double) * ne);
         signed char *wf = (signed char *)malloc(ne), *w0 = (signed char *)malloc(ne);
         const char *dbg_env = getenv("RIC_DEBUG_INST");
+        const int path_cost = getenv("RIC_PATH_COST") != NULL;   /* tuning aid: path + 16 x the step's active-set steps */
         const int dbg_inst = dbg_env ? atoi(dbg_env) : -1;
 #pragma omp for schedule(dynamic, 4)
         for (int b = 0; b < batch; b++) {
@@ -1578,7 +1579,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                 const int step = step0 + s, t = (int)(((long long)offsets[b] + step) % c->period);
                 for (int k = 0; k < N; k++) memcpy(yref + (size_t)k * ny, c->table + (size_t)(t + k) * c->cols, sizeof(double) * ny);
                 memcpy(yref + (size_t)N * ny, c->table + (size_t)(t + N) * c->cols, sizeof(double) * nye);
-                int status = 0, path = 2, iters = 0, ok = 0;
+                int status = 0, path = 2, iters = 0, ok = 0, step_sets = 0;
                 if (ric_dbg) fprintf(stderr, "step %d t=%d\n", step, t);
                 /* mode 1 tries the fast path from the first step on (an empty warm set at step 0) */
                 const int warm = mode == 1 && ab != NULL;
@@ -1586,6 +1587,16 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                     for (int k = 0; k <= N; k++)
                         for (int i = 0; i < nz; i++)
                             wf[k * nz + i] = valid_el(nx, N, k, i) ? ab[(k < N ? k + 1 : k) * nz + i] : 0;
+                    /* a state bound active at the last bounded stage N - 1 but not at N - 2 (held by the horizon's
+                     * end, not an arc travelling toward stage 0) stays at N - 1 instead of moving to N - 2
+                     * (nmpc_cl_fast.hip run_instance, the warm-start source code kinds 1 / 2): the quad13
+                     * bench's rare-path set steps 1,260 -> 693 per 20-step region, the longest chain 56 -> 44 */
+                    if (N >= 3)
+                        for (int i = 0; i < nx; i++)
+                            if (ab[(N - 1) * nz + i] && !ab[(N - 2) * nz + i]) {
+                                wf[(N - 1) * nz + i] = ab[(N - 1) * nz + i];
+                                wf[(N - 2) * nz + i] = 0;
+                            }
                     if (d->polish_mu > 0.0) {
                         int wst = 0, nw = 0;
                         for (int e = 0; e < ne; e++) nw += wf[e] != 0;
@@ -1599,6 +1610,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                         if (!(cert_first && infeasible_stage(d, st) > 0))
                             ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, r0) > 0;
                         cnt[3] += wst;
+                        step_sets += wst;
                         /* not settled: unless the interval certificate proves the QP infeasible (solve_one
                          * returns that), the dual active-set fallback, its set then solved and checked by
                          * fast_finish */
@@ -1608,8 +1620,10 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                             if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
                                 ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
                                 cnt[3] += wst;
+                                step_sets += wst;
                             }
                             cnt[3] += git;
+                            step_sets += git;
                         }
                         if (ok) {
                             path = (nw == 0 && wst == 0) ? 0 : 1;
@@ -1657,7 +1671,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                 if (u_log) memcpy(u_log + ((size_t)b * steps + s) * nu, uo, sizeof(double) * nu);
                 if (x_log) memcpy(x_log + ((size_t)b * steps + s) * nx, st, sizeof(double) * nx);
                 if (status_log) status_log[(size_t)b * steps + s] = status;
-                if (path_log) path_log[(size_t)b * steps + s] = path;
+                if (path_log) path_log[(size_t)b * steps + s] = path + (path_cost ? 16 * step_sets : 0);
             }
         }
         free(buf); free(yref); free(xo); free(uo); free(z0); free(zf); free(wf); free(w0);

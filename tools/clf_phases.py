@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PHASES = ["prologue", "explicit+test", "pdas", "pdas.solve", "pdas.combo", "gi", "certificate", "outputs",
           "plant+cost", "record", "pdas_rounds", "gi_iters", "slow_steps", "steps", "gi.select", "gi.solve",
-          "gi.combo", "gi.hupdate", "pdas.load_set", "pdas.check"]
+          "gi.combo", "gi.hupdate", "pdas.load_set", "pdas.check", "pdas.check.add_states", "pdas.signs",
+          "pdas.count", "pdas.check.z"]
 
 
 def main():
