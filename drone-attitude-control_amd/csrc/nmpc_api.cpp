@@ -260,6 +260,7 @@ struct nmpc_solver {
     int *d_istep = nullptr, *d_park = nullptr;   // [B]; park count, work counter, park list [2 + B]
     signed char *d_flags = nullptr;        // [B][nslot]
     int clf_resident = 0;                  // workgroups of cl_fast_kernel the handle's device holds at once
+    int *d_imap = nullptr;                 // the lean loop's position -> instance map (clf_xcd_map), or null
     int clf_kind = 0;                      // nmpc::CLF_FAST / CLF_LOCK (cl_lock_kernel) / CLF_WLDS (W in LDS) / CLF_ONE
     int clf_parked = 0, clf_rounds = 0;    // the last run: parked solves (list-mode full solves), fast launches
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
@@ -535,7 +536,7 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
                     (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw,
                     (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0, (void *)h->d_sf, (void *)h->d_f64,
-                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch, (void *)h->d_sfcyc, (void *)h->d_clf_check})
+                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch, (void *)h->d_sfcyc, (void *)h->d_clf_check, (void *)h->d_imap})
         if (p) hipFree(p);
     if (h->h_sfpark) hipHostFree(h->h_sfpark);
     if (h->ev_fb) hipEventDestroy(h->ev_fb);
@@ -2014,6 +2015,8 @@ int sf_resolve(nmpc_solver *h)
 // Slots: the bounded elements of z in stage-major order (stage 0's inputs first), their bounds,
 // T_x rows, v_t columns and warm-start sources (the element one stage later; stage N - 1's inputs
 // keep their own flag, as the fused kernel's mirror of stage N).
+int clf_xcd_map(nmpc_solver *h, const nmpc_closed_loop_desc &d, int sid, bool f64);
+
 int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<double> &tx, const std::vector<double> &vv)
 {
     const int nx = h->nx, nu = h->nu, nz = nx + nu, N = h->N, ne = (N + 1) * nz, P_ = d.ref_period;
@@ -2148,6 +2151,10 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
         h->clf_resident = nmpc::cl_fast_resident(nx, nu, fsid, h->clf_kind, f64, h->device);
     }
     if (h->clf_resident <= 0) return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_init: lean closed-loop occupancy query");
+    {
+        const int r = clf_xcd_map(h, d, fsid, f64);
+        if (r < 0) return r;
+    }
     h->clf = true;
     h->clf_nslot = nslot;
     h->clf_nfree = (int)fr.size();
@@ -2156,6 +2163,40 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     h->clf_sid = fsid;
     h->clf_kidx = fk;
     return 0;
+}
+
+// XCD-aware instance placement for the lean loop's per-workgroup claim ranges. The hardware hands workgroup w to XCD
+// w % 8, and each XCD has its own L2; an instance reads the v_t row of its reference-table row every step (offset +
+// step, shared table). With instances in index order every XCD's L2 pulls the whole v_t table (period x slots: 1 MB
+// quad13, 1.28 MB jerk) each launch. The map sorts the instances by start row and gives each XCD's workgroups one
+// contiguous stretch of rows, so an XCD reads about an eighth of the table (+ the launch's steps). Results do not
+// depend on it (instances are independent; every per-instance record stays indexed by the instance); env
+// NMPC_CLF_XCD=0: index order. Not with the device-wide claim (the force shape): its positions go to any workgroup.
+int clf_xcd_map(nmpc_solver *h, const nmpc_closed_loop_desc &d, int sid, bool f64)
+{
+    if (h->d_imap) {
+        hipFree(h->d_imap);
+        h->d_imap = nullptr;
+    }
+    const char *env = std::getenv("NMPC_CLF_XCD");
+    if (env && env[0] == '0') return 0;
+    const int B = h->batch, X = 8;
+    const int G = nmpc::cl_fast_grid(h->nx, h->nu, sid, h->clf_kind, f64, B, h->clf_resident);
+    if (G < 2 * X) return 0;
+    const int per = (B + G - 1) / G;
+    std::vector<int> order(B), map(B);
+    for (int b = 0; b < B; b++) order[b] = b;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return d.offsets[a] % d.ref_period < d.offsets[b] % d.ref_period;
+    });
+    size_t next = 0;
+    for (int x = 0; x < X; x++)
+        for (int w = x; w < G; w += X)
+            for (int q = w * per; q < std::min(B, (w + 1) * per); q++) map[q] = order[next++];
+    if (hipMalloc((void **)&h->d_imap, (size_t)B * sizeof(int)) != hipSuccess)
+        return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: instance map");
+    const hipError_t e = hipMemcpy(h->d_imap, map.data(), (size_t)B * sizeof(int), hipMemcpyHostToDevice);
+    return e == hipSuccess ? 0 : hip_fail(h, e, "nmpc_closed_loop_init: instance map upload");
 }
 
 template <typename T>
@@ -2241,6 +2282,10 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     const char *lo = std::getenv("NMPC_CLF_ORDER");
     p.demoted = (lo && lo[0] == '0') ? nullptr : (unsigned char *)h->d_flags + (size_t)h->batch * h->clf_nslot;
     p.order_buckets = (lo && lo[0] == '2') ? 1 : 0;
+    p.inst_map = p.claim_global ? nullptr : h->d_imap;
+    // the rare path's W column cache in the workgroup's LDS (the shapes with sets of up to 16)
+    const char *wce = std::getenv("NMPC_CLF_WCACHE");
+    p.wcache = (wce && wce[0] == '0') ? 0 : 1;
     return p;
 }
 

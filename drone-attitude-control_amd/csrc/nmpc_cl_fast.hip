@@ -204,6 +204,18 @@ struct SlotView {
     // null-test a generic pointer into LDS.)
     const double *wt_ = nullptr;
     bool wl_ = false;
+    // wc_: this wavefront holds the workgroup's W column cache (WCache; quad13 / jerk shapes): W[ea][eb] is column
+    // colof[sa] of the cache at slot sb — the caller made that column resident (wc_fill) before the access
+    const double *wcol_ = nullptr;
+    const short *wcolof_ = nullptr;
+    int wcld_ = 0;
+    bool wc_ = false;
+    // W[e(sa)][e(sb)] from the cache (column of slot sa resident)
+    __device__ double wcv(int sa, int sb) const
+    {
+        const int c = wcolof_[sa];
+        return wcol_[(c < 0 ? 0 : c) * wcld_ + sb];
+    }
     template <typename T>
     __device__ double w(const ClFastParams<T> &p, int ea, int sa, int eb, int sb) const
     {
@@ -223,6 +235,111 @@ struct SlotView {
     __device__ int src(int j) const { return src_[j * 64 + lane]; }
 };
 
+#define CLF_SYNC()                                               \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+    } while (0)
+
+// The workgroup's cache of W columns over the slots (quad13 / jerk shapes; LDS): column c holds W[e][s] for the
+// element e of slot ce[c] and every slot s of the layout; colof[s] = the column of slot s's element, or -1. W is one
+// matrix for every instance and step, so a resident column stays valid across steps, instances and wavefronts; one
+// wavefront at a time owns the cache (owner, taken per rare step in slow_step), the others read W from L2. An
+// active-set round then reads W_SS and W[:, S] from LDS; only the set's new columns are loaded (the set of the
+// next round, step, or the next instance riding the same bound mostly repeats). WC = the largest set + 1 (the dual
+// fallback's entering bound beside a full set)
+template <int WC, int NSLOT>
+struct WCache {
+    double col[WC][NSLOT];
+    short colof[NSLOT];
+    short ce[WC];
+    int owner;   // the owning wavefront, or -1
+    int next;    // the round-robin eviction start
+};
+
+// the empty cache (every thread of the workgroup, before the workgroup's first barrier)
+template <int WC, int NSLOT>
+__device__ void wc_init(WCache<WC, NSLOT> &C)
+{
+    for (int s = threadIdx.x; s < NSLOT; s += blockDim.x) C.colof[s] = -1;
+    for (int c = threadIdx.x; c < WC; c += blockDim.x) C.ce[c] = -1;
+    if (threadIdx.x == 0) {
+        C.owner = -1;
+        C.next = 0;
+    }
+}
+
+// make the columns of the slots of lanes 0..n-1 (slot_i on lane i; wave-uniform n, n + popcount(keep) <= WC)
+// resident, evicting only columns outside that list and outside `keep` (a column bit mask). Each lane loads its
+// slots' entries of a missing column, WCB columns in flight at a time
+#ifndef NMPC_WCB
+#define NMPC_WCB 2
+#endif
+#ifndef NMPC_WCACHE
+#define NMPC_WCACHE 0   // experiment builds: -DNMPC_WCACHE=1 compiles the cache into the lean kernels
+#endif
+constexpr int WCB = NMPC_WCB;
+template <typename T, int EPL, int WC, int NSLOT>
+__device__ __noinline__ void wc_fill(const ClFastParams<T> &p, WCache<WC, NSLOT> &C, const SlotView<EPL> &sv, int slot_i, int n,
+                        unsigned keep, int lane)
+{
+    if constexpr (WC > 32) return;   // (no cache for sets beyond 16: the force shape's kernels never pass one)
+    const int si = lane < n ? slot_i : 0;
+    const int ci = lane < n ? (int)C.colof[si] : -1;
+    const unsigned long long miss = __ballot(lane < n && ci < 0);
+    if (!miss) return;
+    unsigned used = keep | (ci >= 0 ? 1u << ci : 0u);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) used |= (unsigned)__shfl_xor((int)used, o);
+    int nxt = C.next;
+    int e[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; j++) e[j] = sv.e(j);
+    for (unsigned long long mm = miss; mm;) {
+        int cs[WCB], ss[WCB], nb = 0;
+        double w[WCB][EPL];
+#pragma unroll
+        for (int q = 0; q < WCB; q++) {
+            cs[q] = -1;
+            ss[q] = 0;
+            if (mm) {
+                const int i = (int)__builtin_ctzll(mm);
+                mm &= mm - 1;
+                int c = nxt;
+                for (int t = 0; t < WC && ((used >> c) & 1u); t++) c = c + 1 == WC ? 0 : c + 1;
+                used |= 1u << c;
+                nxt = c + 1 == WC ? 0 : c + 1;
+                cs[q] = c;
+                ss[q] = __builtin_amdgcn_readfirstlane(__shfl(si, i));
+                nb = q + 1;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < WCB; q++) {
+            const int ea = q < nb ? sv.e_[ss[q]] : 0;
+#pragma unroll
+            for (int j = 0; j < EPL; j++)
+                w[q][j] = (q < nb && e[j] >= 0) ? p.W[(size_t)ea * p.ne + e[j]] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < WCB; q++) {
+            if (q >= nb) continue;
+#pragma unroll
+            for (int j = 0; j < EPL; j++) C.col[cs[q]][j * 64 + lane] = w[q][j];
+            if (lane == 0) {
+                const int old = C.ce[cs[q]];
+                if (old >= 0) C.colof[old] = -1;
+                C.ce[cs[q]] = (short)ss[q];
+                C.colof[ss[q]] = (short)cs[q];
+            }
+        }
+        CLF_SYNC();
+    }
+    if (lane == 0) C.next = nxt;
+    CLF_SYNC();
+}
+
 // The rare path's W gathers as unconditional loads (a clamped index outside the set, the value masked after the
 // load; a load under a branch makes the join wait for every load in flight) and the dual fallback's W[p, :] row
 // issued with its a = W[S, p]: for the force shape (two slots per lane). Same-box A/B (profiles/
@@ -238,13 +355,6 @@ __device__ __forceinline__ signed char flag_of(unsigned m, int j)
     return b == 1u ? (signed char)-1 : (b == 2u ? (signed char)1 : (signed char)0);
 }
 __device__ __forceinline__ unsigned bits_of(signed char f) { return f < 0 ? 1u : (f > 0 ? 2u : 0u); }
-
-#define CLF_SYNC()                                               \
-    do {                                                         \
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
-        __builtin_amdgcn_wave_barrier();                         \
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
-    } while (0)
 
 // the solver's initial point at element (k, r) (the lane-per-component kernel's failure output):
 // x_0 pinned, states at the reference projected 1 % inside their box, inputs mid-box
@@ -280,6 +390,10 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView
 {
     double row[WSM];
     const int ei = lane < m ? L.se_e[lane] : 0, si = lane < m ? L.gi_slot[lane] : 0;
+    if (NMPC_WCACHE && sv.wc_) {   // W_SS from the cached columns
+#pragma unroll
+        for (int j = 0; j < WSM; j++) row[j] = (j < m && lane < m) ? sv.wcv(L.gi_slot[j], si) : 0.0;
+    } else {
 #pragma unroll
     for (int j = 0; j < WSM; j++) {
         if constexpr (UNCOND_GATHER<EPL>) {   // clamped index, value masked after the load (no branch per load)
@@ -289,6 +403,7 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView
         } else {
             row[j] = (j < m && lane < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
         }
+    }
     }
     double wii = 1.0;
 #pragma unroll
@@ -335,6 +450,13 @@ __device__ __forceinline__ void sweep_gather(const ClFastParams<T> &p, LdsT &L, 
 {
     constexpr int CPL = HGeom<WSM>::CPL;
     const int ei = i < m ? L.se_e[i] : 0, si = i < m ? L.gi_slot[i] : 0;
+    if (NMPC_WCACHE && sv.wc_) {   // from the cached columns
+#pragma unroll
+        for (int q = 0; q < CPL; q++) {
+            const int j = g * CPL + q;
+            a[q] = (i < m && j < m) ? sv.wcv(L.gi_slot[j], si) : 0.0;
+        }
+    } else {
 #pragma unroll
     for (int q = 0; q < CPL; q++) {
         const int j = g * CPL + q;
@@ -345,6 +467,7 @@ __device__ __forceinline__ void sweep_gather(const ClFastParams<T> &p, LdsT &L, 
         } else {
             a[q] = (i < m && j < m) ? sv.w(p, L.se_e[j], L.gi_slot[j], ei, si) : 0.0;
         }
+    }
     }
 #pragma unroll
     for (int q = 0; q < CPL; q++)
@@ -561,6 +684,16 @@ __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const int
     int e[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; j++) e[j] = sv.e(j);
+    if (NMPC_WCACHE && sv.wc_) {   // the cached columns: LDS reads, same order of terms
+        for (int i = 0; i < m; i++) {
+            const A c = (A)cf[i];
+            const double *col = sv.wcol_ + sv.wcolof_[sl[i]] * sv.wcld_;
+#pragma unroll
+            for (int j = 0; j < EPL; j++)
+                if (e[j] >= 0) acc[j] = fma((A)col[j * 64 + sv.lane], c, acc[j]);
+        }
+        return;
+    }
     for (int i0 = 0; i0 < m; i0 += QB) {
         double w[QB][EPL];
 #pragma unroll
@@ -629,9 +762,12 @@ __device__ int load_set(LdsT &L, const SlotView<EPL> sv, int lane, unsigned wf, 
 // finish's PDAS rule. An emptied set restarts from z_0 (one round). Result: ok | m << 8 | steps << 16
 // (z in L.zb, the set in L.se_*); not ok: a set larger than WSM, W_SS not positive definite, or no
 // acceptance in polish_steps rounds. z: z_0 in, the solution out (when accepted).
+template <int WSM, int EPL>
+using WCacheOf = WCache<WSM + 1, EPL * 64>;
+
 template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
 __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, T (&z)[EPL], unsigned wf,
-                          int rounds)
+                          int rounds, WCacheOf<WSM, EPL> *wc = nullptr)
 {
     constexpr int NZ = NX + NU;
     static_assert(WSM <= 64, "active sets are lane-distributed");
@@ -717,6 +853,7 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         int pos[EPL];
         CLF_T(tl_set);
         load_set<T, EPL, WSM>(L, sv, lane, wf, z0, pos);
+        if (NMPC_WCACHE && sv.wc_) wc_fill<T, EPL>(p, *wc, sv, lane < m ? L.gi_slot[lane] : 0, m, 0u, lane);   // the set's columns
         CLF_TADD(L, 18, tl_set);
         // nu = W_SS^-1 (b - z_0)_S, lane i holding row i: Gauss-Jordan in registers for sets of up to 16
         // (one lane per row) and 32 (two lanes per row: register rows of 32 would go to scratch), the LDS
@@ -820,7 +957,7 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
 // modified.
 template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
 __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, const T (&z0)[EPL],
-                       unsigned w0, unsigned &wf, int &iters)
+                       unsigned w0, unsigned &wf, int &iters, WCacheOf<WSM, EPL> *wc = nullptr)
 {
     constexpr int CPL = HGeom<WSM>::CPL;
     const int ne = p.ne, hi_ = lane % WSM, hg = lane / WSM;
@@ -840,6 +977,7 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         wf = m <= WSM ? w0 : 0u;
         if (m > WSM) m = 0;
         if (m > 0) {
+            if (NMPC_WCACHE && sv.wc_) wc_fill<T, EPL>(p, *wc, sv, lane < m ? L.gi_slot[lane] : 0, m, 0u, lane);
             sweep_inverse<T, WSM>(p, L, sv, m, lane);
             am = m == 32 ? 0xffffffffu : ((1u << m) - 1u);
         } else {
@@ -897,6 +1035,10 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
         CLF_T(tg_sol);
         // a = W[S, p] (occupied positions) and W_pp, loads issued together
         const bool occ = pl && ((am >> lane) & 1u);
+        if (NMPC_WCACHE && sv.wc_) {   // the entering bound's column, keeping the set's
+            const unsigned keep = occ ? 1u << wc->colof[L.gi_slot[lane]] : 0u;
+            wc_fill<T, EPL>(p, *wc, sv, ps, 1, keep, lane);
+        }
         double ai;
         double wpj[EPL];   // (UNCOND_GATHER) W[p, slots] of the step direction, issued with a
         if constexpr (UNCOND_GATHER<EPL>) {
@@ -907,10 +1049,12 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
                 const int e = sv.e(j);
                 wpj[j] = sv.w(p, ep, ps, e >= 0 ? e : 0, e >= 0 ? j * 64 + lane : 0);
             }
+        } else if (NMPC_WCACHE && sv.wc_) {
+            ai = occ ? sv.wcv(ps, L.gi_slot[lane]) : 0.0;
         } else {
             ai = occ ? sv.w(p, L.se_e[lane], L.gi_slot[lane], ep, ps) : 0.0;
         }
-        const double wpp = sv.w(p, ep, ps, ep, ps);
+        const double wpp = (NMPC_WCACHE && sv.wc_) ? sv.wcv(ps, ps) : sv.w(p, ep, ps, ep, ps);
         double zc = 0.0;
 #pragma unroll
         for (int j = 0; j < EPL; j++)
@@ -945,7 +1089,7 @@ __device__ bool gi_set(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv
                 if (e >= 0) {
                     double wj;
                     if constexpr (UNCOND_GATHER<EPL>) wj = wpj[j];
-                    else wj = sv.w(p, ep, ps, e, j * 64 + lane);
+                    else wj = (NMPC_WCACHE && sv.wc_) ? sv.wcv(ps, j * 64 + lane) : sv.w(p, ep, ps, e, j * 64 + lane);
                     z[j] = fma(t, (double)sp * (wj - comb[j]), z[j]);
                 }
             }
@@ -1191,19 +1335,34 @@ __device__ void write_outputs(const ClFastParams<T> &p, LdsT &L, const SlotView<
 // the run after the fallback polish_steps. z: z_0 in, the solution out when accepted. Returns status |
 // accepted << 8 | ran the fallback << 9 | set size << 10 | (status 4 ? 0 : 1 + active-set steps) << 18.
 template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
-__device__ int slow_step(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, const double *abl,
-                         const double *cl, T (&z)[EPL], unsigned wf, bool cert_first, bool gi_prev)
+__device__ int slow_step(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv0, int lane, const double *abl,
+                         const double *cl, T (&z)[EPL], unsigned wf, bool cert_first, bool gi_prev,
+                         WCacheOf<WSM, EPL> *wc = nullptr)
 {
     int r = 0, steps_ = 0, status = 0;
     bool ran_gi = false;
     unsigned wset = wf;
+    // the workgroup's W column cache for this step, if no other wavefront holds it
+    SlotView<EPL> sv = sv0;
+    if (wc) {
+        int got = 0;
+        if (lane == 0) {
+            int expect = -1;
+            got = __hip_atomic_compare_exchange_strong(&wc->owner, &expect, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+        }
+        sv.wc_ = __builtin_amdgcn_readfirstlane(got) != 0;
+        sv.wcol_ = &wc->col[0][0];
+        sv.wcolof_ = wc->colof;
+        sv.wcld_ = EPL * 64;
+    }
     CLF_T(tcf);
     if (cert_first && certificate_infeasible<T, NX, NU>(p, L, abl, cl, lane)) status = 4;
     CLF_TADD(L, 6, tcf);
     for (int pass = 0; pass < 2 && status != 4; pass++) {
         const int rounds = pass == 1 ? p.polish_steps : (gi_prev ? 1 : min(p.polish_steps, PDAS_ROUNDS));
         CLF_T(tw0);
-        r = wsteps_run<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, rounds);
+        r = wsteps_run<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, rounds, wc);
         CLF_TADD(L, 2, tw0);
         steps_ += r >> 16;
         if ((r & 1) || pass == 1) break;
@@ -1218,11 +1377,15 @@ __device__ int slow_step(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> 
         int git = 0;
         ran_gi = true;
         CLF_T(tg0);
-        const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git);
+        const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git, wc);
         CLF_TADD(L, 5, tg0);
         CLF_TCNT(L, 11, git);
         steps_ += git;
         if (!found) break;
+    }
+    if (NMPC_WCACHE && sv.wc_) {   // the cache's columns and tags written before the next owner takes it
+        CLF_SYNC();
+        if (lane == 0) __hip_atomic_store(&wc->owner, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     const bool ok = (r & 1) != 0;
     const int m_acc = ok ? (r >> 8) & 0xff : 0;
@@ -1236,7 +1399,8 @@ __device__ int slow_step(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> 
 // needed, flags, u0, cost / AED, the outputs at the last step, the plant; write-back (or park).
 template <typename T, int NX, int NU, int EPL, int WSM, class SP, class LdsT, class ExplicitF>
 __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane,
-                                             const double *abl, const double *cl, int inst, ExplicitF &&explicit_form)
+                                             const double *abl, const double *cl, int inst, ExplicitF &&explicit_form,
+                                             WCacheOf<WSM, EPL> *wc = nullptr)
 {
     constexpr int NZ = NX + NU, NSLOT = EPL * 64;
     const int nref = p.ncl > p.aed_dims ? p.ncl : p.aed_dims;   // reference components of cost / AED
@@ -1339,7 +1503,7 @@ __device__ __forceinline__ void run_instance(const ClFastParams<T> &p, LdsT &L, 
         if (!ok) {
             CLF_TCNT(L, 12, 1);
             nslow++;
-            const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, wf, last_status == 4, gi_prev);
+            const int sr = slow_step<T, NX, NU, EPL, WSM>(p, L, sv, lane, abl, cl, z, wf, last_status == 4, gi_prev, wc);
             status = sr & 0xff;
             last_gi = (sr >> 9) & 1;
             ok = (sr >> 8) & 1;
@@ -1441,7 +1605,8 @@ constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host ch
 // steps (capped). Groups: bit 7 set, then any rare-path steps, then the rest (buckets = 1: each of the
 // first two split by the rare-path steps, >= 8 / 1-7 / 0 and >= 8 / 1-7); instance order within a group
 // (hard null: instance order)
-__device__ inline void claim_order(unsigned short *ord, const unsigned char *hard, int lo, int cnt, int lane, int buckets)
+__device__ inline void claim_order(unsigned short *ord, const unsigned char *hard, const int *map, int lo, int cnt, int lane,
+                                   int buckets)
 {
     const unsigned long long lt = (1ull << lane) - 1ull;
     constexpr int MN[2][6] = {{128, 1, 0, 0, 0, 0}, {136, 129, 128, 8, 1, 0}}, MX[2][6] = {{255, 127, 0, 0, 0, 0}, {255, 135, 128, 127, 7, 0}};
@@ -1451,7 +1616,7 @@ __device__ inline void claim_order(unsigned short *ord, const unsigned char *har
         const int mn = nb == 1 ? 0 : MN[buckets ? 1 : 0][b], mx = nb == 1 ? 255 : MX[buckets ? 1 : 0][b];
         for (int c = 0; c < cnt; c += 64) {
             const bool in = c + lane < cnt;
-            const int h = in && hard ? (int)hard[lo + c + lane] : 0;
+            const int h = in && hard ? (int)hard[map ? map[lo + c + lane] : lo + c + lane] : 0;
             const bool d = in && h >= mn && h <= mx;
             const unsigned long long m = __ballot(d);
             if (d) ord[pos + __popcll(m & lt)] = (unsigned short)(c + lane);
@@ -1518,6 +1683,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     }
     __shared__ int wg_next;   // the workgroup's next instance (offset into its range)
     __shared__ unsigned short ord[LOCK_QCAP];   // claim order (offsets into the workgroup's range)
+    // the W column cache (sets of up to 16: quad13, jerk; not with W in LDS)
+    constexpr bool WCACHE = NMPC_WCACHE && WSM <= 16 && !WL;
+    using WCT = typename std::conditional<WCACHE, WCacheOf<WSM, EPL>, char>::type;
+    __shared__ WCT wcache_;
+    WCacheOf<WSM, EPL> *wcp = nullptr;
+    if constexpr (WCACHE) {
+        wc_init(wcache_);
+        if (p.wcache) wcp = &wcache_;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Lds<NSLOT, NZ, WSM, SW2> &L = lds_all[wave];
     if (lane < 32) L.xs[lane] = 0.0;
@@ -1530,7 +1704,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // the previous launch's rare-path instances first (longest first: the workgroup's makespan), when the
     // range fits the order table
     const bool ordered = !p.claim_global && p.demoted && wg_hi - wg_lo <= LOCK_QCAP;
-    if (ordered && wave == 0) claim_order(ord, p.demoted, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
+    if (ordered && wave == 0) claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane, wtri, WL};
 
@@ -1551,7 +1725,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         if (lane == 0) next = p.claim_global ? atomicAdd(p.park_count + 1, 1) : atomicAdd(&wg_next, 1);
         next = __builtin_amdgcn_readfirstlane(next);
         if (wg_lo + next >= wg_hi) break;
-        const int inst = wg_lo + (ordered ? (int)ord[next] : next);
+        const int pos = wg_lo + (ordered ? (int)ord[next] : next);
+        const int inst = (p.inst_map && !p.claim_global) ? p.inst_map[pos] : pos;
         // explicit unconstrained solution at the lane's slots: T_x pairs from LDS against x pairs broadcast
         run_instance<T, NX, NU, EPL, WSM, SP>(p, L, sv, lane, abl, cl, inst, [&](T(&z)[EPL], const T(&vt)[EPL]) {
             T z1[EPL];
@@ -1573,7 +1748,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             }
 #pragma unroll
             for (int j = 0; j < EPL; j++) z[j] += z1[j];
-        });
+        }, wcp);
     }
 }
 
@@ -1810,6 +1985,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     __shared__ int dq[LOCK_QCAP];                       // demoted instances (-1: slot not yet written)
     __shared__ unsigned short ord[LOCK_QCAP];           // claim order (offsets into the workgroup's range)
     __shared__ int wg_next, dq_tail, dq_head, ph1_done;
+    constexpr bool WCACHE = NMPC_WCACHE && WSM <= 16;   // the W column cache of the rare path
+    using WCT = typename std::conditional<WCACHE, WCacheOf<WSM, EPL>, char>::type;
+    __shared__ WCT wcache_;
+    WCacheOf<WSM, EPL> *wcp = nullptr;
+    if constexpr (WCACHE) {
+        wc_init(wcache_);
+        if (p.wcache) wcp = &wcache_;
+    }
     for (int e = threadIdx.x; e < NT * KC * 64; e += 64 * WPB) {
         const int t = e / (KC * 64), kc = (e / 64) % KC, l = e % 64;
         const int s_ = 16 * t + 4 * ((l >> 2) & 3) + (l & 3), c = 4 * kc + (l >> 4);
@@ -1851,7 +2034,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // claim order: the instances the previous launch demoted first (the launch's longest chains start at its
     // beginning, not behind the lockstep ones), then the rest, each group in instance order. Only the
     // schedule changes: an instance runs lockstep until its first rare step wherever it is claimed
-    if (wave == 0) claim_order(ord, p.demoted, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
+    if (wave == 0) claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
     const int n = lane & 3, ti = lane >> 4, tb = (lane >> 2) & 3;   // instance slot; D-layout slot offset
@@ -1887,6 +2070,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             if (!want) return;
             CLF_CHECK(nx_ >= wg_hi - wg_lo || nx_ < LOCK_QCAP, 1, nx_);
             inst = nx_ < wg_hi - wg_lo ? wg_lo + (int)ord[nx_] : -1;
+            if (inst >= 0 && p.inst_map) inst = p.inst_map[inst];
             CLF_CHECK(inst < p.B, 2, inst);
             flany = false;
             cost = aed = 0.0;
@@ -2232,7 +2416,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
 #pragma unroll
             for (int j = 0; j < EPL; j++) z[j] = vt[j] + (T)zb[j * 64 + lane];
             CLF_SYNC();
-        });
+        }, wcp);
     }
 }
 
@@ -2331,6 +2515,19 @@ int cl_fast_resident(int nx, int nu, int sid, int kind, bool f64, int device)
 }
 
 // grid: min(workgroups for one wavefront per instance, the resident workgroups)
+int cl_fast_grid(int nx, int nu, int sid, int kind, bool f64, int waves, int resident)
+{
+    int blocks = 0;
+    auto g = [&](auto v) {
+        using V = decltype(v);
+        const int wv = kind == CLF_LOCK ? (waves + 3) / 4 : waves;
+        blocks = std::max(1, std::min((wv + V::WPB - 1) / V::WPB, resident));
+    };
+    if (f64) clf_dispatch<double>(nx, nu, sid, kind, g);
+    else clf_dispatch<float>(nx, nu, sid, kind, g);
+    return blocks;
+}
+
 template <typename T>
 hipError_t cl_fast_launch(int nx, int nu, int sid, int kind, const ClFastParams<T> &p, int waves, int resident,
                           hipStream_t s)

@@ -122,6 +122,9 @@ struct ClFastParams {
     int lock_workers;             // lockstep kernel: wavefronts per workgroup that start in phase 2
     int lock_prio;                // lockstep kernel: phase-2 wavefronts at raised issue priority
     int claim_global;             // cl_fast_kernel: instances from one device-wide counter (park_count[1])
+    int wcache;                   // 1: the rare path's W column cache in LDS (quad13 / jerk shapes; env NMPC_CLF_WCACHE=0: off)
+    const int *inst_map;          // or null: position -> instance of the per-workgroup claim ranges (nmpc_api.cpp
+                                  // clf_xcd_map: each XCD's workgroups own a contiguous stretch of reference-table rows)
     unsigned char *demoted;       // [B] the previous launch's rare-path steps | 128 if its last solution left bounds
                                   // active (lockstep: 1 at demotion), or null: the claim order's key
     int order_buckets;            // claim order: 0 three groups (warm start, rare path, rest); 1 six
@@ -220,6 +223,8 @@ constexpr int CLF_FAST = 0, CLF_LOCK = 1, CLF_WLDS = 2, CLF_ONE = 3;
 // workgroups of the shape's cl_fast_kernel (lock: cl_lock_kernel, fp64 only) in the handle's precision
 // that `device` holds at once (the persistent grid), or 0
 int cl_fast_resident(int nx, int nu, int sid, int kind, bool f64, int device);
+// the lean-loop launch's workgroup count for `waves` (instances) and `resident` (cl_fast_launch's grid)
+int cl_fast_grid(int nx, int nu, int sid, int kind, bool f64, int waves, int resident);
 // grid = min(waves / wavefronts per workgroup, resident); waves = instances (lock: instances / 4)
 template <typename T>
 hipError_t cl_fast_launch(int nx, int nu, int sid, int kind, const ClFastParams<T> &p, int waves, int resident,

@@ -1,13 +1,27 @@
 #!/bin/bash
-# A/B of an environment knob over the BASELINE configs (tuning aid, GPU box):
-#   KNOB=NMPC_WARM_SHIFT VALUES="1 0" [CONFIGS="--model quad13;--model force --batch 1024"] bash tools/ab_env.sh
+# Same-box A/B of an environment switch on bench lines: for each config in CFGS (";"-separated bench.py argument
+# sets), alternate A and B (REPS times), one JSON line each into gpurun_out/ab_<TAG>.jsonl tagged with the arm.
+#   TAG=x A="NMPC_CLF_XCD=0" B="NMPC_CLF_XCD=1" CFGS="--model quad13;--model jerk --batch 4096" REPS=2 bash tools/ab_env.sh
+# (ARMS="A B C" with C=... for a third arm)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-for v in ${VALUES}; do
-  IFS=';' read -ra CFGS <<< "${CONFIGS:---model quad13;--model jerk --batch 4096;--model force --batch 1024}"
-  for a in "${CFGS[@]}"; do
-    env $KNOB=$v timeout -k 10 200 python bench.py $a --no-cpu-baseline --repeats ${REPEATS:-5} > $OUT/ab.json 2> $OUT/ab.err || { echo "bench failed: $KNOB=$v $a"; tail -5 $OUT/ab.err; exit 1; }
-    python -c "import json; b=json.load(open('$OUT/ab.json')); print('$KNOB=$v', b['config']['model'], b['config']['batch_per_gpu'], '%.3fM' % (b['value']/1e6), 'kernel %.4f' % b['roofline']['kernel_ms'], 'failed', b['closed_loop']['failed_solves'], flush=True)"
+: > $OUT/ab_$TAG.jsonl
+IFS=';' read -ra CS <<< "$CFGS"
+for c in "${CS[@]}"; do
+  for r in $(seq ${REPS:-2}); do
+    for arm in ${ARMS:-A B}; do
+      envs=${!arm}
+      line=$(env $envs timeout -k 10 300 python bench.py $c --no-cpu-baseline --python-loop-steps 0 2>> $OUT/ab_$TAG.err) || { echo "bench failed: $arm $c"; tail -20 $OUT/ab_$TAG.err; exit 1; }
+      python -c "import json,sys; d=json.loads(sys.argv[1]); d['ab_arm']=sys.argv[2]; d['ab_env']=sys.argv[3]; print(json.dumps(d))" "$line" "$arm" "$envs" >> $OUT/ab_$TAG.jsonl
+    done
   done
 done
+python - "$OUT/ab_$TAG.jsonl" <<'PY'
+import json, sys
+from collections import defaultdict
+r = defaultdict(list)
+for l in open(sys.argv[1]):
+    d = json.loads(l); r[(d['config']['model'], d['dtype'], d['config']['batch_per_gpu'], d['ab_arm'], d['ab_env'])].append(d['value'] / 1e6)
+for k, v in sorted(r.items()): print(k, ' '.join('%.1f' % x for x in v))
+PY
