@@ -761,12 +761,13 @@ __device__ int load_set(LdsT &L, const SlotView<EPL> sv, int lane, unsigned wf, 
 // sign (displacement nu_i W_ii to 1e-10 (1 + |b - z_0|)); otherwise removals and additions as the
 // finish's PDAS rule. An emptied set restarts from z_0 (one round). Result: ok | m << 8 | steps << 16
 // (z in L.zb, the set in L.se_*); not ok: a set larger than WSM, W_SS not positive definite, or no
-// acceptance in polish_steps rounds. z: z_0 in, the solution out (when accepted).
+// acceptance in polish_steps rounds. z: z_0 in, the solution out (when accepted); wf: the set the rounds start from
+// in, the set they reached out (the dual fallback starts from it)
 template <int WSM, int EPL>
 using WCacheOf = WCache<WSM + 1, EPL * 64>;
 
 template <typename T, int NX, int NU, int EPL, int WSM, class LdsT>
-__device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, T (&z)[EPL], unsigned wf,
+__device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> sv, int lane, T (&z)[EPL], unsigned &wf,
                           int rounds, WCacheOf<WSM, EPL> *wc = nullptr)
 {
     constexpr int NZ = NX + NU;
@@ -1377,7 +1378,9 @@ __device__ int slow_step(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> 
         int git = 0;
         ran_gi = true;
         CLF_T(tg0);
-        const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wf, wset, git, wc);
+        // from the set the PDAS rounds reached (wsteps_run leaves it in wset), made dual feasible — not the warm set
+        // they started from (oracle/c/riccati_ipm.c: quad13 longest chain 44 -> 36 set steps, force B = 1024 -15 %)
+        const bool found = gi_set<T, NX, NU, EPL, WSM>(p, L, sv, lane, z, wset, wset, git, wc);
         CLF_TADD(L, 5, tg0);
         CLF_TCNT(L, 11, git);
         steps_ += git;

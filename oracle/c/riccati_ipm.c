@@ -1617,6 +1617,10 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                         if (!ok && infeasible_stage(d, st) == 0) {
                             int git = 0;
                             gi_prev = 1;
+                            /* the fallback starts from the set the PDAS rounds reached (made dual feasible), not
+                             * the warm set they started from: quad13 longest chain 44 -> 36, force B = 1024
+                             * 145 -> 137 / 118 -> 98 / 123 -> 103 set steps per region (tools/chain_model.py) */
+                            memcpy(w0, wf, (size_t)ne);
                             if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
                                 ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
                                 cnt[3] += wst;
@@ -1780,6 +1784,7 @@ int riccati_ipm_solve_batch_fast(const ocp_ref_desc *d, const void *tables, int 
             ok = fast_finish_z0(d, f, wf, z0, zf, &wst, &cnt[6], wsmax, r0) > 0;
             it += wst;
             if (!ok && infeasible_stage(d, xb) == 0) {
+                memcpy(w0, wf, (size_t)ne);   /* the fallback from the set the PDAS rounds reached (as the closed loop) */
                 if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
                     ok = fast_finish_z0(d, f, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
                     it += wst;
