@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 PMC passes of tools/pmc.sh for one kernel.
 
-    python tools/pmc_summary.py TAG [--kernel ipm_kernel] [--out profiles/r1_pmc_TAG.json]
+    python tools/pmc_summary.py TAG [--kernel ipm_kernel] [--out profiles/history/r1_pmc_TAG.json]
         [--traffic model,N,batch,precision]
 
 Reads gpurun_out/pmc_<TAG>_<i>/run_counter_collection.csv (one counter group per pass),
@@ -16,7 +16,7 @@ FETCH_SIZE/WRITE_SIZE count L2 <-> fabric requests, so Infinity-Cache (MALL) hit
 included. MI355X_MICROARCH.md: on gfx950 FETCH_SIZE reports half the bytes of a coalesced
 streaming read (calibrated there for 16-B lanes); the same half holds for this engine's 8-B-per-lane
 coalesced loads, calibrated on a known byte count — sf_kernel reads x0 + the yref windows, 24.0 MB
-per quad13 B = 8192 solve, and FETCH_SIZE reports 12.5 MB (profiles/r6j_solve_quad13_sf_pmc.json),
+per quad13 B = 8192 solve, and FETCH_SIZE reports 12.5 MB (profiles/history/r6j_solve_quad13_sf_pmc.json),
 while WRITE_SIZE matches its 23.0 MB of trajectory stores. So FETCH_CORR = 2, WRITE_SIZE as is.
 
     python tools/pmc_summary.py --rebuild    re-derive every profiles/pmc_traffic.json entry from
@@ -70,7 +70,7 @@ def rebuild():
     d = json.load(open(TRAFFIC))
     out = []
     for e in d["entries"]:
-        src = os.path.join("profiles", os.path.basename(e["source"]))
+        src = e["source"]
         means = json.load(open(os.path.join(ROOT, src)))["mean_per_dispatch"]
         out.append(entry(means, e["model"], e["N"], e["batch"], e["precision"], e["kernel"], e["steps_per_launch"],
                          e.get("mode", "closed_loop"), src))
