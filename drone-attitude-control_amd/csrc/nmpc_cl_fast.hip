@@ -385,14 +385,8 @@ __device__ T init_point(const ClFastParams<T> &p, int nx, int nz, int k, int r, 
 // readlane, every other row eliminates column c, so at the end nu_i = t_i / (row i's pivot). Pivots get
 // fast_finish's regularisation (below 1e-9 of W_ii: + 1e-6 W_ii), i.e. the same regularised system the
 // oracle's Cholesky solves. The diagonal W_ii goes to L.wdg (the multiplier test). pd: every W_ii > 0.
-struct NoHook {
-    __device__ void operator()() const {}
-};
-// after_gather: called once the gather's loads are issued and before their first use (the caller issues the
-// combination's first W rows there, so both load rounds share one memory latency)
-template <typename T, int WSM, int EPL, class LdsT, class Hook = NoHook>
-__device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> &sv, int m, int lane, double t, bool &pd,
-                               Hook &&after_gather = Hook{})
+template <typename T, int WSM, int EPL, class LdsT>
+__device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL> &sv, int m, int lane, double t, bool &pd)
 {
     double row[WSM];
     const int ei = lane < m ? L.se_e[lane] : 0, si = lane < m ? L.gi_slot[lane] : 0;
@@ -411,7 +405,6 @@ __device__ double solve_set_gj(const ClFastParams<T> &p, LdsT &L, const SlotView
         }
     }
     }
-    after_gather();
     double wii = 1.0;
 #pragma unroll
     for (int j = 0; j < WSM; j++)
@@ -683,43 +676,11 @@ __device__ int compact_set(LdsT &L, unsigned am, int lane, double coef)
 // lane's slots in flight together (one memory latency per batch, not one per slot and batch); per slot
 // the sum runs in list order, in the accumulator's precision A (fp64 for both storage precisions: the
 // terms of an ill-conditioned set cancel)
-template <int EPL>
-constexpr int combo_qb() { return EPL <= 2 ? 8 : (EPL <= 4 ? 4 : 2); }
-// rows of the combination's first batch loaded early (behind the set solve's gather): what the register budget
-// takes — 2 of quad13's 4 (the whole batch spilled 61 VGPRs), jerk's whole batch of 2, none for the force shape
-// (its default variant dropped to one wavefront per SIMD)
-template <int EPL>
-constexpr int combo_pre() { return EPL <= 2 ? 4 : combo_qb<EPL>(); }
-
-// the combination's first batch of W rows (set positions 0 .. QB - 1), issued early (wsteps_run: during the set
-// solve's gather): w[q][j] = W[e_q][e(slot j)], 0 beyond the set
-template <typename T, int EPL>
-__device__ void w_combo_first(const ClFastParams<T> &p, const int *el, const int *sl, const SlotView<EPL> sv, int m,
-                              double (&w)[combo_pre<EPL>() > 0 ? combo_pre<EPL>() : 1][EPL])
-{
-    constexpr int QB = combo_pre<EPL>();
-#pragma unroll
-    for (int q = 0; q < QB; q++) {
-        const int row = q < m ? el[q] : 0, rs = q < m ? sl[q] : 0;
-#pragma unroll
-        for (int j = 0; j < EPL; j++) {
-            const int e = sv.e(j);
-            if constexpr (UNCOND_GATHER<EPL>) {
-                const double wl = sv.w(p, row, rs, e >= 0 ? e : 0, e >= 0 ? j * 64 + sv.lane : 0);
-                w[q][j] = (q < m && e >= 0) ? wl : 0.0;
-            } else {
-                w[q][j] = (q < m && e >= 0) ? sv.w(p, row, rs, e, j * 64 + sv.lane) : 0.0;
-            }
-        }
-    }
-}
-
-template <typename T, int EPL, typename A, bool PRE = false>
+template <typename T, int EPL, typename A>
 __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const int *sl, const SlotView<EPL> sv,
-                              const double *cf, int m, A (&acc)[EPL],
-                              const double (&pre)[combo_pre<EPL>() > 0 ? combo_pre<EPL>() : 1][EPL] = {}, bool use_pre = false)
+                              const double *cf, int m, A (&acc)[EPL])
 {
-    constexpr int QB = combo_qb<EPL>(), PQ = PRE ? combo_pre<EPL>() : 0;
+    constexpr int QB = EPL <= 2 ? 8 : (EPL <= 4 ? 4 : 2);
     int e[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; j++) e[j] = sv.e(j);
@@ -737,11 +698,6 @@ __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const int
         double w[QB][EPL];
 #pragma unroll
         for (int q = 0; q < QB; q++) {
-            if (PQ > 0 && use_pre && i0 == 0 && q < PQ) {   // loaded early by the caller
-#pragma unroll
-                for (int j = 0; j < EPL; j++) w[q][j] = pre[q < PQ ? q : 0][j];
-                continue;
-            }
             const int row = i0 + q < m ? el[i0 + q] : 0, rs = i0 + q < m ? sl[i0 + q] : 0;
 #pragma unroll
             for (int j = 0; j < EPL; j++) {
@@ -906,17 +862,8 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
         bool pd = true;
         double y;
         CLF_T(ts0);
-        double wpre[combo_pre<EPL>() > 0 ? combo_pre<EPL>() : 1][EPL];
-        bool have_pre = false;
         if (WSM <= 16 || m <= 16) {
-            // the combination's first W rows issued behind the gather: one memory latency for both (sets of up to
-            // combo_qb rows need no further load round)
-            y = solve_set_gj<T, (WSM < 16 ? WSM : 16)>(p, L, sv, m, lane, lane < m ? L.se_t[lane] : 0.0, pd, [&]() {
-                if (combo_pre<EPL>() > 0 && !(NMPC_WCACHE && sv.wc_)) {
-                    w_combo_first<T, EPL>(p, L.se_e, L.gi_slot, sv, m, wpre);
-                    have_pre = true;
-                }
-            });
+            y = solve_set_gj<T, (WSM < 16 ? WSM : 16)>(p, L, sv, m, lane, lane < m ? L.se_t[lane] : 0.0, pd);
         } else {
             // sets of 17..WSM: the sweep's explicit inverse, nu = H (b - z_0)_S
             pd = sweep_inverse<T, WSM>(p, L, sv, m, lane);
@@ -952,7 +899,7 @@ __device__ int wsteps_run(const ClFastParams<T> &p, LdsT &L, const SlotView<EPL>
 #pragma unroll
         for (int j = 0; j < EPL; j++) zd[j] = (double)z0[j];
         CLF_T(tc0);
-        w_combo_slots<T, EPL, double, true>(p, L.se_e, L.gi_slot, sv, L.se_nu, m, zd, wpre, have_pre);
+        w_combo_slots<T, EPL>(p, L.se_e, L.gi_slot, sv, L.se_nu, m, zd);
         CLF_TADD(L, 4, tc0);
         CLF_T(tk0);
 #pragma unroll
