@@ -41,7 +41,7 @@ step "step log"
 timeout -k 10 200 python tools/clf_steps.py --model quad13 --batch 8192 --regions 3 > $OUT/steps_quad13.json || { echo "step log failed"; exit 1; }
 step "rocprofv3 kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_quad13 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --python-loop-steps 0 > $OUT/prof_quad13.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof_quad13.log; exit 1; }
-if [ "${PMC:-1}" = "1" ]; then
+if [ "${PMC:-1}" = "1" ]; then   # (also alone: tools/pmc_only.sh)
   i=0
   for cfg in "quad13:--model quad13" "force1024:--model force --batch 1024" "force8192f32:--model force --batch 8192 --precision fp32" "jerk:--model jerk --batch 4096" "quad13f32:--model quad13 --precision fp32"; do
     name=${cfg%%:*}; args=${cfg#*:}
