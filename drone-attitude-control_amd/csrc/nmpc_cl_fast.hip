@@ -680,7 +680,10 @@ template <typename T, int EPL, typename A>
 __device__ void w_combo_slots(const ClFastParams<T> &p, const int *el, const int *sl, const SlotView<EPL> sv,
                               const double *cf, int m, A (&acc)[EPL])
 {
-    constexpr int QB = EPL <= 2 ? 8 : (EPL <= 4 ? 4 : 2);
+#ifndef NMPC_QB34
+#define NMPC_QB34 4
+#endif
+    constexpr int QB = EPL <= 2 ? 8 : (EPL <= 4 ? NMPC_QB34 : 2);
     int e[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; j++) e[j] = sv.e(j);

@@ -1206,6 +1206,7 @@ static int gi_set(const ocp_ref_desc *d, const fast_tables *f, const double *z0,
 {
     const int nx = d->nx, nu = d->nu, N = d->N, nz = nx + nu, ne = f->ne;
     int A[WSMAX], sg[WSMAX], m = 0, p = -1, sp = 0, it;
+    *iters = 0;
     double u[WSMAX], l[WSMAX], r[WSMAX], up = 0.0, z[NZMAX * 64];
     static double L[WSMAX][WSMAX];
 #pragma omp threadprivate(L)
@@ -1284,7 +1285,7 @@ static int gi_set(const ocp_ref_desc *d, const fast_tables *f, const double *z0,
         const double cp = sp * (z[p] - (sp > 0 ? LBk(d, kp, ip) : UBk(d, kp, ip)));
         const double t2 = theta > 1e-12 * wpp ? -cp / theta : INFINITY;
         *flops += 2.0 * m * m + 2.0 * m;
-        if (t1 == INFINITY && t2 == INFINITY) return -5;
+        if (t1 == INFINITY && t2 == INFINITY) { *iters = it + 1; return -5; }
         const int full = t2 <= t1;
         const double t = full ? t2 : t1;
         if (t2 < INFINITY) {
@@ -1301,7 +1302,7 @@ static int gi_set(const ocp_ref_desc *d, const fast_tables *f, const double *z0,
         for (int i = 0; i < m; i++) u[i] -= t * r[i];
         up += t;
         if (full) {
-            if (m >= wsmax) return -6;
+            if (m >= wsmax) { *iters = it + 1; return -6; }
             for (int q = 0; q < m; q++) L[m][q] = l[q];
             L[m][m] = sqrt(theta);
             A[m] = p; sg[m] = sp; u[m] = up; m++;
@@ -1566,7 +1567,10 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
         double *z0 = (double *)malloc(sizeof(double) * ne), *zf = (double *)malloc(sizeof(double) * ne);
         signed char *wf = (signed char *)malloc(ne), *w0 = (signed char *)malloc(ne);
         const char *dbg_env = getenv("RIC_DEBUG_INST");
-        const int path_cost = getenv("RIC_PATH_COST") != NULL;   /* tuning aid: path + 16 x the step's active-set steps */
+        const int path_cost = getenv("RIC_PATH_COST") != NULL;   /* tuning aid: path | active-set steps << 4 | certificates << 12 */
+        /* tuning experiment (tools/chain_model.py): the certificate after the dual fallback instead of
+         * before it — DESIGN.md §3.9 has the result (force's chains -7 %, quad13's and jerk's longer) */
+        const int cert_after = getenv("RIC_CERT_AFTER") && getenv("RIC_CERT_AFTER")[0] == '1';
         const int dbg_inst = dbg_env ? atoi(dbg_env) : -1;
 #pragma omp for schedule(dynamic, 4)
         for (int b = 0; b < batch; b++) {
@@ -1579,7 +1583,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                 const int step = step0 + s, t = (int)(((long long)offsets[b] + step) % c->period);
                 for (int k = 0; k < N; k++) memcpy(yref + (size_t)k * ny, c->table + (size_t)(t + k) * c->cols, sizeof(double) * ny);
                 memcpy(yref + (size_t)N * ny, c->table + (size_t)(t + N) * c->cols, sizeof(double) * nye);
-                int status = 0, path = 2, iters = 0, ok = 0, step_sets = 0;
+                int status = 0, path = 2, iters = 0, ok = 0, step_sets = 0, step_certs = 0;
                 if (ric_dbg) fprintf(stderr, "step %d t=%d\n", step, t);
                 /* mode 1 tries the fast path from the first step on (an empty warm set at step 0) */
                 const int warm = mode == 1 && ab != NULL;
@@ -1607,6 +1611,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                         const int cert_first = failed && failed[b];
                         const int r0 = gi_prev ? 1 : (d->polish_steps < PDAS_ROUNDS ? d->polish_steps : PDAS_ROUNDS);
                         gi_prev = 0;
+                        step_certs += cert_first;
                         if (!(cert_first && infeasible_stage(d, st) > 0))
                             ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, r0) > 0;
                         cnt[3] += wst;
@@ -1614,19 +1619,21 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                         /* not settled: unless the interval certificate proves the QP infeasible (solve_one
                          * returns that), the dual active-set fallback, its set then solved and checked by
                          * fast_finish */
-                        if (!ok && infeasible_stage(d, st) == 0) {
+                        if (!ok && !cert_after) step_certs++;
+                        if (!ok && (cert_after || infeasible_stage(d, st) == 0)) {
                             int git = 0;
                             gi_prev = 1;
                             /* the fallback starts from the set the PDAS rounds reached (made dual feasible), not
                              * the warm set they started from: quad13 longest chain 44 -> 36, force B = 1024
                              * 145 -> 137 / 118 -> 98 / 123 -> 103 set steps per region (tools/chain_model.py) */
                             memcpy(w0, wf, (size_t)ne);
-                            if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
+                            const int gr = gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]);
+                            if (gr > 0) {
                                 ok = fast_finish(d, f, st, t, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
                                 cnt[3] += wst;
                                 step_sets += wst;
                             }
-                            cnt[3] += git;
+                            cnt[3] += gr == -5 || gr == -6 ? 0 : git;   /* (the early exits count no steps) */
                             step_sets += git;
                         }
                         if (ok) {
@@ -1641,6 +1648,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                     }
                 }
                 if (!ok) {
+                    step_certs++;   /* (solve_one's certificate) */
                     status = solve_one(d, st, yref, xo, uo, &iters, &w, warm ? wf : NULL, 0);
                     if (mode == 0 && status == 0) {
                         const int kr = kkt_refine(d, st, yref, xo, uo);
@@ -1675,7 +1683,7 @@ int riccati_ipm_closed_loop(const ocp_ref_desc *d, const cl_ref_desc *c, int bat
                 if (u_log) memcpy(u_log + ((size_t)b * steps + s) * nu, uo, sizeof(double) * nu);
                 if (x_log) memcpy(x_log + ((size_t)b * steps + s) * nx, st, sizeof(double) * nx);
                 if (status_log) status_log[(size_t)b * steps + s] = status;
-                if (path_log) path_log[(size_t)b * steps + s] = path + (path_cost ? 16 * step_sets : 0);
+                if (path_log) path_log[(size_t)b * steps + s] = path + (path_cost ? (step_sets << 4 | step_certs << 12) : 0);
             }
         }
         free(buf); free(yref); free(xo); free(uo); free(z0); free(zf); free(wf); free(w0);
@@ -1785,11 +1793,12 @@ int riccati_ipm_solve_batch_fast(const ocp_ref_desc *d, const void *tables, int 
             it += wst;
             if (!ok && infeasible_stage(d, xb) == 0) {
                 memcpy(w0, wf, (size_t)ne);   /* the fallback from the set the PDAS rounds reached (as the closed loop) */
-                if (gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]) > 0) {
+                const int gr = gi_set(d, f, z0, w0, wf, wsmax, &git, &cnt[6]);
+                if (gr > 0) {
                     ok = fast_finish_z0(d, f, wf, z0, zf, &wst, &cnt[6], wsmax, d->polish_steps) > 0;
                     it += wst;
                 }
-                it += git;
+                it += gr == -5 || gr == -6 ? 0 : git;
             }
             cnt[3] += it;
             if (ok) {

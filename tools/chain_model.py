@@ -12,6 +12,7 @@ import sys
 import numpy as np
 
 os.environ["RIC_PATH_COST"] = "1"
+CERT = float(os.environ.get("CERT", "0.5"))
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -37,12 +38,16 @@ def main():
     out = []
     for _ in range(args.regions):
         _, _, _, path = cl.run(args.steps, logs=True)
-        sets = path >> 4
+        sets = (path >> 4) & 255
+        certs = path >> 12
         chain = sets.sum(1)
+        cost = sets + CERT * certs   # in PDAS-round units (env CERT: the certificate's cost per round)
+        wc = cost.sum(1)
         out.append({"sets_total": int(sets.sum()), "chain_max": int(chain.max()), "chain_p999": float(np.percentile(chain, 99.9)),
                     "chain_p99": float(np.percentile(chain, 99)), "instances_with_sets": int((chain > 0).sum()),
                     "worst": int(chain.argmax()), "worst_steps": sets[chain.argmax()].tolist(),
-                    "full": int(((path & 15) == 2).sum())})
+                    "full": int(((path & 15) == 2).sum()), "certs_total": int(certs.sum()),
+                    "cost_max": float(wc.max()), "cost_p999": float(np.percentile(wc, 99.9))})
     print(json.dumps({"model": args.model, "batch": args.batch, "warm_end": os.environ.get("RIC_WARM_END", "0"),
                       "regions": out}))
 
