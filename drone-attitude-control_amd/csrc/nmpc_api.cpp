@@ -1346,10 +1346,26 @@ int nmpc_solve_async(nmpc_solver *h)
     return h->precision == NMPC_FP64 ? launch<double>(h) : launch<float>(h);
 }
 
+// The host's wait for the handle's stream. hipStreamSynchronize parks the thread once its short active wait has
+// passed and wakes ~10-20 µs after the work ends (the bench timeline, rocprofv3 API trace: 22 µs from the lean
+// kernel's end to the return); a closed-loop controller waits on the critical path every step, so the wait
+// polls the stream instead (hipStreamQuery until done: one core busy for the kernel's duration). Env
+// NMPC_SPIN_WAIT=0: hipStreamSynchronize.
+hipError_t stream_wait(hipStream_t s)
+{
+    static const bool spin = !(std::getenv("NMPC_SPIN_WAIT") && std::getenv("NMPC_SPIN_WAIT")[0] == '0');
+    if (!spin) return hipStreamSynchronize(s);
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    (void)hipGetLastError();   // (the polls' not-ready status is not a launch error)
+    return e;
+}
+
 int nmpc_synchronize(nmpc_solver *h)
 {
     if (!h) return NMPC_EINVAL;
-    hipError_t e = hipStreamSynchronize(h->stream);
+    hipError_t e = stream_wait(h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize");
     const int r = sf_resolve(h);   // the last fast solve's listed / parked counts (its kernels are done)
     if (r < 0) return r;
@@ -1376,7 +1392,7 @@ static int download_outputs(nmpc_solver *h)
     }
     hipMemcpyAsync(h->h_status.data(), h->d_status, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
     hipMemcpyAsync(h->h_iters.data(), h->d_iters, h->batch * sizeof(int), hipMemcpyDeviceToHost, h->stream);
-    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return hip_fail(h, e, "solve");
+    if ((e = stream_wait(h->stream)) != hipSuccess) return hip_fail(h, e, "solve");
     if (h->precision == NMPC_FP32) {
         for (size_t i = 0; i < nxo; i++) h->h_x[i] = fx[i];
         for (size_t i = 0; i < nuo; i++) h->h_u[i] = fu[i];
@@ -2100,12 +2116,17 @@ int clf_setup(nmpc_solver *h, const nmpc_closed_loop_desc &d, const std::vector<
     bool ok = hipMalloc(&h->d_fsT, tot * es) == hipSuccess &&
               hipMalloc((void **)&h->d_fsI, itot * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_istep, (size_t)h->batch * sizeof(int)) == hipSuccess &&
-              hipMalloc((void **)&h->d_park, (size_t)(h->batch + 2 + CLF_ROUND_WORDS) * sizeof(int)) == hipSuccess &&
+              hipMalloc((void **)&h->d_park, (size_t)(h->batch + 2 + CLF_ROUND_WORDS + 1) * sizeof(int)) == hipSuccess &&
               hipMalloc((void **)&h->d_flags, (size_t)h->batch * (nslot + 1)) == hipSuccess;   // + the order bytes
     if (ok && fk != h->kidx)
         ok = hipMalloc(&h->d_clf_scratch, (f64 ? nmpc::ipm_scratch_elems<double>(fk, h->batch, N)
                                                 : nmpc::ipm_scratch_elems<float>(fk, h->batch, N)) * es) == hipSuccess;
     if (!ok) return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_init: lean closed-loop tables");
+    // the park count and claim counter, and the fast kernels' exit counter (after the asynchronous rounds'
+    // counters): 0 between launches (each host-driven launch's last wavefront rezeroes them, report_exit)
+    if (hipMemset(h->d_park, 0, 2 * sizeof(int)) != hipSuccess ||
+        hipMemset(h->d_park + h->batch + 2 + CLF_ROUND_WORDS, 0, sizeof(int)) != hipSuccess)
+        return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_init: counters");
     if (!f64) {
         const int r = ensure_w64(h);
         if (r < 0) return r;
@@ -2366,6 +2387,11 @@ int clf_run(nmpc_solver *h, int steps, bool async)
         }
     }
     int *d_rc = h->d_park + 2 + h->batch;   // asynchronous runs: the rounds' [park count, claim counter] pairs
+    // host-driven rounds: the fast kernel's last wavefront stores the park count into the pinned word (report_exit,
+    // nmpc_cl_fast.hip), so the round's wait needs no copy behind the kernel (env NMPC_CLF_PARK_COPY=1: the copy)
+    static const bool park_copy = std::getenv("NMPC_CLF_PARK_COPY") && std::getenv("NMPC_CLF_PARK_COPY")[0] == '1';
+    static const bool noise_kernel = std::getenv("NMPC_CLF_NOISE_KERNEL") && std::getenv("NMPC_CLF_NOISE_KERNEL")[0] == '1';
+    volatile int *park_word = h->h_park;
     // env NMPC_CLF_CYCLES=<file> with a timing build (-DNMPC_CLF_TIMING): per-instance phase cycles of the
     // run, [B][CLF_NT_HOST] uint64, appended to <file> (tools/clf_phases.py)
     static const char *cyc_path = std::getenv("NMPC_CLF_CYCLES");
@@ -2375,10 +2401,20 @@ int clf_run(nmpc_solver *h, int steps, bool async)
     for (int done = 0; done < steps;) {
         const int n = std::min(CLF_CHUNK, steps - done), target = h->cl_step + n;
         nmpc::ClParams<T> cp = cl_params<T>(h);
-        // (the noise kernel also zeroes the park count and claim counter of the chunk's first round)
-        hipError_t e = nmpc::cl_noise_launch<T>(cp, h->cl_step, n, h->d_fnoise, h->stream, h->d_park);
-        if (e != hipSuccess) return hip_fail(h, e, "closed-loop noise");
         nmpc::ClFastParams<T> fp = clf_params<T>(h, target, h->cl_step, n);
+        // host-driven rounds with per-workgroup claims: the first round's kernel draws the chunk's noise itself
+        // (gen_noise) and the previous launch left the counters zero (report_exit); otherwise the noise kernel,
+        // which also zeroes the park count and claim counter of the chunk's first round (env
+        // NMPC_CLF_NOISE_KERNEL=1: always)
+        const bool gen = !async && !park_copy && !noise_kernel && !fp.claim_global;
+        hipError_t e = hipSuccess;
+        if (!gen && (e = nmpc::cl_noise_launch<T>(cp, h->cl_step, n, h->d_fnoise, h->stream, h->d_park)) != hipSuccess)
+            return hip_fail(h, e, "closed-loop noise");
+        fp.seed = cp.seed;
+        fp.inst_base = cp.inst_base;
+        fp.noise_std = cp.noise_std;
+        fp.noise_table = cp.noise_table;
+        fp.noise_len = cp.noise_len;
         fp.cycles = d_cyc;
         fp.check = h->d_clf_check;
         if (iter_log && h->d_iter_log) {
@@ -2395,6 +2431,10 @@ int clf_run(nmpc_solver *h, int steps, bool async)
                 return hip_fail(h, e, "park reset");
             fp.park_count = async ? d_rc + 2 * round : h->d_park;
             fp.run_if = async && round > 0 ? d_rc + 2 * (round - 1) : nullptr;
+            fp.park_host = async || park_copy ? nullptr : h->h_park;
+            fp.noise_gen = gen && round == 0 ? h->d_fnoise : nullptr;
+            fp.exit_count = (unsigned *)(h->d_park + h->batch + 2 + CLF_ROUND_WORDS);
+            if (fp.park_host) park_word[0] = -1;   // (no copy into the word is pending: host-driven rounds wait)
             hipEvent_t ea = cl_event(h, 2 * launches), eb = cl_event(h, 2 * launches + 1);
             if (!ea || !eb) return h->fail(NMPC_EDEVICE, "nmpc_closed_loop_run: hipEventCreate");
             e = hipEventRecord(ea, h->stream);
@@ -2412,10 +2452,11 @@ int clf_run(nmpc_solver *h, int steps, bool async)
                 if (r < 0) return r;
                 continue;
             }
-            e = hipMemcpyAsync(h->h_park, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+            if (!fp.park_host) e = hipMemcpyAsync(h->h_park, h->d_park, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess) e = stream_wait(h->stream);
             if (e != hipSuccess) return hip_fail(h, e, "lean closed loop (fast kernel)");
-            const int parked = h->h_park[0];
+            const int parked = park_word[0];
+            if (parked < 0) return h->fail(NMPC_EDEVICE, "lean closed loop: the fast kernel did not report its park count");
             if (h->d_clf_check) {
                 unsigned bad = 0;
                 if ((e = hipMemcpy(&bad, h->d_clf_check, sizeof(bad), hipMemcpyDeviceToHost)) != hipSuccess)

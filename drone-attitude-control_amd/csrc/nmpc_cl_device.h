@@ -45,6 +45,17 @@ __device__ __forceinline__ double philox_normal_dev(uint64_t seed, uint64_t inst
     return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
 
+// instance b's noise draw at closed-loop step `step`: the recorded table's value (0 past its end), else
+// noise_std x the Philox normal (cl_noise_kernel, the lean kernels' in-launch draws and cl_advance_instance
+// share it: the same bits on every path)
+__device__ __forceinline__ double noise_draw(uint64_t seed, long long inst_base, double noise_std, const double *table,
+                                             int table_len, int b, int step)
+{
+    if (table) return step < table_len ? table[(size_t)b * table_len + step] : 0.0;
+    if (noise_std > 0) return noise_std * philox_normal_dev(seed, (unsigned long long)(inst_base + b), (unsigned long long)step);
+    return 0.0;
+}
+
 __device__ __forceinline__ void crazyflie_rhs(const double x[4], double st, double ct, double Fd, double inv_m,
                                               double g, double f[4])
 {
@@ -75,12 +86,7 @@ __device__ void cl_advance_instance(const ClParams<T> &p, int b, int step, int s
         cost += (double)p.wcl[i] * e * e;
     }
     for (int i = 0; i < p.aed_dims; i++) aed += fabs((double)xref[i] - (double)st[i]);
-    double w = 0.0;
-    if (p.noise_table) {
-        if (step < p.noise_len) w = p.noise_table[(size_t)b * p.noise_len + step];
-    } else if (p.noise_std > 0) {
-        w = p.noise_std * philox_normal_dev(p.seed, (unsigned long long)(p.inst_base + b), (unsigned long long)step);
-    }
+    const double w = noise_draw(p.seed, p.inst_base, p.noise_std, p.noise_table, p.noise_len, b, step);
     if (p.plant == 0) {
         // controller's own discrete model
         constexpr int NXA = NXC > 0 ? NXC : 32, NUA = NUC > 0 ? NUC : 32;

@@ -1167,18 +1167,42 @@ __device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, const 
         br[j] = bb ? 0.5 * (h - l) : (double)INFINITY;
     }
     const double lb1 = p.lbnd[NZ + i], ub1 = p.ubnd[NZ + i], lb2 = p.lbnd[2 * NZ + i], ub2 = p.ubnd[2 * NZ + i];
+    // the skipped zero terms only matter against an infinite radius (0 x inf): with every radius finite,
+    // fma(0, r, tr) = tr, so the chains run without the per-term selects — the same bits, half the chain
+    // (a select pair per term doubled the radius chain's latency); the wave-uniform test per stage
+    bool binf = false;
+#pragma unroll
+    for (int j = 0; j < NU; j++) binf |= !(br[j] <= DBL_MAX);
+    bool rinf = false;   // (r = 0 at stage 0)
     for (int k = 0; k < p.N; k++) {
         double s = cl[i], tr = 0.0;
+        if (!rinf) {
 #pragma unroll
-        for (int j = 0; j < NX; j++) {
-            const double mj = bcast(m, j), rj = bcast(r, j);
-            s = fma(a[j], mj, s);
-            if (a[j] != 0.0) tr = fma(fabs(a[j]), rj, tr);
+            for (int j = 0; j < NX; j++) {
+                const double mj = bcast(m, j), rj = bcast(r, j);
+                s = fma(a[j], mj, s);
+                tr = fma(fabs(a[j]), rj, tr);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NX; j++) {
+                const double mj = bcast(m, j), rj = bcast(r, j);
+                s = fma(a[j], mj, s);
+                if (a[j] != 0.0) tr = fma(fabs(a[j]), rj, tr);
+            }
         }
+        if (!binf) {
 #pragma unroll
-        for (int j = 0; j < NU; j++) {
-            s = fma(bu[j], bm[j], s);
-            if (bu[j] != 0.0) tr = fma(fabs(bu[j]), br[j], tr);
+            for (int j = 0; j < NU; j++) {
+                s = fma(bu[j], bm[j], s);
+                tr = fma(fabs(bu[j]), br[j], tr);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NU; j++) {
+                s = fma(bu[j], bm[j], s);
+                if (bu[j] != 0.0) tr = fma(fabs(bu[j]), br[j], tr);
+            }
         }
         const bool last = k + 1 == p.N;
         const double lb = last ? lb2 : lb1, ub = last ? ub2 : ub1;
@@ -1191,6 +1215,7 @@ __device__ bool certificate_infeasible(const ClFastParams<T> &p, LdsT &L, const 
         const bool fin = isfinite(lo) && isfinite(hi);
         m = fin ? 0.5 * (lo + hi) : s;
         r = fin ? 0.5 * (hi - lo) : tr;
+        rinf = __any(lane < NX && !(r <= DBL_MAX));   // (NaN too: the selecting chain)
     }
     return false;
 }
@@ -1631,6 +1656,46 @@ __device__ inline void claim_order(unsigned short *ord, const unsigned char *har
     }
 }
 
+// The host-driven rounds' park count without a copy behind the kernel (a blit launch on the stream, ≈5 µs
+// per round): every wavefront counts itself out at the kernel's end; the last one reads the count and
+// stores it to the pinned host word (a system-scope store, written through), then rezeroes the exit counter
+// for the next launch (stream order). No fences: a wavefront's park atomic returned (its list position was
+// used) before its exit atomic is issued, the atomics are performed at the device's coherence point, and the
+// list entries themselves are read by the next kernel only (an agent-scope release here would write back the
+// XCD's L2 at every wavefront's exit: jerk 358M -> 325M). Every wavefront reaches the kernels' ends (no early
+// exit but the asynchronous rounds' run_if, which have no host word).
+template <typename T>
+__device__ __forceinline__ void report_exit(const ClFastParams<T> &p, int lane)
+{
+    if (!p.park_host) return;
+    if (lane == 0) {
+        const unsigned total = gridDim.x * (blockDim.x >> 6);
+        if (__hip_atomic_fetch_add(p.exit_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1u) {
+            const int v = __hip_atomic_load(p.park_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.park_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the next launch's park count and claim counter (the parked list stays for the list-mode solve,
+            // whose length the host passes)
+            __hip_atomic_store(p.park_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.park_count + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.exit_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// The launch's noise draws of the workgroup's own instances (per-workgroup claim ranges), written before the
+// workgroup's first barrier, so its wavefronts read them as they read the noise kernel's (the chunk's noise
+// kernel and its launch gap, ≈12 µs per host-driven round, saved; noise_draw: the same bits)
+template <typename T>
+__device__ __forceinline__ void gen_noise(const ClFastParams<T> &p, int wg_lo, int wg_hi)
+{
+    const int ld = p.noise_ld, cnt = (wg_hi - wg_lo) * ld;
+    for (int q = threadIdx.x; q < cnt; q += blockDim.x) {
+        const int r = q / ld, s = q - r * ld;
+        const int b = p.inst_map ? p.inst_map[wg_lo + r] : wg_lo + r;
+        p.noise_gen[(size_t)b * ld + s] = noise_draw(p.seed, p.inst_base, p.noise_std, p.noise_table, p.noise_len, b, p.step0 + s);
+    }
+}
+
 // WPB wavefronts per workgroup (the slot tables in LDS are shared by them), MW the occupancy target
 // (waves per SIMD; 0: none)
 template <typename T, int NX, int NU, int EPL, int WSM, int WPB, int MW, class SP, bool WL = false, bool SW2 = false>
@@ -1711,6 +1776,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // range fits the order table
     const bool ordered = !p.claim_global && p.demoted && wg_hi - wg_lo <= LOCK_QCAP;
     if (ordered && wave == 0) claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
+    if (p.noise_gen && !p.claim_global) gen_noise(p, wg_lo, wg_hi);
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane, wtri, WL};
 
@@ -1756,6 +1822,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             for (int j = 0; j < EPL; j++) z[j] += z1[j];
         }, wcp);
     }
+    report_exit(p, lane);
 }
 
 
@@ -2041,6 +2108,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // beginning, not behind the lockstep ones), then the rest, each group in instance order. Only the
     // schedule changes: an instance runs lockstep until its first rare step wherever it is claimed
     if (wave == 0) claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
+    if (p.noise_gen) gen_noise(p, wg_lo, wg_hi);
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
     const int n = lane & 3, ti = lane >> 4, tb = (lane >> 2) & 3;   // instance slot; D-layout slot offset
@@ -2424,6 +2492,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
             CLF_SYNC();
         }, wcp);
     }
+    report_exit(p, lane);
 }
 
 }  // namespace clf

@@ -71,13 +71,7 @@ __global__ __launch_bounds__(256) void cl_noise_kernel(ClParams<T> p, int step0,
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
          idx += (size_t)gridDim.x * blockDim.x) {
         const int b = (int)(idx / nsteps), step = step0 + (int)(idx % nsteps);
-        double w = 0.0;
-        if (p.noise_table) {
-            if (step < p.noise_len) w = p.noise_table[(size_t)b * p.noise_len + step];
-        } else if (p.noise_std > 0) {
-            w = p.noise_std * philox_normal_dev(p.seed, (unsigned long long)(p.inst_base + b), (unsigned long long)step);
-        }
-        out[idx] = w;
+        out[idx] = noise_draw(p.seed, p.inst_base, p.noise_std, p.noise_table, p.noise_len, b, step);
     }
 }
 

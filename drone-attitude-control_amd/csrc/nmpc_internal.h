@@ -156,6 +156,17 @@ struct ClFastParams {
     int *park_count, *park_list;  // instances that need a full solve (list mode of ipm_lpc_kernel)
     const int *run_if;            // or null: the launch runs only if *run_if != 0 (the lean loop's asynchronous rounds:
                                   // the previous round's park count), else every workgroup returns at entry
+    int *park_host;               // or null: the launch's last wavefront to exit writes the park count here (pinned
+                                  // host word; the host-driven rounds read it after the stream wait, no copy)
+    unsigned *exit_count;         // ... counting the exited wavefronts (device word, 0 between launches)
+    // or null: each workgroup first writes its instances' noise draws of the launch's steps here ([B][noise_ld],
+    // the buffer `noise` reads; per-workgroup claims only) — the chunk's noise kernel launch saved
+    double *noise_gen;
+    unsigned long long seed;
+    long long inst_base;
+    double noise_std;
+    const double *noise_table;
+    int noise_len;
     int *iter_log;                // optional [steps][B]: active-set steps (<= 255) | status << 8 | wall-clock ticks (<= 32767) << 16
     unsigned long long *cycles;   // diagnostic builds (NMPC_CLF_TIMING): [B][14] phase cycles / counts per instance
     unsigned *check;              // checked builds (NMPC_CLF_CHECK): bit mask of the failed index checks
