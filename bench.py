@@ -338,14 +338,9 @@ def main():
     # set solves and acceptance), so its CPU counterpart is the fp64 oracle loop with the exact finish
     lean = info["closed_loop_kernel"] != "fused"
 
-    # CPU baseline and the B=1 Python drop-in loop first (rank 0, single-GPU runs only)
-    cpu, flops_cpu, pyloop = None, None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, flops_cpu = cpu_baseline(model, N, table, offsets_r, x_r, args.warmup, args.repeats * args.steps,
-                                      args.cpu_seconds, "fp64" if lean else args.precision, args.seed)
-        if args.python_loop_steps > 0:
-            pyloop = python_loop_rate(20, args.python_loop_steps)
-            cpu["python_loop"] = pyloop
+    # (the CPU baseline runs after the timed regions: ahead of them it left the GPU idle for its 10-30 s and the
+    # first regions ran while the clocks ramped up — 0.38 ms against 0.25-0.30 ms, profiles/r7/evidence_r7z2)
+    x_cpu = np.array(x_r, copy=True)
 
     def barrier():
         if dist is not None:
@@ -367,6 +362,14 @@ def main():
     regions = np.array(regions)
     st = cl.stats()
     red = np.array([st["cost_sum"], st["aed_sum"], st["failed"], st["instance_steps"]])
+    # CPU baseline and the B=1 Python drop-in loop (rank 0, single-GPU runs only), from the same initial states
+    cpu, flops_cpu, pyloop = None, None, None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, flops_cpu = cpu_baseline(model, N, table, offsets_r, x_cpu, args.warmup, args.repeats * args.steps,
+                                      args.cpu_seconds, "fp64" if lean else args.precision, args.seed)
+        if args.python_loop_steps > 0:
+            pyloop = python_loop_rate(20, args.python_loop_steps)
+            cpu["python_loop"] = pyloop
     # one SUM of the statistics and one MAX of the timings over RCCL, after the timed regions
     red, regions, kernel_ms_r = reduce_run(dist, red, regions, np.array(kernel_ms_r),
                                            device="cuda" if dist is not None and args.dist_backend == "nccl" else None)
@@ -502,38 +505,41 @@ def main_solve(args, world, rank, dist, device):
     info = s.launch_info()
     fast = info["solve_kernel"] == "sf_kernel"
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import cref, models
-        ref = cref.RiccatiIpmRef.for_options(models.MODELS[model](N), ocp.solver_options, args.precision)
+    # the CPU baseline (after the timed regions: ahead of them the idle GPU's clocks ramp down)
+    def cpu_part():
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle import cref, models
+            ref = cref.RiccatiIpmRef.for_options(models.MODELS[model](N), ocp.solver_options, args.precision)
 
-        def run(n, threads):
-            if fast:   # the same algorithm (riccati_ipm_solve_batch_fast); its tables are built once, untimed
-                ref.solve_fast(x0[:1], Y[:1], wsmax=cref.WSMAX[model], nthreads=1)
-                t0 = time.perf_counter()
-                _, _, st_c, it_c, cnt = ref.solve_fast(x0[:n], Y[:n], wsmax=cref.WSMAX[model], nthreads=threads)
-            else:
-                t0 = time.perf_counter()
-                _, _, st_c, it_c = ref.solve(x0[:n], Y[:n], nthreads=threads)
-                cnt = None
-            return time.perf_counter() - t0, st_c, it_c, cnt
+            def run(n, threads):
+                if fast:   # the same algorithm (riccati_ipm_solve_batch_fast); its tables are built once, untimed
+                    ref.solve_fast(x0[:1], Y[:1], wsmax=cref.WSMAX[model], nthreads=1)
+                    t0 = time.perf_counter()
+                    _, _, st_c, it_c, cnt = ref.solve_fast(x0[:n], Y[:n], wsmax=cref.WSMAX[model], nthreads=threads)
+                else:
+                    t0 = time.perf_counter()
+                    _, _, st_c, it_c = ref.solve(x0[:n], Y[:n], nthreads=threads)
+                    cnt = None
+                return time.perf_counter() - t0, st_c, it_c, cnt
 
-        n0 = min(B, 256)
-        el0 = run(n0, ref.max_threads())[0]
-        n = int(min(B, max(n0, n0 / max(el0, 1e-6) * args.cpu_seconds)))
-        el, st_c, it_c, cnt = run(n, ref.max_threads())
-        n1 = min(n, 128)
-        e1 = run(n1, 1)[0]
-        algo = ("riccati_ipm_solve_batch_fast (the GPU's algorithm: unconstrained solution on the shared "
-                "factorisation, active-set steps on W, the dual fallback, the full IPM + exact finish for what is "
-                "left; fp64)" if fast else "riccati_ipm_solve_batch (the same cold IPM + exact finish, fp64)")
-        cpu = {"value": n / el, "unit": "QP solves/s", "cores": ref.max_threads(), "kind": "port",
-               "sample": f"{n} of the {B} QPs in {el:.2f} s: oracle/c/riccati_ipm.c {algo}, OpenMP over instances",
-               "mean_newton_systems": float(np.mean(it_c)), "failed": int((st_c != 0).sum()),
-               "single_core": {"value": n1 / e1, "cores": 1, "sample": f"{n1} QPs in {e1:.2f} s"}}
-        if cnt:
-            cpu["paths"] = {k: cnt[k] / max(1.0, cnt["solves"]) for k in ("unconstrained", "set", "full", "failed")}
-            cpu["flops_per_qp"] = cnt["flops"] / max(1.0, cnt["solves"])
+            n0 = min(B, 256)
+            el0 = run(n0, ref.max_threads())[0]
+            n = int(min(B, max(n0, n0 / max(el0, 1e-6) * args.cpu_seconds)))
+            el, st_c, it_c, cnt = run(n, ref.max_threads())
+            n1 = min(n, 128)
+            e1 = run(n1, 1)[0]
+            algo = ("riccati_ipm_solve_batch_fast (the GPU's algorithm: unconstrained solution on the shared "
+                    "factorisation, active-set steps on W, the dual fallback, the full IPM + exact finish for what is "
+                    "left; fp64)" if fast else "riccati_ipm_solve_batch (the same cold IPM + exact finish, fp64)")
+            cpu = {"value": n / el, "unit": "QP solves/s", "cores": ref.max_threads(), "kind": "port",
+                   "sample": f"{n} of the {B} QPs in {el:.2f} s: oracle/c/riccati_ipm.c {algo}, OpenMP over instances",
+                   "mean_newton_systems": float(np.mean(it_c)), "failed": int((st_c != 0).sum()),
+                   "single_core": {"value": n1 / e1, "cores": 1, "sample": f"{n1} QPs in {e1:.2f} s"}}
+            if cnt:
+                cpu["paths"] = {k: cnt[k] / max(1.0, cnt["solves"]) for k in ("unconstrained", "set", "full", "failed")}
+                cpu["flops_per_qp"] = cnt["flops"] / max(1.0, cnt["solves"])
+        return cpu
 
     def barrier():
         if dist is not None:
@@ -554,6 +560,7 @@ def main_solve(args, world, rank, dist, device):
         regions.append(t1 - t0)
         kms.append(s.get_stats("time_tot") * 1e3)   # the region's last launch (HIP events)
     s.solve()                                   # one synchronous solve: outputs, status and qp_iter to the host
+    cpu = cpu_part()
     counts = ({"listed": s.get_stats("fast_listed"), "parked": s.get_stats("fast_parked"),
                "note": "the final solve's instances listed for fin64_kernel / parked for the list-mode IPM; every timed "
                        "solve is complete in stream order (the three launches read their list lengths on the device)"}

@@ -2287,12 +2287,15 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     const char *nogi = std::getenv("NMPC_CLF_NO_GI");
     p.gi = (nogi && nogi[0] == '1') ? 0 : 1;
     const char *lw = std::getenv("NMPC_LOCK_WORKERS");
-    // one wavefront per workgroup starts in phase 2 (drains demoted instances while the others still run
-    // lockstep): quad13 B = 8192 415M (0) -> 458-463M (1), 452-457M (2), 405-412M (3) steps/s (tools/lock_ab.sh, ab1/ab2)
+    // wavefronts per workgroup that start in phase 2 (drain demoted instances while the others still run
+    // lockstep). Round 4: quad13 B = 8192 415M (0) -> 458-463M (1), 452-457M (2), 405-412M (3) steps/s
+    // (tools/lock_ab.sh, ab1/ab2). Round 6, after the warm start at the horizon's end, the fallback's start and
+    // the XCD map shortened the lockstep phase: 503-506M (0), 551-573M (1), 578-591M (2), 581-590M (3)
+    // (profiles/r7/ab_lock_workers.jsonl, ab_lock_workers_run2_summary.txt), so two
     // (the jerk shape's lockstep variant, four wavefronts per workgroup and rarely a demotion: none)
     // (at most the variant's wavefronts per workgroup minus one, so some wavefront runs phase 1: quad13 8, jerk 4)
     const int lock_wpb = (h->nx == 6 && h->nu == 2) ? 4 : 8;
-    p.lock_workers = lw ? std::max(0, std::min(lock_wpb - 1, std::atoi(lw))) : (h->nx == 6 && h->nu == 2 ? 0 : 1);
+    p.lock_workers = lw ? std::max(0, std::min(lock_wpb - 1, std::atoi(lw))) : (h->nx == 6 && h->nu == 2 ? 0 : 2);
     const char *lp = std::getenv("NMPC_LOCK_PRIO");
     p.lock_prio = lp ? (lp[0] == '1') : 1;
     // the force shape claims its instances device-wide (env NMPC_CLF_GCLAIM=0 / 1 overrides)
