@@ -5,7 +5,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-ev}
 OUT=gpurun_out/ev_$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
-for cfg in ${CFGS:-"quad13:--model quad13" "force1024:--model force --batch 1024" "force8192f32:--model force --batch 8192 --precision fp32" "jerk:--model jerk --batch 4096" "quad13f32:--model quad13 --precision fp32"}; do
+# CFGS: ";"-separated name:args pairs (default: the five configs)
+IFS=';' read -ra CS <<< "${CFGS:-quad13:--model quad13;force1024:--model force --batch 1024;force8192f32:--model force --batch 8192 --precision fp32;jerk:--model jerk --batch 4096;quad13f32:--model quad13 --precision fp32}"
+for cfg in "${CS[@]}"; do
   name=${cfg%%:*}; args=${cfg#*:}
   echo "[pmc] $name"
   j=0
