@@ -2392,8 +2392,9 @@ int clf_run(nmpc_solver *h, int steps, bool async)
     int *d_rc = h->d_park + 2 + h->batch;   // asynchronous runs: the rounds' [park count, claim counter] pairs
     // host-driven rounds: the fast kernel's last wavefront stores the park count into the pinned word (report_exit,
     // nmpc_cl_fast.hip), so the round's wait needs no copy behind the kernel (env NMPC_CLF_PARK_COPY=1: the copy)
-    static const bool park_copy = std::getenv("NMPC_CLF_PARK_COPY") && std::getenv("NMPC_CLF_PARK_COPY")[0] == '1';
-    static const bool noise_kernel = std::getenv("NMPC_CLF_NOISE_KERNEL") && std::getenv("NMPC_CLF_NOISE_KERNEL")[0] == '1';
+    // (read per run: tests/test_gpu_bench_parity.py compares the paths in one process)
+    const bool park_copy = std::getenv("NMPC_CLF_PARK_COPY") && std::getenv("NMPC_CLF_PARK_COPY")[0] == '1';
+    const bool noise_kernel = std::getenv("NMPC_CLF_NOISE_KERNEL") && std::getenv("NMPC_CLF_NOISE_KERNEL")[0] == '1';
     volatile int *park_word = h->h_park;
     // env NMPC_CLF_CYCLES=<file> with a timing build (-DNMPC_CLF_TIMING): per-instance phase cycles of the
     // run, [B][CLF_NT_HOST] uint64, appended to <file> (tools/clf_phases.py)

@@ -199,6 +199,52 @@ def test_claim_order_changes_only_the_schedule(model, N, B):
     assert p0 == p1
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("model,N,B,no_gi,gclaim", [("quad13", 20, 4096, "0", None), ("jerk", 40, 2048, "0", None),
+                                                   ("force", 20, 2048, "1", None), ("force", 20, 2048, "1", "0")])
+def test_host_round_paths_agree(model, N, B, no_gi, gclaim, monkeypatch):
+    """The host-driven round's two forms: the default — the lean kernel draws the chunk's noise
+    itself (gen_noise) and its last wavefront stores the park count into the pinned word (report_exit) — and
+    the noise kernel + a copy of the count (NMPC_CLF_NOISE_KERNEL=1, NMPC_CLF_PARK_COPY=1), with one or two
+    early phase-2 wavefronts (NMPC_LOCK_WORKERS; schedule only). With NMPC_CLF_NO_GI=1 steps park, so the
+    host reads nonzero park counts (force, whose saturating inputs need the fallback); force's device-wide claim
+    keeps the noise kernel, so its per-workgroup claim (NMPC_CLF_GCLAIM=0) is the case where the list-mode solves
+    read the kernel-drawn noise. Five launches each: states, per-instance sums and parked counts bit for bit (with
+    parks: counts exact, states and sums to 1e-12 — the parked solves' list order is not deterministic)."""
+    from drone_attitude_control_amd.batched import ClosedLoop
+    monkeypatch.setenv("NMPC_CLF_NO_GI", no_gi)
+    if gclaim is not None:
+        monkeypatch.setenv("NMPC_CLF_GCLAIM", gclaim)
+    arms = [{}, {"NMPC_CLF_NOISE_KERNEL": "1", "NMPC_CLF_PARK_COPY": "1"}, {"NMPC_LOCK_WORKERS": "1"}]
+    out = []
+    for env in arms:
+        for k in ("NMPC_CLF_NOISE_KERNEL", "NMPC_CLF_PARK_COPY", "NMPC_LOCK_WORKERS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        cl = ClosedLoop(model, B, N=N, seed=5)
+        parked = 0
+        for n in (3, 20, 20, 20, 20):
+            cl.run(n)
+            parked += cl.stats()["parked"]
+        out.append((cl.state(), cl.instance_stats(), parked))
+    x0, a0, p0 = out[0]
+    if no_gi == "1":
+        assert p0 > 0
+    for x1, a1, p1 in out[1:]:
+        assert p0 == p1
+        if no_gi == "1":
+            # the parked steps' full solves: the park list is filled by atomics, and the list-mode kernel picks a
+            # wavefront's finish path over all the instances it holds (ipm_lpc_kernel: refine_back when every
+            # group refines), so a parked instance's solution depends on its list neighbours to rounding
+            np.testing.assert_allclose(x1, x0, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(a1[:, :2], a0[:, :2], rtol=1e-12, atol=1e-12)
+            assert np.array_equal(a1[:, 2:], a0[:, 2:])
+        else:
+            assert np.array_equal(x0, x1), np.abs(x0 - x1).max()
+            assert np.array_equal(a0, a1), np.abs(a0 - a1).max()
+
+
 TOL_CL32 = 1e-5        # fp32 lean loop, force (BASELINE config 3), DESIGN.md §6 (measured 1.4e-6)
 TOL_CL32_LOOP = 1e-3   # fp32 lean loop, quad13 / jerk: a few loop-sensitive instances (measured 2.6e-4 / 5.2e-4)
 
