@@ -239,7 +239,8 @@ typedef struct nmpc_closed_loop_desc {
 
 /* bind the closed loop to a solver handle (allocates the table/state/accumulators on the device) */
 int nmpc_closed_loop_init(nmpc_solver *h, const nmpc_closed_loop_desc *d);
-/* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion.
+/* enqueue `steps` closed-loop steps on the handle's stream; sync != 0 waits for completion (polling the
+ * stream: one host core busy for the wait; env NMPC_SPIN_WAIT=0 sleeps in hipStreamSynchronize).
  * Paths (the same results on every one; the choice may change from run to run on one handle):
  *   - the lean loop (nmpc_cl_fast.hip; quad13 / jerk / force shapes, fp64 and fp32 — fp32: fp32 tables
  *     and explicit form, fp64 W, set solves and acceptance — the default): launches of at
