@@ -2324,9 +2324,10 @@ hipEvent_t cl_event(nmpc_solver *h, size_t i)
 }
 
 // `steps` closed-loop steps on the lean loop, in chunks of at most CLF_CHUNK steps: per chunk the noise
-// draws, then rounds of (fast kernel over every instance up to the chunk's target step; the count of
-// parked instances back to the host — the one host wait per round; one full solve + plant step per
-// parked instance, ipm_lpc_kernel in list mode) until none is parked. Returns the number of kernel
+// draws (by the first round's fast kernel itself, or the noise kernel), then rounds of (fast kernel over every
+// instance up to the chunk's target step; the count of parked instances to the pinned host word — the one
+// host wait per round; one full solve + plant step per parked instance, ipm_lpc_kernel in list mode) until
+// none is parked. Returns the number of kernel
 // launches (each bracketed by an event pair), or < 0. h->clf_parked / clf_rounds: the run's parked
 // solves and fast launches.
 // async (nmpc_closed_loop_run with sync = 0): no host wait at all — every chunk enqueues all its possible rounds
