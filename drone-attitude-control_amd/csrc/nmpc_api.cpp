@@ -2298,6 +2298,8 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     p.lock_workers = lw ? std::max(0, std::min(lock_wpb - 1, std::atoi(lw))) : (h->nx == 6 && h->nu == 2 ? 0 : 2);
     const char *lp = std::getenv("NMPC_LOCK_PRIO");
     p.lock_prio = lp ? (lp[0] == '1') : 1;
+    const char *ld = std::getenv("NMPC_LOCK_DIRECT");
+    p.lock_direct = ld ? (ld[0] == '1') : 1;
     // the force shape claims its instances device-wide (env NMPC_CLF_GCLAIM=0 / 1 overrides)
     const char *gc = std::getenv("NMPC_CLF_GCLAIM");
     p.claim_global = gc ? (gc[0] == '1') : (h->nx == 4 && h->nu == 2);
@@ -2523,7 +2525,8 @@ int clf_resync(nmpc_solver *h)
     std::vector<int> st((size_t)h->batch, h->cl_step);
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e == hipSuccess) e = hipMemcpy(h->d_istep, st.data(), st.size() * sizeof(int), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * h->clf_nslot);
+    // (the order bytes too: bit 7 promises a nonempty warm set, which the lockstep kernel routes to phase 2)
+    if (e == hipSuccess) e = hipMemset(h->d_flags, 0, (size_t)h->batch * (h->clf_nslot + 1));
     return e == hipSuccess ? 0 : hip_fail(h, e, "lean closed loop resync");
 }
 

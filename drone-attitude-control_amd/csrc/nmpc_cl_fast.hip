@@ -1636,13 +1636,14 @@ constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host ch
 // steps (capped). Groups: bit 7 set, then any rare-path steps, then the rest (buckets = 1: each of the
 // first two split by the rare-path steps, >= 8 / 1-7 / 0 and >= 8 / 1-7); instance order within a group
 // (hard null: instance order)
-__device__ inline void claim_order(unsigned short *ord, const unsigned char *hard, const int *map, int lo, int cnt, int lane,
-                                   int buckets)
+// Returns how many of the ordered instances lead with a nonempty warm start (bit 7).
+__device__ inline int claim_order(unsigned short *ord, const unsigned char *hard, const int *map, int lo, int cnt, int lane,
+                                  int buckets)
 {
     const unsigned long long lt = (1ull << lane) - 1ull;
     constexpr int MN[2][6] = {{128, 1, 0, 0, 0, 0}, {136, 129, 128, 8, 1, 0}}, MX[2][6] = {{255, 127, 0, 0, 0, 0}, {255, 135, 128, 127, 7, 0}};
     const int nb = hard ? (buckets ? 6 : 3) : 1;
-    int pos = 0;
+    int pos = 0, warm = 0;
     for (int b = 0; b < nb; b++) {
         const int mn = nb == 1 ? 0 : MN[buckets ? 1 : 0][b], mx = nb == 1 ? 255 : MX[buckets ? 1 : 0][b];
         for (int c = 0; c < cnt; c += 64) {
@@ -1653,7 +1654,9 @@ __device__ inline void claim_order(unsigned short *ord, const unsigned char *har
             if (d) ord[pos + __popcll(m & lt)] = (unsigned short)(c + lane);
             pos += __popcll(m);
         }
+        if (nb > 1 && mn >= 128) warm = pos;
     }
+    return warm;
 }
 
 // The host-driven rounds' park count without a copy behind the kernel (a blit launch on the stream, ≈5 µs
@@ -2107,7 +2110,24 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // claim order: the instances the previous launch demoted first (the launch's longest chains start at its
     // beginning, not behind the lockstep ones), then the rest, each group in instance order. Only the
     // schedule changes: an instance runs lockstep until its first rare step wherever it is claimed
-    if (wave == 0) claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
+    // The instances that start from a nonempty warm set take the rare path at their first step: lockstep would
+    // demote them at once (slow = ... || flany), so they go straight to the phase-2 queue, where the early
+    // workers start their chains at the launch's beginning (env NMPC_LOCK_DIRECT=0: through lockstep). The same
+    // steps on the same path (the record is read by run_instance either way).
+    if (wave == 0) {
+        const int warm = claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
+        if (p.lock_direct && p.lock_workers > 0 && warm > 0) {
+            for (int q = lane; q < warm; q += 64) {
+                int inst_ = wg_lo + (int)ord[q];
+                if (p.inst_map) inst_ = p.inst_map[inst_];
+                dq[q] = inst_;
+            }
+            if (lane == 0) {
+                dq_tail = warm;
+                wg_next = warm;
+            }
+        }
+    }
     if (p.noise_gen) gen_noise(p, wg_lo, wg_hi);
     __syncthreads();
     const SlotView<EPL> sv{slb, sub, slo, shi, sol, sou, sse, ssrc, lane};
