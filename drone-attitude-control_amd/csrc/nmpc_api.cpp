@@ -2299,7 +2299,7 @@ nmpc::ClFastParams<T> clf_params(nmpc_solver *h, int target, int step0, int nois
     const char *lp = std::getenv("NMPC_LOCK_PRIO");
     p.lock_prio = lp ? (lp[0] == '1') : 1;
     const char *ld = std::getenv("NMPC_LOCK_DIRECT");
-    p.lock_direct = ld ? (ld[0] == '1') : 1;
+    p.lock_direct = ld ? std::max(0, std::min(6, std::atoi(ld))) : 1;
     // the force shape claims its instances device-wide (env NMPC_CLF_GCLAIM=0 / 1 overrides)
     const char *gc = std::getenv("NMPC_CLF_GCLAIM");
     p.claim_global = gc ? (gc[0] == '1') : (h->nx == 4 && h->nu == 2);

@@ -1636,9 +1636,9 @@ constexpr int LOCK_QCAP = 512;   // demoted instances per workgroup (the host ch
 // steps (capped). Groups: bit 7 set, then any rare-path steps, then the rest (buckets = 1: each of the
 // first two split by the rare-path steps, >= 8 / 1-7 / 0 and >= 8 / 1-7); instance order within a group
 // (hard null: instance order)
-// Returns how many of the ordered instances lead with a nonempty warm start (bit 7).
+// Returns how many of the ordered instances fall in the first `lead` groups (0 without the order bytes).
 __device__ inline int claim_order(unsigned short *ord, const unsigned char *hard, const int *map, int lo, int cnt, int lane,
-                                  int buckets)
+                                  int buckets, int lead = 0)
 {
     const unsigned long long lt = (1ull << lane) - 1ull;
     constexpr int MN[2][6] = {{128, 1, 0, 0, 0, 0}, {136, 129, 128, 8, 1, 0}}, MX[2][6] = {{255, 127, 0, 0, 0, 0}, {255, 135, 128, 127, 7, 0}};
@@ -1654,7 +1654,7 @@ __device__ inline int claim_order(unsigned short *ord, const unsigned char *hard
             if (d) ord[pos + __popcll(m & lt)] = (unsigned short)(c + lane);
             pos += __popcll(m);
         }
-        if (nb > 1 && mn >= 128) warm = pos;
+        if (nb > 1 && b < lead) warm = pos;
     }
     return warm;
 }
@@ -2115,8 +2115,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
     // workers start their chains at the launch's beginning (env NMPC_LOCK_DIRECT=0: through lockstep). The same
     // steps on the same path (the record is read by run_instance either way).
     if (wave == 0) {
-        const int warm = claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets);
-        if (p.lock_direct && p.lock_workers > 0 && warm > 0) {
+        // (lock_direct = the leading claim-order groups routed: 1 = the warm-started ones, the default; more
+        // groups also route instances with rare-path steps in the previous launch — a tuning experiment)
+        const int warm = claim_order(ord, p.demoted, p.inst_map, wg_lo, wg_hi - wg_lo, lane, p.order_buckets,
+                                     p.lock_workers > 0 ? p.lock_direct : 0);
+        if (warm > 0) {
             for (int q = lane; q < warm; q += 64) {
                 int inst_ = wg_lo + (int)ord[q];
                 if (p.inst_map) inst_ = p.inst_map[inst_];

@@ -121,7 +121,7 @@ struct ClFastParams {
     int gi;                       // 1: the dual active-set fallback runs; 0 (test knob): such steps park
     int lock_workers;             // lockstep kernel: wavefronts per workgroup that start in phase 2
     int lock_prio;                // lockstep kernel: phase-2 wavefronts at raised issue priority
-    int lock_direct;              // lockstep kernel: warm-started instances straight to the phase-2 queue
+    int lock_direct;              // lockstep kernel: the leading claim-order groups straight to the phase-2 queue (1: warm-started)
     int claim_global;             // cl_fast_kernel: instances from one device-wide counter (park_count[1])
     int wcache;                   // 1: the rare path's W column cache in LDS (quad13 / jerk shapes; env NMPC_CLF_WCACHE=0: off)
     const int *inst_map;          // or null: position -> instance of the per-workgroup claim ranges (nmpc_api.cpp
