@@ -469,6 +469,15 @@ def main():
             "closed_loop": {"mean_cost_per_step": red[0] / max(1.0, red[3]),
                             "aed": red[1] / max(1.0, red[3]) / (2 if model != "quad13" else 3),
                             "failed_solves": int(red[2]), "instance_steps": int(red[3])},
+            "parity": {"checked_against": (
+                "the builder's CPU oracle only (oracle/c/riccati_ipm.c closed loop: mode 0 exact KKT-certified QP "
+                "solutions, mode 1 this engine's algorithm): quad13 is a synthetic model the reference does not "
+                "have (SURVEY.md §0), so no acados run exists for it" if model == "quad13" else
+                "the CPU oracle (oracle/c/riccati_ipm.c) and the reference's own recorded runs "
+                "(tests/test_reference_plots.py: jerk reproduces acados's loop to 3e-7; force explained step by "
+                "step as acados's interior-point termination, DESIGN.md §6)"),
+                "tests": "tests/test_gpu_bench_parity.py: this workload against committed oracle goldens at every "
+                         "region boundary (fp64 1e-6 relative, failure counts exact)"},
         }
         emit(line)
     if dist is not None:
