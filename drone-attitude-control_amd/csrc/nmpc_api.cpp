@@ -261,6 +261,7 @@ struct nmpc_solver {
     signed char *d_flags = nullptr;        // [B][nslot]
     int clf_resident = 0;                  // workgroups of cl_fast_kernel the handle's device holds at once
     int *d_imap = nullptr;                 // the lean loop's position -> instance map (clf_xcd_map), or null
+    int *d_gorder = nullptr;               // the device-wide claim's order (clf_order_launch), [B]
     int clf_kind = 0;                      // nmpc::CLF_FAST / CLF_LOCK (cl_lock_kernel) / CLF_WLDS (W in LDS) / CLF_ONE
     int clf_parked = 0, clf_rounds = 0;    // the last run: parked solves (list-mode full solves), fast launches
     size_t fnoise_cap = 0;                 // capacity of d_fnoise (doubles)
@@ -536,7 +537,8 @@ void free_all(nmpc_solver *h)
                     (void *)h->d_fnoise, (void *)h->d_iter_log, h->d_cltx, h->d_clv, h->d_fsT, (void *)h->d_fsI,
                     (void *)h->d_istep, (void *)h->d_park, (void *)h->d_flags, h->d_clf_scratch, (void *)h->d_clw,
                     (void *)h->d_fin_f, (void *)h->d_fin_i, (void *)h->d_z0, (void *)h->d_sf, (void *)h->d_f64,
-                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch, (void *)h->d_sfcyc, (void *)h->d_clf_check, (void *)h->d_imap})
+                    (void *)h->d_f64i, (void *)h->d_sfl, h->d_sf_scratch, (void *)h->d_sfcyc, (void *)h->d_clf_check, (void *)h->d_imap,
+                    (void *)h->d_gorder})
         if (p) hipFree(p);
     if (h->h_sfpark) hipHostFree(h->h_sfpark);
     if (h->ev_fb) hipEventDestroy(h->ev_fb);
@@ -2417,6 +2419,21 @@ int clf_run(nmpc_solver *h, int steps, bool async)
         hipError_t e = hipSuccess;
         if (!gen && (e = nmpc::cl_noise_launch<T>(cp, h->cl_step, n, h->d_fnoise, h->stream, h->d_park)) != hipSuccess)
             return hip_fail(h, e, "closed-loop noise");
+        // the device-wide claim (the force shape): a batch-wide claim order from the previous launch's order bytes,
+        // the longest chains first (env NMPC_CLF_GORDER=0: instance order)
+        const char *go = std::getenv("NMPC_CLF_GORDER");
+        // (not when every instance has a wavefront of its own: force B = 1024)
+        if (fp.claim_global && fp.demoted && !(go && go[0] == '0') &&
+            !nmpc::cl_fast_fits(h->nx, h->nu, h->clf_sid, h->clf_kind, std::is_same<T, double>::value, h->batch,
+                                h->clf_resident)) {
+            if (!h->d_gorder && hipMalloc((void **)&h->d_gorder, (size_t)h->batch * sizeof(int)) != hipSuccess) {
+                h->d_gorder = nullptr;
+                return h->fail(NMPC_ENOMEM, "nmpc_closed_loop_run: claim order");
+            }
+            if ((e = nmpc::clf_order_launch(fp.demoted, h->batch, h->d_gorder, h->stream)) != hipSuccess)
+                return hip_fail(h, e, "claim order");
+            fp.gorder = h->d_gorder;
+        }
         fp.seed = cp.seed;
         fp.inst_base = cp.inst_base;
         fp.noise_std = cp.noise_std;

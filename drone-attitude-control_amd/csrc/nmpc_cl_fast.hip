@@ -1801,7 +1801,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MW > 0
         next = __builtin_amdgcn_readfirstlane(next);
         if (wg_lo + next >= wg_hi) break;
         const int pos = wg_lo + (ordered ? (int)ord[next] : next);
-        const int inst = (p.inst_map && !p.claim_global) ? p.inst_map[pos] : pos;
+        const int inst = p.claim_global ? (p.gorder ? p.gorder[pos] : pos) : (p.inst_map ? p.inst_map[pos] : pos);
         // explicit unconstrained solution at the lane's slots: T_x pairs from LDS against x pairs broadcast
         run_instance<T, NX, NU, EPL, WSM, SP>(p, L, sv, lane, abl, cl, inst, [&](T(&z)[EPL], const T(&vt)[EPL]) {
             T z1[EPL];
@@ -2613,6 +2613,19 @@ int cl_fast_resident(int nx, int nu, int sid, int kind, bool f64, int device)
 }
 
 // grid: min(workgroups for one wavefront per instance, the resident workgroups)
+bool cl_fast_fits(int nx, int nu, int sid, int kind, bool f64, int waves, int resident)
+{
+    bool fits = false;
+    auto g = [&](auto v) {
+        using V = decltype(v);
+        const int wv = kind == CLF_LOCK ? (waves + 3) / 4 : waves;
+        fits = std::min((wv + V::WPB - 1) / V::WPB, resident) * V::WPB >= wv;
+    };
+    if (f64) clf_dispatch<double>(nx, nu, sid, kind, g);
+    else clf_dispatch<float>(nx, nu, sid, kind, g);
+    return fits;
+}
+
 int cl_fast_grid(int nx, int nu, int sid, int kind, bool f64, int waves, int resident)
 {
     int blocks = 0;
@@ -2641,6 +2654,61 @@ hipError_t cl_fast_launch(int nx, int nu, int sid, int kind, const ClFastParams<
 }
 
 template hipError_t cl_fast_launch<double>(int, int, int, int, const ClFastParams<double> &, int, int, hipStream_t);
+
+namespace clf {
+// one workgroup of 1024 threads: each thread a contiguous run of instances; per group the runs' counts, their
+// exclusive scan over the workgroup (wavefront scans by shuffles, then the wavefront totals), then every thread
+// writes its run's instances at its offsets — the same order as claim_order's three groups, batch-wide
+__global__ __launch_bounds__(1024) void clf_order_kernel(const unsigned char *hard, int B, int *gorder)
+{
+    __shared__ int wtot[16][3];
+    __shared__ int gbase[3];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int per = (B + 1023) / 1024, b0 = min(B, t * per), b1 = min(B, b0 + per);
+    int c[3] = {0, 0, 0};
+    for (int b = b0; b < b1; b++) {
+        const int h = hard[b];
+        c[h >= 128 ? 0 : (h > 0 ? 1 : 2)]++;
+    }
+    int x[3];
+#pragma unroll
+    for (int g = 0; g < 3; g++) {
+        int v = c[g];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(v, o);
+            if (lane >= o) v += u;
+        }
+        x[g] = v - c[g];   // exclusive within the wavefront
+        if (lane == 63) wtot[wv][g] = v;
+    }
+    __syncthreads();
+    if (t < 3) {   // the wavefront totals' scan and the groups' bases
+        int acc = 0;
+        for (int w = 0; w < 16; w++) {
+            const int v = wtot[w][t];
+            wtot[w][t] = acc;
+            acc += v;
+        }
+        gbase[t] = acc;   // (the group's total for now)
+    }
+    __syncthreads();
+    const int base[3] = {0, gbase[0], gbase[0] + gbase[1]};
+    int pos[3];
+#pragma unroll
+    for (int g = 0; g < 3; g++) pos[g] = base[g] + wtot[wv][g] + x[g];
+    for (int b = b0; b < b1; b++) {
+        const int h = hard[b], g = h >= 128 ? 0 : (h > 0 ? 1 : 2);
+        gorder[pos[g]++] = b;
+    }
+}
+}  // namespace clf
+
+hipError_t clf_order_launch(const unsigned char *hard, int B, int *gorder, hipStream_t s)
+{
+    NMPC_LAUNCH(clf::clf_order_kernel, dim3(1), dim3(1024), 0, s, hard, B, gorder);
+    return hipGetLastError();
+}
 
 hipError_t fin32_z0_launch(const Fin32Z0Params &p, hipStream_t s)
 {

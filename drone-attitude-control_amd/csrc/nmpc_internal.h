@@ -124,6 +124,7 @@ struct ClFastParams {
     int lock_direct;              // lockstep kernel: the leading claim-order groups straight to the phase-2 queue (1: warm-started)
     int claim_global;             // cl_fast_kernel: instances from one device-wide counter (park_count[1])
     int wcache;                   // 1: the rare path's W column cache in LDS (quad13 / jerk shapes; env NMPC_CLF_WCACHE=0: off)
+    const int *gorder;            // or null: claim position -> instance of the device-wide claim (clf_order_launch)
     const int *inst_map;          // or null: position -> instance of the per-workgroup claim ranges (nmpc_api.cpp
                                   // clf_xcd_map: each XCD's workgroups own a contiguous stretch of reference-table rows)
     unsigned char *demoted;       // [B] the previous launch's rare-path steps | 128 if its last solution left bounds
@@ -237,10 +238,15 @@ constexpr int CLF_FAST = 0, CLF_LOCK = 1, CLF_WLDS = 2, CLF_ONE = 3;
 int cl_fast_resident(int nx, int nu, int sid, int kind, bool f64, int device);
 // the lean-loop launch's workgroup count for `waves` (instances) and `resident` (cl_fast_launch's grid)
 int cl_fast_grid(int nx, int nu, int sid, int kind, bool f64, int waves, int resident);
+// every instance has its own wavefront from the launch's start (no claim order can matter)
+bool cl_fast_fits(int nx, int nu, int sid, int kind, bool f64, int waves, int resident);
 // grid = min(waves / wavefronts per workgroup, resident); waves = instances (lock: instances / 4)
 template <typename T>
 hipError_t cl_fast_launch(int nx, int nu, int sid, int kind, const ClFastParams<T> &p, int waves, int resident,
                           hipStream_t s);
+// the device-wide claim's order for the next launch: the instances whose last solution left bounds active, then those
+// with rare-path steps in the previous launch, then the rest, each group in instance order (one workgroup)
+hipError_t clf_order_launch(const unsigned char *hard, int B, int *gorder, hipStream_t s);
 
 size_t scratch_elems_per_instance(int N, int nx, int nu);
 

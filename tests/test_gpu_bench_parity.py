@@ -207,7 +207,8 @@ def test_host_round_paths_agree(model, N, B, no_gi, gclaim, monkeypatch):
     itself (gen_noise) and its last wavefront stores the park count into the pinned word (report_exit) — and
     the noise kernel + a copy of the count (NMPC_CLF_NOISE_KERNEL=1, NMPC_CLF_PARK_COPY=1), with one or two
     early phase-2 wavefronts (NMPC_LOCK_WORKERS) and with the warm-started instances through lockstep instead of
-    straight to phase 2 (NMPC_LOCK_DIRECT=0) — schedule only. With NMPC_CLF_NO_GI=1 steps park, so the
+    straight to phase 2 (NMPC_LOCK_DIRECT=0), and force's device-wide claim in instance order instead of the
+    batch-wide claim order (NMPC_CLF_GORDER=0) — schedule only. With NMPC_CLF_NO_GI=1 steps park, so the
     host reads nonzero park counts (force, whose saturating inputs need the fallback); force's device-wide claim
     keeps the noise kernel, so its per-workgroup claim (NMPC_CLF_GCLAIM=0) is the case where the list-mode solves
     read the kernel-drawn noise. Five launches each: states, per-instance sums and parked counts bit for bit (with
@@ -217,10 +218,10 @@ def test_host_round_paths_agree(model, N, B, no_gi, gclaim, monkeypatch):
     if gclaim is not None:
         monkeypatch.setenv("NMPC_CLF_GCLAIM", gclaim)
     arms = [{}, {"NMPC_CLF_NOISE_KERNEL": "1", "NMPC_CLF_PARK_COPY": "1"}, {"NMPC_LOCK_WORKERS": "1"},
-            {"NMPC_LOCK_DIRECT": "0"}]
+            {"NMPC_LOCK_DIRECT": "0"}, {"NMPC_CLF_GORDER": "0"}]
     out = []
     for env in arms:
-        for k in ("NMPC_CLF_NOISE_KERNEL", "NMPC_CLF_PARK_COPY", "NMPC_LOCK_WORKERS", "NMPC_LOCK_DIRECT"):
+        for k in ("NMPC_CLF_NOISE_KERNEL", "NMPC_CLF_PARK_COPY", "NMPC_LOCK_WORKERS", "NMPC_LOCK_DIRECT", "NMPC_CLF_GORDER"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
